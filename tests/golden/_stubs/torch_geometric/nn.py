@@ -1,0 +1,21 @@
+"""Stub of ``torch_geometric.nn``: GATConv = the oracle's PyG 1.7.2 restatement."""
+import torch
+
+from oracle.gat import GATConv as _OracleGATConv
+
+
+class GATConv(_OracleGATConv):
+    def forward(self, x, edge_index):
+        st = edge_index.storage
+        return super().forward(x, (st.rowptr(), st.col()))
+
+
+class MessagePassing(torch.nn.Module):
+    def __init__(self, aggr="add", **kwargs):
+        super().__init__()
+        self.aggr = aggr
+
+
+class GCNConv(torch.nn.Module):
+    def __init__(self, *a, **k):
+        raise NotImplementedError("GCNConv is out of scope")

@@ -1,0 +1,144 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE's own code.
+
+Run in the build container only (the reference tree does not exist on the GPU box):
+
+    python tests/golden/make_golden.py /root/reference
+
+It imports the reference ``utils.py`` / ``models.py`` (``/root/reference``) with the stand-ins in
+``tests/golden/_stubs`` for the absent ``torch_geometric`` / ``torch_sparse`` packages and records:
+
+* ``graph_<case>.npz``  -- ``utils.convert_to_matrix`` (utils.py:10-26), ``utils.load_input``
+  (utils.py:29-73: networkx edge list, masked self loops, symmetric CSR) and ``utils.cont2dist``
+  (utils.py:75-80) at factors 0.5 and 1.0, for GM12878 chr19 1mb / 500kb (``Data/*.txt``) and a
+  synthetic 3-column list with duplicates, gaps and asymmetric entries.
+* ``model_<name>.npz``  -- a reference model class (``models.py:614-691`` / ``:1010-1047``) built
+  under ``torch.manual_seed(0)`` on chr19 1mb with 0.1*N(0,1) features: initial state_dict,
+  forward distance matrix, coordinates, MSE vs cont2dist(y, 0.5), every parameter gradient, and the
+  combined-loss value of ``HiC_GAT_generalize_directly.py:206-225``.
+* ``train_<name>.npz``  -- the ``HiC-GNN_main.py:117-132`` loop run for a fixed K on the same input
+  (deterministic algorithms), loss history and final coordinates.
+
+Only data is written (inputs and expected outputs); no reference source is copied.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+from scipy.stats import pearsonr
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+
+def _import_reference(ref):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(HERE, "_stubs"))
+    sys.path.insert(0, ref)
+    import models as ref_models  # noqa: E402  (reference models.py)
+    import utils as ref_utils    # noqa: E402  (reference utils.py)
+    return ref_utils, ref_models
+
+
+def graph_case(ref_utils, name, lst):
+    mat = ref_utils.convert_to_matrix(lst)
+    n = mat.shape[0]
+    rng = np.random.default_rng(1)
+    feats = (0.1 * rng.standard_normal((n, 512))).astype(np.float32)
+    data = ref_utils.load_input(mat.copy(), feats)
+    st = data.edge_index.storage
+    out = dict(
+        list=lst, matrix=mat,
+        rowptr=st.rowptr().numpy(), col=st.col().numpy(), value=st.value().numpy(),
+        y=data.y.numpy(),
+        truth05=ref_utils.cont2dist(data.y.clone(), 0.5).numpy(),
+        truth1=ref_utils.cont2dist(data.y.clone(), 1).numpy(),
+    )
+    np.savez_compressed(os.path.join(HERE, f"graph_{name}.npz"), **out)
+    print(f"graph_{name}: N={n} nnz={len(out['col'])}")
+    return mat, data
+
+
+def synth_list(seed=7):
+    """Ragged 3-column Hi-C list: gaps in the bin ids, repeated pairs, lower-triangle and
+    asymmetric entries, an isolated bin whose row ends up all zero (and is removed)."""
+    rng = np.random.default_rng(seed)
+    bins = np.sort(rng.choice(np.arange(0, 400) * 50000, size=256, replace=False))
+    rows = []
+    for _ in range(3000):
+        i, j = rng.integers(0, 256, size=2)
+        if rng.random() < 0.8:
+            i, j = min(i, j), max(i, j)
+        rows.append((bins[i], bins[j], float(rng.integers(1, 500))))
+    rows.append((bins[3], bins[3], 77.0))                 # a pure self contact
+    rows.extend(rows[:40])                                 # repeats (last write wins)
+    return np.array(rows, dtype=np.float64)
+
+
+def model_case(ref_utils, ref_models, cls_name, data, seed=0):
+    torch.manual_seed(seed)
+    model = getattr(ref_models, cls_name)()
+    x = data.x.float()
+    truth = ref_utils.cont2dist(data.y.clone(), 0.5)
+    state = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    model.zero_grad()
+    out = model(x, data.edge_index)
+    coords = model.get_model(x, data.edge_index)
+    mse = torch.nn.MSELoss()(out.float(), truth.float())
+    mse.backward()
+    grads = {f"grad::{k}": p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
+    n = truth.shape[0]
+    idx = torch.triu_indices(n, n, offset=1)
+    r = pearsonr(truth[idx[0], idx[1]].numpy(), torch.cdist(coords, coords)[idx[0], idx[1]].detach().numpy())[0]
+    alpha = min(1.0, 0.1 + (1.0 / (mse.item() + 1e-6)))
+    total = mse.item() + alpha * (1 - r)
+    np.savez_compressed(
+        os.path.join(HERE, f"model_{cls_name}.npz"),
+        x=x.numpy(), truth=truth.float().numpy(), out=out.detach().numpy(), coords=coords.detach().numpy(),
+        mse=np.float64(mse.item()), pearson=np.float64(r), alpha=np.float64(alpha), total=np.float64(total),
+        **{f"state::{k}": v for k, v in state.items()}, **grads)
+    print(f"model_{cls_name}: mse={mse.item():.8g} r={r:.8g}")
+    return model
+
+
+def train_case(ref_utils, ref_models, cls_name, data, steps=25, seed=0):
+    torch.use_deterministic_algorithms(True)
+    torch.manual_seed(seed)
+    model = getattr(ref_models, cls_name)()
+    x = data.x.float()
+    truth = ref_utils.cont2dist(data.y.clone(), 0.5)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    crit = torch.nn.MSELoss()
+    hist = []
+    oldloss = 1
+    for _ in range(steps):                    # HiC-GNN_main.py:123-132 with a fixed K
+        model.train()
+        opt.zero_grad()
+        out = model(x, data.edge_index)
+        loss = crit(out.float(), truth.float())
+        _ = abs(oldloss - loss)
+        loss.backward()
+        opt.step()
+        oldloss = loss
+        hist.append(loss.item())
+    coords = model.get_model(x, data.edge_index).detach().numpy()
+    np.savez_compressed(os.path.join(HERE, f"train_{cls_name}.npz"), loss=np.array(hist),
+                        coords=coords, steps=np.int64(steps))
+    print(f"train_{cls_name}: loss {hist[0]:.6g} -> {hist[-1]:.6g}")
+
+
+def main(ref):
+    torch.set_num_threads(1)
+    ref_utils, ref_models = _import_reference(ref)
+    l1 = np.loadtxt(os.path.join(ref, "Data", "GM12878_1mb_chr19_list.txt"))
+    l5 = np.loadtxt(os.path.join(ref, "Data", "GM12878_500kb_chr19_list.txt"))
+    _, data1 = graph_case(ref_utils, "chr19_1mb", l1)
+    graph_case(ref_utils, "chr19_500kb", l5)
+    graph_case(ref_utils, "synth256", synth_list())
+    for cls in ("GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2"):
+        model_case(ref_utils, ref_models, cls, data1)
+    train_case(ref_utils, ref_models, "GATNetSelectiveResidualsUpdated", data1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
