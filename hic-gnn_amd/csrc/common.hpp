@@ -1,0 +1,91 @@
+// Shared device helpers for the gfx950 kernels of libhicgat.so (wave64 everywhere).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hicgat.h"
+
+namespace hicgat {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Wave index inside the block, forced into an SGPR so that everything derived from it is scalar.
+__device__ __forceinline__ int wave_in_block() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+// Sum over the 32 lanes of each half wave.
+__device__ __forceinline__ float half_wave_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// torch.nn.functional.leaky_relu: x > 0 ? x : x * slope.
+__device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
+
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 acc) {
+  acc.x = fmaf(a, x.x, acc.x);
+  acc.y = fmaf(a, x.y, acc.y);
+  acc.z = fmaf(a, x.z, acc.z);
+  acc.w = fmaf(a, x.w, acc.w);
+  return acc;
+}
+__device__ __forceinline__ float f4_dot(float4 a, float4 b) {
+  return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+}
+
+// "Transpose reduce": every lane holds V values; after the call lane l holds, in v[0], the sum
+// over all 64 lanes of value index idx(l) where the bits of idx are taken, most significant
+// first, from lane bits 5, 4, ... (V = 16: idx = (l>>5&1)*8 + (l>>4&1)*4 + (l>>3&1)*2 + (l>>2&1)).
+// Cost: V-1 shuffles + 2 for the final intra-group sum (vs 6 per value for independent sums).
+template <int V>
+__device__ __forceinline__ void transpose_reduce(float (&v)[V], int lane) {
+  static_assert(V == 16 || V == 8, "transpose_reduce: V must be 8 or 16");
+  int mask = 32;
+#pragma unroll
+  for (int n = V; n > 1; n >>= 1, mask >>= 1) {
+    const bool upper = (lane & mask) != 0;
+#pragma unroll
+    for (int q = 0; q < n / 2; ++q) {
+      const float send = upper ? v[q] : v[q + n / 2];
+      const float keep = upper ? v[q + n / 2] : v[q];
+      v[q] = keep + __shfl_xor(send, mask);
+    }
+  }
+  // remaining lane bits below `mask*2` are still partial: finish the sum across them
+#pragma unroll
+  for (int o = mask; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o);
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md section 5 T1): the 8 XCDs each get a
+// contiguous range of logical blocks, so rows that share neighbours share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+}  // namespace hicgat
+
+#define HICGAT_CHECK_LAUNCH()                                   \
+  do {                                                          \
+    if (hipGetLastError() != hipSuccess) return HICGAT_ELAUNCH; \
+  } while (0)

@@ -1,0 +1,276 @@
+// GATConv backward on gfx950 (autograd of a4+a5 in the reference: segment_csr/gather_csr/
+// index_select/leaky_relu/exp backward of PyG 1.7.2), without float atomics.
+//
+// With out_i = sum_j alpha_ij h_j (+bias) and alpha the ptr-path softmax of
+// e_ij = lrelu(a_src[j] + a_dst[i]):
+//   g_ij   = <dout_i, h_j>                   (per head)
+//   de_ij  = alpha_ij (g_ij - delta_i),      delta_i = sum_j alpha_ij g_ij
+//   ds_ij  = de_ij * lrelu'(e_ij)
+//   da_dst[i] = sum_j ds_ij,  da_src[j] = sum_i ds_ij,  dh_j = sum_i alpha_ij dout_i (+ logit terms)
+// (the +1e-16 of the softmax denominator and the detached-max gradient change these by
+// O(1e-16) relative; both are dropped.)
+//
+// Pass 1 (dst side, row i) gathers h_j; pass 2 (src side, row r) gathers dout_i of the rows that
+// have r as a neighbour.  The graph is structurally symmetric (to_symmetric, utils.py:71), so
+// row r's own CSR list *is* that set: the transpose needs no permutation array and no atomics.
+// The per-edge dot products are reduced 8 neighbours x 2 heads at a time with one 17-shuffle
+// transpose reduce instead of 16 independent 6-step wave sums.
+#include "common.hpp"
+
+namespace hicgat {
+
+__global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
+    const int *__restrict__ rowptr, const int *__restrict__ col, int N, const float *__restrict__ h,
+    const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ rmax, const float *__restrict__ rsum,
+    const float *__restrict__ dout, float ns, float *__restrict__ delta,
+    float *__restrict__ da_dst) {
+  constexpr int U = 8;
+  const int lane = lane_id();
+  const int i = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (i >= N) return;
+  const int beg = rowptr[i], end = rowptr[i + 1];
+  const float4 *h4 = reinterpret_cast<const float4 *>(h);
+  const float4 *g4 = reinterpret_cast<const float4 *>(dout);
+  const float4 d0 = g4[(size_t)i * 128 + lane], d1 = g4[(size_t)i * 128 + 64 + lane];
+  // after transpose_reduce<16> with values [head*8 + k], lane owns (head hh, neighbour slot kk)
+  const int hh = lane >> 5, kk = (lane >> 2) & 7;
+  const bool owner = (lane & 3) == 0;
+  const float adh = a_dst[2 * (size_t)i + hh];
+  const float mh = rmax[2 * (size_t)i + hh];
+  const float denh = rsum[2 * (size_t)i + hh] + 1e-16f;
+  float S1 = 0.f, S2 = 0.f, S3 = 0.f;
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    const int j = e < end ? col[e] : i;
+    const int cnt = min(64, end - base);
+    for (int k = 0; k < cnt; k += U) {
+      float4 v0[U], v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t jj = (size_t)readlane_i(j, k + u);
+        v0[u] = h4[jj * 128 + lane];
+        v1[u] = h4[jj * 128 + 64 + lane];
+      }
+      float v[2 * U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = f4_dot(d0, v0[u]);
+        v[U + u] = f4_dot(d1, v1[u]);
+      }
+      transpose_reduce<2 * U>(v, lane);
+      const int jn = __shfl(j, k + kk);
+      const float eh = a_src[2 * (size_t)jn + hh] + adh;
+      const float lp = eh > 0.f ? 1.f : ns;
+      const float al = expf(lrelu(eh, ns) - mh) / denh;
+      if (owner && k + kk < cnt) {
+        S1 = fmaf(al, v[0], S1);
+        S2 = fmaf(al * lp, v[0], S2);
+        S3 = fmaf(al, lp, S3);
+      }
+    }
+  }
+  S1 = half_wave_sum(S1);
+  S2 = half_wave_sum(S2);
+  S3 = half_wave_sum(S3);
+  if ((lane & 31) == 0) {
+    delta[2 * (size_t)i + hh] = S1;
+    da_dst[2 * (size_t)i + hh] = S2 - S1 * S3;
+  }
+}
+
+__global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
+    const int *__restrict__ rowptr, const int *__restrict__ col, int N, const float *__restrict__ h,
+    const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ rmax, const float *__restrict__ rsum,
+    const float *__restrict__ delta, const float *__restrict__ da_dst,
+    const float *__restrict__ dout, const float *__restrict__ att_s,
+    const float *__restrict__ att_d, float ns, float *__restrict__ dh,
+    float *__restrict__ da_src) {
+  constexpr int U = 8;
+  const int lane = lane_id();
+  const int r = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (r >= N) return;
+  const int beg = rowptr[r], end = rowptr[r + 1];
+  const float4 *h4 = reinterpret_cast<const float4 *>(h);
+  const float4 *g4 = reinterpret_cast<const float4 *>(dout);
+  const float4 hr0 = h4[(size_t)r * 128 + lane], hr1 = h4[(size_t)r * 128 + 64 + lane];
+  const float2 asr = *reinterpret_cast<const float2 *>(a_src + 2 * (size_t)r);
+  const float2 *ad2 = reinterpret_cast<const float2 *>(a_dst);
+  const float2 *mx2 = reinterpret_cast<const float2 *>(rmax);
+  const float2 *sm2 = reinterpret_cast<const float2 *>(rsum);
+  const float2 *dl2 = reinterpret_cast<const float2 *>(delta);
+  const int hh = lane >> 5, kk = (lane >> 2) & 7;
+  const bool owner = (lane & 3) == 0;
+  float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
+  float Sda = 0.f;
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    int inb = r;
+    float al0 = 0.f, al1 = 0.f, A0 = 0.f, A1 = 0.f, B0 = 0.f, B1 = 0.f;
+    if (e < end) {
+      inb = col[e];
+      const float2 ad = ad2[inb], mx = mx2[inb], sm = sm2[inb], dl = dl2[inb];
+      const float e0 = asr.x + ad.x, e1 = asr.y + ad.y;
+      al0 = expf(lrelu(e0, ns) - mx.x) / (sm.x + 1e-16f);
+      al1 = expf(lrelu(e1, ns) - mx.y) / (sm.y + 1e-16f);
+      A0 = al0 * (e0 > 0.f ? 1.f : ns);
+      A1 = al1 * (e1 > 0.f ? 1.f : ns);
+      B0 = A0 * dl.x;
+      B1 = A1 * dl.y;
+    }
+    const int cnt = min(64, end - base);
+    for (int k = 0; k < cnt; k += U) {
+      float4 g0[U], g1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t ii = (size_t)readlane_i(inb, k + u);
+        g0[u] = g4[ii * 128 + lane];
+        g1[u] = g4[ii * 128 + 64 + lane];
+      }
+      float v[2 * U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc0 = f4_fma(readlane_f(al0, k + u), g0[u], acc0);
+        acc1 = f4_fma(readlane_f(al1, k + u), g1[u], acc1);
+        v[u] = f4_dot(g0[u], hr0);
+        v[U + u] = f4_dot(g1[u], hr1);
+      }
+      transpose_reduce<2 * U>(v, lane);
+      const int src = k + kk;
+      const float a0 = __shfl(A0, src), a1 = __shfl(A1, src);
+      const float b0 = __shfl(B0, src), b1 = __shfl(B1, src);
+      if (owner && src < cnt) Sda += hh ? fmaf(a1, v[0], -b1) : fmaf(a0, v[0], -b0);
+    }
+  }
+  Sda = half_wave_sum(Sda);
+  const float ds0 = readlane_f(Sda, 0), ds1 = readlane_f(Sda, 32);
+  const float2 dd = *reinterpret_cast<const float2 *>(da_dst + 2 * (size_t)r);
+  const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
+  const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
+  const float4 as0 = s4[lane], as1 = s4[64 + lane], at0 = t4[lane], at1 = t4[64 + lane];
+  acc0 = f4_fma(ds0, as0, acc0);
+  acc0 = f4_fma(dd.x, at0, acc0);
+  acc1 = f4_fma(ds1, as1, acc1);
+  acc1 = f4_fma(dd.y, at1, acc1);
+  float4 *o4 = reinterpret_cast<float4 *>(dh);
+  o4[(size_t)r * 128 + lane] = acc0;
+  o4[(size_t)r * 128 + 64 + lane] = acc1;
+  if (lane == 0) {
+    da_src[2 * (size_t)r] = ds0;
+    da_src[2 * (size_t)r + 1] = ds1;
+  }
+}
+
+// ---- GATConv parameter gradients: deterministic two-stage column reductions over N rows. ------
+// stage 1: block b sums rows [b*R, (b+1)*R) into part[b][3][D] (datt_src, datt_dst, dbias);
+// stage 2: one thread per output column sums the partials in block order.
+constexpr int kParamBlocks = 512;
+
+__global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
+                                                         const float *__restrict__ dout,
+                                                         const float *__restrict__ da_src,
+                                                         const float *__restrict__ da_dst, int N,
+                                                         int H, int C, int rows_per_block,
+                                                         float *__restrict__ part) {
+  const int D = H * C, Q = D / 4;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(N, r0 + rows_per_block);
+  const float4 *h4 = reinterpret_cast<const float4 *>(h);
+  const float4 *g4 = reinterpret_cast<const float4 *>(dout);
+  float4 *p4 = reinterpret_cast<float4 *>(part + (size_t)blockIdx.x * 3 * D);
+  for (int q = threadIdx.x; q < Q; q += blockDim.x) {
+    const int hd = (4 * q) / C;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), t = s, b = s;
+    for (int n = r0; n < r1; ++n) {
+      const float4 hv = h4[(size_t)n * Q + q], gv = g4[(size_t)n * Q + q];
+      s = f4_fma(da_src[(size_t)n * H + hd], hv, s);
+      t = f4_fma(da_dst[(size_t)n * H + hd], hv, t);
+      b.x += gv.x; b.y += gv.y; b.z += gv.z; b.w += gv.w;
+    }
+    p4[q] = s;
+    p4[Q + q] = t;
+    p4[2 * Q + q] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict__ part, int nblk,
+                                                         int D, float *__restrict__ datt_s,
+                                                         float *__restrict__ datt_d,
+                                                         float *__restrict__ dbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 3 * D) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * 3 * D + c];
+  const int which = c / D, cc = c % D;
+  (which == 0 ? datt_s : which == 1 ? datt_d : dbias)[cc] = s;
+}
+
+}  // namespace hicgat
+
+using namespace hicgat;
+
+extern "C" int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int H,
+                                      int C, const float *h, const float *a_src,
+                                      const float *a_dst, const float *row_max,
+                                      const float *row_sum, const float *dout, float neg_slope,
+                                      float *delta, float *da_dst, hicgat_stream_t stream) {
+  if (N < 0) return HICGAT_EINVAL;
+  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (N == 0) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !row_max || !row_sum || !dout || !delta || !da_dst)
+    return HICGAT_EINVAL;
+  hipLaunchKernelGGL(agg_bwd_dst_h2c256_kernel, dim3((N + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, N, h, a_src, a_dst, row_max, row_sum, dout,
+                     neg_slope, delta, da_dst);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H,
+                                      int C, const float *h, const float *a_src,
+                                      const float *a_dst, const float *row_max,
+                                      const float *row_sum, const float *delta,
+                                      const float *da_dst, const float *dout,
+                                      const float *att_src, const float *att_dst,
+                                      float neg_slope, float *dh, float *da_src,
+                                      hicgat_stream_t stream) {
+  if (N < 0) return HICGAT_EINVAL;
+  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (N == 0) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !row_max || !row_sum || !delta || !da_dst ||
+      !dout || !att_src || !att_dst || !dh || !da_src)
+    return HICGAT_EINVAL;
+  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((N + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, N, h, a_src, a_dst, row_max, row_sum, delta,
+                     da_dst, dout, att_src, att_dst, neg_slope, dh, da_src);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" size_t hicgat_gat_param_grad_workspace_bytes(int N, int D) {
+  (void)N;
+  return (size_t)kParamBlocks * 3 * (size_t)(D > 0 ? D : 0) * sizeof(float);
+}
+
+extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
+                                     const float *da_dst, int N, int H, int C, float *datt_src,
+                                     float *datt_dst, float *dbias, void *workspace,
+                                     size_t workspace_bytes, hicgat_stream_t stream) {
+  if (N < 0 || H <= 0 || C <= 0 || (C % 4) != 0) return HICGAT_EINVAL;
+  const int D = H * C;
+  if (!h || !dout || !da_src || !da_dst || !datt_src || !datt_dst || !dbias || !workspace)
+    return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_gat_param_grad_workspace_bytes(N, D)) return HICGAT_EINVAL;
+  const int rpb = N > 0 ? (N + kParamBlocks - 1) / kParamBlocks : 1;
+  const int nblk = N > 0 ? (N + rpb - 1) / rpb : 0;
+  float *part = static_cast<float *>(workspace);
+  if (nblk > 0) {
+    hipLaunchKernelGGL(param_grad_stage1, dim3(nblk), dim3(128), 0, (hipStream_t)stream, h, dout,
+                       da_src, da_dst, N, H, C, rpb, part);
+    HICGAT_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

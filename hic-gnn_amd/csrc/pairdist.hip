@@ -1,0 +1,410 @@
+// All-pairs 3-D distance, MSE + Pearson moments and their gradient on gfx950 (a7, a8, a9).
+//
+// Reference: out = torch.cdist(c, c, p=2) (models.py:661) -> MSELoss()(out, truth)
+// (HiC-GNN_main.py:127) and scipy pearsonr of the triu pairs (HiC_GAT_generalize_directly.py:220).
+// The reference materialises D [N, N] (and its grad) in HBM; the fused kernel here streams the
+// truth matrix once, only its upper-triangle 128x128 tiles, and never stores D.
+//
+// Tile kernel: one 256-thread block per 128x128 tile; thread (ty, tx) in a 16x16 grid owns rows
+// {4ty..4ty+3, 64+4ty..} x cols {4tx..4tx+3, 64+4tx..}, so every T row segment is two coalesced
+// 256 B float4 sweeps.  Per pair it forms d, r = d - t, the moments and w = r/d, and accumulates
+// w*(c_i - c_j) into row partials (reduced over the 16 tx lanes) and column partials (reduced over
+// ty through LDS).  Partials go to a [tile][2][128] float4 slab and a second kernel adds, per row,
+// the slabs of every tile touching it in a fixed order: bitwise reproducible, no float atomics.
+#include "common.hpp"
+
+namespace hicgat {
+
+constexpr int BT = 128;
+enum { MODE_SYM = 0, MODE_FULL = 1 };
+
+__host__ __device__ inline int pd_nb(int N) { return (N + BT - 1) / BT; }
+__host__ __device__ inline int64_t tri_start(int64_t I, int64_t nb) { return I * nb - I * (I - 1) / 2; }
+
+__device__ inline void tri_decode(int64_t t, int nb, int &I, int &J) {
+  const double b = 2.0 * nb + 1.0;
+  int64_t Ii = (int64_t)floor((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
+  if (Ii < 0) Ii = 0;
+  if (Ii > nb - 1) Ii = nb - 1;
+  while (Ii > 0 && tri_start(Ii, nb) > t) --Ii;
+  while (Ii + 1 < nb && tri_start(Ii + 1, nb) <= t) ++Ii;
+  I = (int)Ii;
+  J = (int)(Ii + (t - tri_start(Ii, nb)));
+}
+
+__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes sharing lane>>4
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  const int2 p = *reinterpret_cast<int2 *>(&v);
+  int2 q;
+  q.x = __shfl_xor(p.x, m);
+  q.y = __shfl_xor(p.y, m);
+  return *reinterpret_cast<double *>(&q);
+}
+
+// MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
+// MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restrict__ coords,
+                                                            const float *__restrict__ T, int N,
+                                                            int64_t ldt, int nb, int64_t t0,
+                                                            float4 *__restrict__ part,
+                                                            double *__restrict__ mom) {
+  __shared__ float sc[2][BT][3];
+  __shared__ float4 colred[4][BT];
+  __shared__ double mred[4][6];
+  const int64_t t = t0 + blockIdx.x;
+  int I, J;
+  if (MODE == MODE_SYM) {
+    tri_decode(t, nb, I, J);
+  } else {
+    I = (int)(t / nb);
+    J = (int)(t % nb);
+  }
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, lane = tid & 63, wv = tid >> 6;
+  for (int k = tid; k < 2 * BT; k += 256) {
+    const int which = k / BT, li = k % BT;
+    const int g = (which ? J : I) * BT + li;
+    float x = 0.f, y = 0.f, z = 0.f;
+    if (g < N) {
+      x = coords[3 * (size_t)g];
+      y = coords[3 * (size_t)g + 1];
+      z = coords[3 * (size_t)g + 2];
+    }
+    sc[which][li][0] = x;
+    sc[which][li][1] = y;
+    sc[which][li][2] = z;
+  }
+  __syncthreads();
+
+  float cx[8], cy[8], cz[8], ax[8], ay[8], az[8];
+  int gj[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int lc = tx * 4 + (q & 3) + (q >> 2) * 64;
+    gj[q] = J * BT + lc;
+    cx[q] = sc[1][lc][0];
+    cy[q] = sc[1][lc][1];
+    cz[q] = sc[1][lc][2];
+    ax[q] = ay[q] = az[q] = 0.f;
+  }
+  float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f;
+  float4 *prow = part + (size_t)t * 2 * BT;
+
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
+    const int gi = I * BT + lr;
+    const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
+    float tv[8];
+    if (gi < N) {
+      const float *trow = T + (size_t)gi * ldt + (size_t)J * BT;
+      if (VEC) {
+        const float4 a = *reinterpret_cast<const float4 *>(trow + tx * 4);
+        const float4 b = *reinterpret_cast<const float4 *>(trow + 64 + tx * 4);
+        tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
+        tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tv[q] = 0.f;
+    }
+    float px = 0.f, py = 0.f, pz = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float dx = rx - cx[q], dy = ry - cy[q], dz = rz - cz[q];
+      const float d = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
+      bool valid = gi < N && gj[q] < N;
+      float w;
+      if (MODE == MODE_SYM) {
+        valid = valid && (I != J || gi < gj[q]);
+        const float tt = tv[q], r = d - tt;
+        if (valid) {
+          L = fmaf(r, r, L);
+          sd += d;
+          sdd = fmaf(d, d, sdd);
+          sdt = fmaf(d, tt, sdt);
+          st += tt;
+          stt = fmaf(tt, tt, stt);
+        }
+        w = (valid && d > 0.f) ? r / d : 0.f;
+      } else {
+        valid = valid && gi != gj[q];
+        w = (valid && d > 0.f) ? tv[q] / d : 0.f;
+      }
+      px = fmaf(w, dx, px);
+      py = fmaf(w, dy, py);
+      pz = fmaf(w, dz, pz);
+      ax[q] = fmaf(-w, dx, ax[q]);
+      ay[q] = fmaf(-w, dy, ay[q]);
+      az[q] = fmaf(-w, dz, az[q]);
+    }
+    px = sum16(px);
+    py = sum16(py);
+    pz = sum16(pz);
+    if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
+  }
+  // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ax[q] += __shfl_xor(ax[q], 16);
+    ax[q] += __shfl_xor(ax[q], 32);
+    ay[q] += __shfl_xor(ay[q], 16);
+    ay[q] += __shfl_xor(ay[q], 32);
+    az[q] += __shfl_xor(az[q], 16);
+    az[q] += __shfl_xor(az[q], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) colred[wv][tx * 4 + (q & 3) + (q >> 2) * 64] = make_float4(ax[q], ay[q], az[q], 0.f);
+  }
+  if (MODE == MODE_SYM) {
+    double m[6] = {L, sd, sdd, sdt, st, stt};
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      for (int o = 32; o > 0; o >>= 1) m[c] += shfl_xor_d(m[c], o);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) mred[wv][c] = m[c];
+    }
+  }
+  __syncthreads();
+  if (tid < BT) {
+    float4 s = colred[0][tid];
+#pragma unroll
+    for (int w2 = 1; w2 < 4; ++w2) {
+      const float4 o = colred[w2][tid];
+      s.x += o.x;
+      s.y += o.y;
+      s.z += o.z;
+    }
+    prow[BT + tid] = s;
+  }
+  if (MODE == MODE_SYM && tid < 6) {
+    mom[(size_t)t * 8 + tid] = ((mred[0][tid] + mred[1][tid]) + mred[2][tid]) + mred[3][tid];
+  }
+}
+
+// dcoords[i] = scale * (sum of the row partials of tiles (R, *) + column partials of (*, R)).
+__global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__restrict__ part,
+                                                              int N, int nb, int mode, int64_t t0,
+                                                              int64_t t1, float scale,
+                                                              float *__restrict__ dcoords) {
+  const int gi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= N) return;
+  const int R = gi / BT, lr = gi % BT;
+  float sx = 0.f, sy = 0.f, sz = 0.f;
+  for (int J = 0; J < nb; ++J) {
+    int64_t trow, tcol;
+    if (mode == MODE_SYM) {
+      trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
+      tcol = J <= R ? tri_start(J, nb) + (R - J) : -1;
+    } else {
+      trow = (int64_t)R * nb + J;
+      tcol = (int64_t)J * nb + R;
+    }
+    if (trow >= t0 && trow < t1) {
+      const float4 p = part[(size_t)trow * 2 * BT + lr];
+      sx += p.x; sy += p.y; sz += p.z;
+    }
+    if (tcol >= t0 && tcol < t1) {
+      const float4 p = part[(size_t)tcol * 2 * BT + BT + lr];
+      sx += p.x; sy += p.y; sz += p.z;
+    }
+  }
+  dcoords[3 * (size_t)gi] = sx * scale;
+  dcoords[3 * (size_t)gi + 1] = sy * scale;
+  dcoords[3 * (size_t)gi + 2] = sz * scale;
+}
+
+// stats[0..5] = sum over tiles [t0,t1) of the tile moments (fixed order, fp64).
+__global__ __launch_bounds__(256) void moments_reduce_kernel(const double *__restrict__ mom,
+                                                             int64_t t0, int64_t t1,
+                                                             double *__restrict__ stats) {
+  __shared__ double red[256][6];
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s[c] += mom[(size_t)t * 8 + c];
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) red[threadIdx.x][c] = s[c];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) red[threadIdx.x][c] += red[threadIdx.x + o][c];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) stats[threadIdx.x] = red[0][threadIdx.x];
+}
+
+// stats[6..9] and loss from stats[0..5] (+ the truth diagonal): mse, pearson r, alpha, total.
+__global__ __launch_bounds__(64) void finalize_kernel(const float *__restrict__ T, int N, int64_t ldt,
+                                                      int loss_kind, double *__restrict__ stats,
+                                                      float *__restrict__ loss) {
+  double dg = 0.0;
+  for (int i = threadIdx.x; i < N; i += 64) {
+    const double v = T[(size_t)i * ldt + i];
+    dg += v * v;
+  }
+  for (int o = 32; o > 0; o >>= 1) dg += shfl_xor_d(dg, o);
+  if (threadIdx.x != 0) return;
+  const double n2 = (double)N * (double)N;
+  const double mse = (2.0 * stats[0] + dg) / n2;
+  const double M = 0.5 * (double)N * (double)(N - 1);
+  const double sd = stats[1], sdd = stats[2], sdt = stats[3], st = stats[4], stt = stats[5];
+  const double cov = sdt - sd * st / M, vd = sdd - sd * sd / M, vt = stt - st * st / M;
+  const double r = (vd > 0.0 && vt > 0.0) ? cov / sqrt(vd * vt) : NAN;
+  // HiC_GAT_generalize_directly.py:223-225: alpha from mse_loss.item() (the fp32 value), then
+  // total_loss = mse_loss + alpha*(1-r) evaluated as an fp32 tensor + scalar add.
+  const float msef = (float)mse;
+  const double alpha = fmin(1.0, 0.1 + 1.0 / ((double)msef + 1e-6));
+  const float totalf = msef + (float)(alpha * (1.0 - r));
+  const double total = (double)totalf;
+  stats[6] = mse;
+  stats[7] = r;
+  stats[8] = alpha;
+  stats[9] = total;
+  if (loss) loss[0] = loss_kind == 1 ? totalf : msef;
+}
+
+// D[i, j] = ||c_i - c_j||: one thread per element.
+__global__ __launch_bounds__(256) void pairdist_fwd_kernel(const float *__restrict__ coords, int N,
+                                                           float *__restrict__ D, int64_t ldd) {
+  __shared__ float ci[3];
+  const int i = blockIdx.y;
+  if (threadIdx.x < 3) ci[threadIdx.x] = coords[3 * (size_t)i + threadIdx.x];
+  __syncthreads();
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const float dx = ci[0] - coords[3 * (size_t)j], dy = ci[1] - coords[3 * (size_t)j + 1],
+              dz = ci[2] - coords[3 * (size_t)j + 2];
+  D[(size_t)i * ldd + j] = i == j ? 0.f : sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
+}
+
+}  // namespace hicgat
+
+using namespace hicgat;
+
+extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
+  if (N <= 0) return 0;
+  const int64_t nb = pd_nb(N);
+  return mode == MODE_SYM ? nb * (nb + 1) / 2 : nb * nb;
+}
+
+extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
+  // mode 1 (fused, triangular tiles) and mode 0 (backward, square tiles) of the public API.
+  const int64_t tiles = hicgat_pairdist_num_tiles(N, mode == 1 ? MODE_SYM : MODE_FULL);
+  return (size_t)tiles * (2 * BT * sizeof(float4) + 8 * sizeof(double)) + 256;
+}
+
+static void carve(void *ws, int64_t tiles, float4 **part, double **mom) {
+  char *p = static_cast<char *>(ws);
+  *part = reinterpret_cast<float4 *>(p);
+  *mom = reinterpret_cast<double *>(p + (size_t)tiles * 2 * BT * sizeof(float4));
+}
+
+extern "C" int hicgat_pairdist_fwd(const float *coords, int N, float *D, int64_t ldd,
+                                   hicgat_stream_t stream) {
+  if (N < 0 || ldd < N) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!coords || !D) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(pairdist_fwd_kernel, dim3((N + 255) / 256, N), dim3(256), 0,
+                     (hipStream_t)stream, coords, N, D, ldd);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg,
+                                   float *dcoords, void *workspace, size_t workspace_bytes,
+                                   hicgat_stream_t stream) {
+  if (N < 0 || ldg < N) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!coords || !G || !dcoords || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, 0)) return HICGAT_EINVAL;
+  const int nb = pd_nb(N);
+  const int64_t tiles = (int64_t)nb * nb;
+  float4 *part;
+  double *mom;
+  carve(workspace, tiles, &part, &mom);
+  const bool vec = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) &&
+                   ldg >= (int64_t)nb * BT;
+  if (vec)
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true>), dim3(tiles), dim3(256), 0,
+                       (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
+  else
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false>), dim3(tiles), dim3(256), 0,
+                       (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, part, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
+                     dcoords);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
+                                         int64_t tile_begin, int64_t tile_end, int loss_kind,
+                                         double *stats, float *loss, float *dcoords,
+                                         void *workspace, size_t workspace_bytes,
+                                         hicgat_stream_t stream) {
+  if (N < 0 || ldt < N || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!coords || !T || !stats || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, 1)) return HICGAT_EINVAL;
+  const int nb = pd_nb(N);
+  const int64_t tiles = (int64_t)nb * (nb + 1) / 2;
+  if (tile_end < 0 || tile_end > tiles) tile_end = tiles;
+  if (tile_begin < 0) tile_begin = 0;
+  if (tile_begin > tile_end) return HICGAT_EINVAL;
+  float4 *part;
+  double *mom;
+  carve(workspace, tiles, &part, &mom);
+  const int64_t nt = tile_end - tile_begin;
+  const bool vec = (ldt % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+                   ldt >= (int64_t)nb * BT;
+  if (nt > 0) {
+    if (vec)
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, true>), dim3(nt), dim3(256), 0,
+                         (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom);
+    else
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false>), dim3(nt), dim3(256), 0,
+                         (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom);
+    HICGAT_CHECK_LAUNCH();
+  }
+  if (dcoords) {
+    const float scale = (float)(4.0 / ((double)N * (double)N));
+    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, part, N, nb, (int)MODE_SYM, tile_begin, tile_end,
+                       scale, dcoords);
+    HICGAT_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, mom,
+                     tile_begin, tile_end, stats);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, T, N, ldt,
+                     loss_kind, stats, loss);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_finalize(const float *T, int N, int64_t ldt, int loss_kind,
+                                        double *stats, float *loss, hicgat_stream_t stream) {
+  if (N <= 0 || !T || !stats || ldt < N) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, T, N, ldt,
+                     loss_kind, stats, loss);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

@@ -1,0 +1,97 @@
+"""ctypes binding of libhicgat.so (the C ABI in include/hicgat.h).
+
+The library is built in-tree (``make -C hic-gnn_amd`` or ``__graft_entry__.build()``).  There is
+no fallback: if the library or a GPU is missing every op raises ``HicgatUnavailable``.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhicgat.so")
+
+c_int, c_i64, c_f, c_d, c_sz, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double,
+                                     ctypes.c_size_t, ctypes.c_void_p)
+
+# name -> (restype, argtypes); mirrors include/hicgat.h one to one
+SIGNATURES = {
+    "hicgat_version": (c_int, []),
+    "hicgat_strerror": (ctypes.c_char_p, [c_int]),
+    "hicgat_csr_from_dense": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_sz, c_p]),
+    "hicgat_csr_workspace_bytes": (c_sz, [c_int]),
+    "hicgat_cont2dist": (c_int, [c_p, c_int, c_i64, c_d, c_p, c_p, c_i64, c_p, c_sz, c_p]),
+    "hicgat_cont2dist_workspace_bytes": (c_sz, [c_int]),
+    "hicgat_gat_linear_att": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
+    "hicgat_gat_att_logits": (c_int, [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
+    "hicgat_gat_agg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_f,
+                                   c_p, c_p, c_p, c_p]),
+    "hicgat_gat_agg_bwd_dst": (c_int, [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p,
+                                       c_f, c_p, c_p, c_p]),
+    "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p,
+                                       c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                      c_sz, c_p]),
+    "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),
+    "hicgat_pairdist_fwd": (c_int, [c_p, c_int, c_p, c_i64, c_p]),
+    "hicgat_pairdist_bwd": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p, c_sz, c_p]),
+    "hicgat_pairdist_mse_fused": (c_int, [c_p, c_p, c_int, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_p,
+                                          c_p, c_sz, c_p]),
+    "hicgat_pairdist_finalize": (c_int, [c_p, c_int, c_i64, c_int, c_p, c_p, c_p]),
+    "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
+    "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),
+    "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
+}
+
+
+class HicgatUnavailable(RuntimeError):
+    """libhicgat.so or the GPU it needs is not available (there is deliberately no fallback)."""
+
+
+class HicgatError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libhicgat.so and bind every symbol of include/hicgat.h (no GPU needed for this)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HicgatUnavailable(f"{path} not built: run `make -C hic-gnn_amd` (hipcc, gfx950)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    l = load()
+    if not torch.cuda.is_available():
+        raise HicgatUnavailable("hicgat kernels need an MI355X (torch.cuda.is_available() is False)")
+    return l
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().hicgat_strerror(rc).decode()
+        raise HicgatError(f"{what} failed: {msg} ({rc})")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

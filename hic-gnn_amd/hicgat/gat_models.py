@@ -1,0 +1,79 @@
+"""The in-scope GAT-HiC models on the HIP path, with the reference's forward()/get_model() surface.
+
+* ``GATNetSelectiveResidualsUpdated``       -- models.py:614-691 (flagship, 601 475 parameters).
+* ``GATNetHeadsChanged3LayersLeakyReLUv2``  -- models.py:1010-1047 (411 651 parameters).
+
+Submodules are registered in the reference's order (so the same seed gives the same initial
+weights and the same state_dict keys).  ``forward`` returns the N x N distance matrix like the
+reference (``cdist`` on the GPU); ``get_model`` returns the N x 3 coordinates; ``loss`` is the
+fused path used by the training loop (distance + MSE [+ Pearson] without materialising N x N).
+"""
+import torch
+import torch.nn.functional as F
+from torch.nn import LayerNorm, Linear
+
+from . import ops
+from .nn import GATConv
+
+
+class _CoordsModel(torch.nn.Module):
+    def forward(self, x, edge_index):
+        return ops.pairwise_dist(self.get_model(x, edge_index))
+
+    def loss(self, x, edge_index, truth, kind="mse", tile_range=(0, -1), stats=None):
+        """Fused ``criterion(model(x, ei), truth)``; returns ``(loss, stats, coords)``."""
+        coords = self.get_model(x, edge_index)
+        loss, stats = ops.fused_dist_loss(coords, truth, kind, tile_range, stats)
+        return loss, stats, coords
+
+
+class GATNetSelectiveResidualsUpdated(_CoordsModel):
+    def __init__(self):
+        super().__init__()
+        self.conv = GATConv(512, 256, heads=2, concat=True)
+        self.densea = Linear(512, 256)
+        self.norm_a = LayerNorm(256)
+        self.align_densea = Linear(512, 256)
+        self.dense1 = Linear(256, 128)
+        self.norm1 = LayerNorm(128)
+        self.align_dense1 = Linear(256, 128)
+        self.dense2 = Linear(128, 64)
+        self.norm2 = LayerNorm(64)
+        self.dense3 = Linear(64, 3)
+
+    def tail(self, x):
+        """models.py:637-659 after the GATConv (relu, two residual LayerNorm blocks, 64 -> 3)."""
+        x = F.relu(x)
+        res = self.align_densea(x)
+        x = F.relu(self.norm_a(self.densea(x))) + res
+        res = self.align_dense1(x)
+        x = F.relu(self.norm1(self.dense1(x))) + res
+        x = F.relu(self.norm2(self.dense2(x)))
+        return self.dense3(x)
+
+    def get_model(self, x, edge_index):
+        return self.tail(self.conv(x, edge_index))
+
+
+class GATNetHeadsChanged3LayersLeakyReLUv2(_CoordsModel):
+    def __init__(self):
+        super().__init__()
+        self.conv = GATConv(512, 256, heads=2, concat=True)
+        self.densea = Linear(512, 256)
+        self.dense1 = Linear(256, 64)
+        self.dense2 = Linear(64, 3)
+
+    def tail(self, x):
+        x = F.leaky_relu(x)
+        x = F.leaky_relu(self.densea(x))
+        x = F.leaky_relu(self.dense1(x))
+        return self.dense2(x)
+
+    def get_model(self, x, edge_index):
+        return self.tail(self.conv(x, edge_index))
+
+
+MODELS = {
+    "GATNetSelectiveResidualsUpdated": GATNetSelectiveResidualsUpdated,
+    "GATNetHeadsChanged3LayersLeakyReLUv2": GATNetHeadsChanged3LayersLeakyReLUv2,
+}

@@ -1,0 +1,229 @@
+"""Graph and target construction: the host-side mirror of reference ``utils.py``.
+
+* ``convert_to_matrix``  -- utils.py:10-26 (host, vectorised; the 3-column list is host data).
+* ``Adj``                -- the SparseTensor surface the reference touches (``(row, col, value,
+  sparse_sizes)`` constructor, ``.to_symmetric()``, ``.storage.rowptr()/col()/value()``,
+  utils.py:70-71) plus the device CSR the kernels read: int32, self loops inserted (set_diag).
+* ``load_input``         -- utils.py:29-73: the symmetric CSR is built ON THE DEVICE by
+  ``hicgat_csr_from_dense`` (a13 + a3), bit-exact with the networkx/to_symmetric pattern.
+* ``cont2dist``          -- utils.py:75-80 on the device (``hicgat_cont2dist``, a12).
+* ``Truth``              -- the fp32 target of the fused distance/MSE kernel: padded leading dim
+  (multiple of 128), symmetric.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+TILE = 128
+
+
+def convert_to_matrix(adj):
+    """utils.py:10-26: (bin_i, bin_j, count) list -> dense symmetric matrix, zero rows removed.
+
+    Bins are ranked among the unique ids (``np.argwhere(adj[k,0] == idx)``), later repeats of a
+    pair overwrite earlier ones, ``triu(mat) + tril(mat.T, 1)`` mirrors the upper triangle and
+    every all-zero column (and the same rows) is deleted."""
+    adj = np.asarray(adj, dtype=np.float64)
+    ids = np.unique(np.concatenate((adj[:, 0], adj[:, 1])))
+    mat = np.zeros((len(ids), len(ids)))
+    i = np.searchsorted(ids, adj[:, 0])
+    j = np.searchsorted(ids, adj[:, 1])
+    # last write wins: keep, for every (i, j), the final occurrence in list order
+    key = i * len(ids) + j
+    _, last = np.unique(key[::-1], return_index=True)
+    keep = len(key) - 1 - last
+    mat[i[keep], j[keep]] = adj[keep, 2]
+    mat = np.triu(mat) + np.tril(mat.T, 1)
+    zero = np.argwhere(np.all(mat == 0, axis=0))
+    mat = np.delete(mat, zero, axis=1)
+    return np.delete(mat, zero, axis=0)
+
+
+class _Storage:
+    def __init__(self, rowptr, col, value):
+        self._rowptr, self._col, self._value = rowptr, col, value
+
+    def rowptr(self):
+        return self._rowptr
+
+    def col(self):
+        return self._col
+
+    def value(self):
+        return self._value
+
+
+class Adj:
+    """Symmetric CSR adjacency with a torch_sparse.SparseTensor-like surface.
+
+    ``storage`` holds the reference view (int64, no self loops, row-major sorted/coalesced);
+    ``rowptr32``/``col32`` the device view the kernels read (int32, one self loop per row at its
+    sorted position, i.e. after PyG's ``set_diag``)."""
+
+    def __init__(self, row=None, col=None, value=None, sparse_sizes=None, *, _csr=None):
+        if _csr is not None:
+            rowptr, colv, val, n = _csr
+        else:
+            row = torch.as_tensor(row, dtype=torch.long).cpu()
+            colt = torch.as_tensor(col, dtype=torch.long).cpu()
+            n = int(sparse_sizes[0]) if sparse_sizes is not None else int(max(row.max(), colt.max())) + 1
+            key = row * n + colt
+            order = torch.argsort(key, stable=True)
+            key = key[order]
+            uniq, inverse = torch.unique_consecutive(key, return_inverse=True)
+            val = None
+            if value is not None:
+                v = torch.as_tensor(value)[order]
+                val = torch.zeros(uniq.numel(), dtype=v.dtype).index_add(0, inverse, v)
+            r = uniq // n
+            colv = uniq % n
+            rowptr = torch.zeros(n + 1, dtype=torch.long)
+            rowptr[1:] = torch.cumsum(torch.bincount(r, minlength=n), 0)
+        self.n = n
+        self.storage = _Storage(rowptr, colv, val)
+        self.rowptr32 = None
+        self.col32 = None
+
+    def sparse_sizes(self):
+        return (self.n, self.n)
+
+    def nnz(self):
+        return int(self.storage.col().numel())
+
+    def to_symmetric(self):
+        rp, c, v = self.storage.rowptr(), self.storage.col(), self.storage.value()
+        r = torch.repeat_interleave(torch.arange(self.n), rp[1:] - rp[:-1])
+        vv = None if v is None else torch.cat([v, v])
+        return Adj(torch.cat([r, c]), torch.cat([c, r]), vv, (self.n, self.n))
+
+    def to(self, device):
+        """Upload the set_diag'd int32 CSR (the host CSR is assumed structurally symmetric)."""
+        rp = self.storage.rowptr()
+        c = self.storage.col()
+        n = self.n
+        r = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+        keep = r != c
+        r, c = r[keep], c[keep]
+        r = torch.cat([r, torch.arange(n)])
+        c = torch.cat([c, torch.arange(n)])
+        key = torch.sort(r * n + c).values
+        self.rowptr32 = torch.zeros(n + 1, dtype=torch.int32)
+        self.rowptr32[1:] = torch.cumsum(torch.bincount(key // n, minlength=n), 0).to(torch.int32)
+        self.col32 = (key % n).to(torch.int32)
+        self.rowptr32 = self.rowptr32.to(device)
+        self.col32 = self.col32.to(device)
+        return self
+
+    @property
+    def device_nnz(self):
+        return int(self.col32.numel())
+
+    @classmethod
+    def from_dense_device(cls, A, keep_host=True):
+        """a13 + a3 on the GPU: CSR of (A != 0 | A.T != 0), i != j, plus self loops.
+
+        ``A`` is a float64 [N, N] device tensor.  The host ``storage`` view (without self loops)
+        is derived from the device CSR when ``keep_host`` is set."""
+        lib = _lib.lib()
+        A = A.contiguous()
+        n = A.shape[0]
+        dev = A.device
+        rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        s = _lib.stream(dev)
+        _lib.check(lib.hicgat_csr_from_dense(_lib.ptr(A), n, n, _lib.ptr(rowptr), None, None, 0, s),
+                   "hicgat_csr_from_dense(count)")
+        nnz = int(rowptr[-1].item())
+        col = torch.empty(nnz, dtype=torch.int32, device=dev)
+        _lib.check(lib.hicgat_csr_from_dense(_lib.ptr(A), n, n, _lib.ptr(rowptr), _lib.ptr(col), None, 0, s),
+                   "hicgat_csr_from_dense(fill)")
+        obj = cls.__new__(cls)
+        obj.n = n
+        obj.rowptr32, obj.col32 = rowptr, col
+        if keep_host:
+            rp = rowptr.cpu().long()
+            c = col.cpu().long()
+            r = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+            keep = r != c
+            hrp = torch.zeros(n + 1, dtype=torch.long)
+            hrp[1:] = torch.cumsum(torch.bincount(r[keep], minlength=n), 0)
+            obj.storage = _Storage(hrp, c[keep], None)
+        else:
+            obj.storage = None
+        return obj
+
+
+class Data:
+    """torch_geometric.data.Data stand-in: x, edge_index (Adj), y."""
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def load_input(input, features, device="cuda"):
+    """utils.py:29-73 with the graph built on the device.
+
+    Returns ``Data(x, edge_index: Adj, y)``; ``y`` is the float64 matrix with zeroed diagonal and
+    ``x`` keeps the dtype of ``features`` (utils.py:54), both on ``device``."""
+    adj_mat = input
+    if adj_mat.shape[1] == 3:
+        adj_mat = convert_to_matrix(adj_mat)
+    np.fill_diagonal(adj_mat, 0)
+    y = torch.tensor(adj_mat, dtype=torch.double, device=device)
+    edge_index = Adj.from_dense_device(y)
+    x = torch.tensor(features).to(device)
+    return Data(x=x, edge_index=edge_index, y=y)
+
+
+def cont2dist(adj, factor, dtype=torch.float64):
+    """utils.py:75-80 on the device: (1/y)^f, diag 0, +inf -> max finite, NaN -> 0, / max."""
+    lib = _lib.lib()
+    y = adj.to(torch.float64).contiguous()
+    n = y.shape[0]
+    out = torch.empty((n, n), dtype=dtype, device=y.device)
+    ws = _lib.workspace(lib.hicgat_cont2dist_workspace_bytes(n), y.device)
+    o32 = out if dtype == torch.float32 else None
+    o64 = out if dtype == torch.float64 else None
+    _lib.check(lib.hicgat_cont2dist(_lib.ptr(y), n, n, float(factor), _lib.ptr(o32), _lib.ptr(o64), n,
+                                    _lib.ptr(ws), ws.numel(), _lib.stream(y.device)), "hicgat_cont2dist")
+    return out
+
+
+def padded_ld(n):
+    return ((n + TILE - 1) // TILE) * TILE
+
+
+class Truth:
+    """fp32 target for the fused distance/MSE kernel: [N, ld] with ld = ceil(N/128)*128.
+
+    ``Truth.from_contacts(y, factor)`` runs cont2dist straight into the padded buffer;
+    ``Truth(t)`` copies an existing [N, N] target (``truth.float()`` of the reference loop)."""
+
+    def __init__(self, t=None, *, _buf=None, _n=None):
+        if _buf is None:
+            t = t.detach()
+            n = t.shape[0]
+            buf = torch.zeros((n, padded_ld(n)), dtype=torch.float32, device=t.device)
+            buf[:, :n] = t.float()
+        else:
+            buf, n = _buf, _n
+        self.buf, self.n, self.ld = buf, n, buf.shape[1]
+        view = buf[:, :n]
+        self.symmetric = bool(torch.equal(view, view.t()))
+
+    @classmethod
+    def from_contacts(cls, y, factor):
+        lib = _lib.lib()
+        y = y.to(torch.float64).contiguous()
+        n = y.shape[0]
+        ld = padded_ld(n)
+        buf = torch.zeros((n, ld), dtype=torch.float32, device=y.device)
+        ws = _lib.workspace(lib.hicgat_cont2dist_workspace_bytes(n), y.device)
+        _lib.check(lib.hicgat_cont2dist(_lib.ptr(y), n, n, float(factor), _lib.ptr(buf), None, ld,
+                                        _lib.ptr(ws), ws.numel(), _lib.stream(y.device)),
+                   "hicgat_cont2dist")
+        return cls(_buf=buf, _n=n)
+
+    def dense(self):
+        return self.buf[:, :self.n]

@@ -1,0 +1,53 @@
+"""``FlatAdam``: torch.optim.Adam semantics (HiC-GNN_main.py:118,130) on one flat buffer.
+
+All parameters of the model are re-pointed into one contiguous fp32 buffer and their ``.grad``
+into another, so one ``hicgat_adam_step`` launch updates every parameter and a data-parallel run
+all-reduces one contiguous gradient buffer (one RCCL call).  Shared parameters (GATConv's
+lin_l / lin_r) are one tensor and appear once, as in ``model.parameters()``.
+"""
+import torch
+
+from . import _lib
+
+
+class FlatAdam:
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.params = [p for p in params if p.requires_grad]
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        # keep every view 16-byte aligned
+        offs, o = [], 0
+        for p in self.params:
+            offs.append(o)
+            o += (p.numel() + 3) // 4 * 4
+        self.numel = o
+        self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(o, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, off in zip(self.params, offs):
+                view = self.flat[off:off + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.grad = self.grad[off:off + p.numel()].view_as(p)
+        self.n_params = n
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none=False):
+        self.grad.zero_()
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        lib = _lib.lib()
+        _lib.check(lib.hicgat_adam_step(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.exp_avg),
+                                        _lib.ptr(self.exp_avg_sq), self.numel, float(self.lr),
+                                        float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                                        self.step_count, _lib.stream(self.flat.device)),
+                   "hicgat_adam_step")
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
+                "lr": self.lr, "betas": self.betas, "eps": self.eps}

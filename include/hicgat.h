@@ -1,0 +1,149 @@
+/*
+ * hicgat.h -- C ABI of libhicgat.so, the MI355X (gfx950) kernels of the GAT-HiC per-epoch step.
+ *
+ * The reference (beyzoskaya/HiC-GNN, /root/reference) is pure Python: its "native boundary" is the
+ * set of third-party torch custom ops that PyG 1.7.2's GATConv, torch.cdist and torch.optim.Adam
+ * call.  Each entry point below replaces one group of those ops; the
+ * comment on each names the reference call site it stands in for.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (PyTorch's caching allocator); nothing
+ *     is allocated inside; scratch ("workspace") is passed in and sized by the *_workspace_bytes()
+ *     query;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*; NULL = the legacy default
+ *     stream) and is stream-ordered; no call synchronises the host, so every call can be captured
+ *     into a hipGraph;
+ *   - return 0 on success or a negative HICGAT_E* code (hicgat_strerror() names it);
+ *   - stateless and re-entrant; one process drives one GPU;
+ *   - index arrays are int32 (nnz < 2^31), converted once from the reference's int64 when the
+ *     adjacency is built; every matrix is row-major with the stated leading dimension.
+ */
+#ifndef HICGAT_H
+#define HICGAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *hicgat_stream_t;
+
+enum {
+  HICGAT_OK = 0,
+  HICGAT_EINVAL = -1,   /* bad size / null pointer / misaligned buffer */
+  HICGAT_ELAUNCH = -2,  /* hipGetLastError() reported a launch failure */
+  HICGAT_EUNSUPPORTED = -3
+};
+
+int hicgat_version(void);
+const char *hicgat_strerror(int code);
+
+/* ---- a13/a3: graph build -------------------------------------------------------------------
+ * Reference: utils.load_input (utils.py:29-73; networkx edges + SparseTensor(...).to_symmetric())
+ * followed by torch_sparse.set_diag inside PyG 1.7.2 GATConv.forward.  From a dense row-major
+ * N x N contact matrix A (float64, leading dim lda), builds the symmetric CSR of
+ * (A[i,j] != 0 || A[j,i] != 0) for i != j, with one self loop (i,i) inserted per row at its sorted
+ * position.  Two calls: first with col == NULL to get rowptr (row_counts scratch of N+1 ints is
+ * rowptr itself), then with col to fill the columns.  Bit-exact with the reference pattern. */
+int hicgat_csr_from_dense(const double *A, int N, int64_t lda, int32_t *rowptr, int32_t *col,
+                          void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_csr_workspace_bytes(int N);
+
+/* ---- a12: utils.cont2dist (utils.py:75-80) on the device ------------------------------------
+ * dist = (1/y)^factor, diagonal 0, +inf -> max finite, NaN -> 0, divided by the max; float64 in,
+ * float32 (or float64) out with leading dimension ldo. workspace: hicgat_cont2dist_workspace_bytes */
+int hicgat_cont2dist(const double *y, int N, int64_t ldy, double factor, float *out32, double *out64,
+                     int64_t ldo, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_cont2dist_workspace_bytes(int N);
+
+/* ---- a2: GATConv lin_l + attention logits (PyG 1.7.2 GATConv.forward) ----------------------
+ * h [N, H*C] = x [N, F] * W^T (W [H*C, F], lin_l.weight, no bias; lin_r is lin_l) and
+ * a_src[n,h] = <h[n,h,:], att_l[h,:]>, a_dst[n,h] = <h[n,h,:], att_r[h,:]>.
+ * hicgat_gat_linear_att computes both (fp32 MFMA GEMM with the logits fused in its epilogue);
+ * hicgat_gat_att_logits computes only the logits from an existing h. */
+int hicgat_gat_linear_att(const float *x, const float *W, const float *att_src, const float *att_dst,
+                          int N, int F, int H, int C, float *h, float *a_src, float *a_dst,
+                          hicgat_stream_t stream);
+int hicgat_gat_att_logits(const float *h, const float *att_src, const float *att_dst, int N, int H,
+                          int C, float *a_src, float *a_dst, hicgat_stream_t stream);
+
+/* ---- a4+a5: edge softmax + neighbour aggregation (PyG 1.7.2 GATConv.propagate) --------------
+ * CSR rows are destinations i, columns sources j, self loops already present (set_diag).
+ *   e_ij = leaky_relu(a_src[j] + a_dst[i], neg_slope)
+ *   alpha_ij = exp(e_ij - max_i) / (sum_i + 1e-16)        (torch_geometric.utils.softmax, ptr path)
+ *   out[i] = sum_j alpha_ij * h[j] + bias                  (segment_csr sum; concat=True)
+ * Saves row_max/row_sum [N, H] for the backward.  Fast path: H*C == 512 with C % 256 == 0 or
+ * H == 1..8 with C % 4 == 0 (generic path otherwise). */
+int hicgat_gat_agg_fwd(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
+                       const float *h, const float *a_src, const float *a_dst, const float *bias,
+                       float neg_slope, float *out, float *row_max, float *row_sum,
+                       hicgat_stream_t stream);
+
+/* ---- a10 (part): backward of a4+a5 ----------------------------------------------------------
+ * Pass 1 (destination side, row i):  g_ij = <dout[i,h,:], h[j,h,:]>,
+ *   delta[i,h] = sum_j alpha_ij g_ij,  da_dst[i,h] = sum_j alpha_ij lrelu'(e_ij) (g_ij - delta[i,h]).
+ * Pass 2 (source side, row r; symmetric graph so N(r) lists every i that has r as a neighbour):
+ *   dh[r] = sum_i alpha_ir dout[i] + da_src[r] (x) att_l + da_dst[r] (x) att_r,
+ *   da_src[r,h] = sum_i alpha_ir lrelu'(e_ir) (g_ir - delta[i,h]).
+ * Requires a structurally symmetric CSR (utils.py:71 to_symmetric guarantees it). */
+int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
+                           const float *h, const float *a_src, const float *a_dst,
+                           const float *row_max, const float *row_sum, const float *dout,
+                           float neg_slope, float *delta, float *da_dst, hicgat_stream_t stream);
+int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
+                           const float *h, const float *a_src, const float *a_dst,
+                           const float *row_max, const float *row_sum, const float *delta,
+                           const float *da_dst, const float *dout, const float *att_src,
+                           const float *att_dst, float neg_slope, float *dh, float *da_src,
+                           hicgat_stream_t stream);
+/* Column reductions for the GATConv parameter gradients (deterministic, two-stage):
+ *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with da_dst;
+ *   dbias[c] = sum_n dout[n,c].  workspace: hicgat_gat_param_grad_workspace_bytes(N, H*C). */
+int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src, const float *da_dst,
+                          int N, int H, int C, float *datt_src, float *datt_dst, float *dbias,
+                          void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_gat_param_grad_workspace_bytes(int N, int D);
+
+/* ---- a7: torch.cdist(c, c, p=2) (models.py:661) and its backward -----------------------------
+ * D[i,j] = ||c_i - c_j||_2 (exact formula; the diagonal is exactly 0), ld = leading dim of D.
+ * Backward: dc_i = sum_j (G_ij + G_ji) (c_i - c_j) / D_ij over D_ij != 0 (torch's
+ * _euclidean_dist_backward masks res == 0).  workspace: hicgat_pairdist_workspace_bytes(N, 0). */
+int hicgat_pairdist_fwd(const float *coords, int N, float *D, int64_t ldd, hicgat_stream_t stream);
+int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg, float *dcoords,
+                        void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+
+/* ---- a7+a8+a9 fused: distance + MSE + Pearson moments + d(MSE)/dcoords, D never stored ------
+ * Reference: out = cdist(coords) (models.py:661); MSELoss()(out, truth) (HiC-GNN_main.py:127);
+ * pearsonr / alpha / total (HiC_GAT_generalize_directly.py:210-225).  T is the SYMMETRIC truth
+ * (leading dim ldt); only upper-triangle tiles [tile_begin, tile_end) of the 128x128 tiling are
+ * read (pass 0, -1 for all).  Outputs:
+ *   stats[10] (float64): 0 sum_{i<j}(d-t)^2, 1 sum d, 2 sum d^2, 3 sum dt, 4 sum t, 5 sum t^2
+ *     (all over i<j of the tile range), 6 mse = (2*[0] + sum_i T_ii^2)/N^2, 7 pearson r,
+ *     8 alpha = min(1, 0.1 + 1/(mse + 1e-6)), 9 total = mse + alpha*(1 - r);
+ *   loss[1] (float32): mse (loss_kind 0) or total (loss_kind 1);
+ *   dcoords [N,3] = d(mse)/dcoords restricted to the tile range (sum over ranks = full gradient).
+ * stats 6..9 are only meaningful when the range covers every tile (or after an all-reduce of
+ * 0..5 followed by hicgat_pairdist_finalize). workspace: hicgat_pairdist_workspace_bytes(N, 1). */
+int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
+                              int64_t tile_begin, int64_t tile_end, int loss_kind, double *stats,
+                              float *loss, float *dcoords, void *workspace, size_t workspace_bytes,
+                              hicgat_stream_t stream);
+int hicgat_pairdist_finalize(const float *T, int N, int64_t ldt, int loss_kind, double *stats,
+                             float *loss, hicgat_stream_t stream);
+int64_t hicgat_pairdist_num_tiles(int N, int mode);
+size_t hicgat_pairdist_workspace_bytes(int N, int mode);
+
+/* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
+ * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
+ *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);
+ *   p += (-lr/(1-b1^t) * m) / (sqrt(v)/sqrt(1-b2^t) + eps). */
+int hicgat_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                     double lr, double beta1, double beta2, double eps, int64_t step,
+                     hicgat_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HICGAT_H */

@@ -1,0 +1,393 @@
+"""GPU parity: every HIP kernel (through libhicgat.so's C ABI) against the CPU oracle / fixtures.
+
+Tolerances (north star: coordinates and loss within 1e-5 relative fp32):
+  * graph build (a3, a13) and cont2dist (a12): bit-exact;
+  * Adam (a10): bit-exact against the torch-CPU restatement;
+  * GATConv forward output, coordinates, loss: rtol 1e-5 (plus a tiny atol for values near 0);
+  * gradients: rtol 1e-4 relative to the tensor's max magnitude (fp32 reassociation over up to
+    4e6 edges; the reference's own CPU thread count changes them by the same order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hicgat  # noqa: F401  (fails loudly if libhicgat.so is missing)
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def _golden_graph(case):
+    import hicgat
+    g = load_golden(f"graph_{case}.npz")
+    y = torch.tensor(g["matrix"], dtype=torch.float64, device=DEV)
+    y.fill_diagonal_(0)
+    adj = hicgat.Adj.from_dense_device(y)
+    return g, y, adj
+
+
+# ---------------------------------------------------------------- a13 / a3 / a12 (bit-exact)
+@pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth256"])
+def test_csr_from_dense_bit_exact(case):
+    from oracle import graph as og
+    g, _, adj = _golden_graph(case)
+    assert np.array_equal(adj.storage.rowptr().numpy(), g["rowptr"])
+    assert np.array_equal(adj.storage.col().numpy(), g["col"])
+    rp, c = og.set_diag(g["rowptr"], g["col"])
+    assert np.array_equal(adj.rowptr32.cpu().numpy(), rp)
+    assert np.array_equal(adj.col32.cpu().numpy(), c)
+
+
+def test_csr_from_dense_asymmetric_and_isolated():
+    import hicgat
+    from oracle import graph as og
+    rng = np.random.default_rng(3)
+    n = 300
+    a = np.where(rng.random((n, n)) < 0.05, rng.random((n, n)), 0.0)   # asymmetric pattern
+    a[7, :] = 0
+    a[:, 7] = 0                                                          # isolated node 7
+    a[11, 12] = np.nan                                                   # NaN counts as an edge
+    np.fill_diagonal(a, 0)
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    rp, c, _ = og.csr_from_matrix(a)
+    assert np.array_equal(adj.storage.rowptr().numpy(), rp)
+    assert np.array_equal(adj.storage.col().numpy(), c)
+    r2, c2 = og.set_diag(rp, c)
+    assert np.array_equal(adj.rowptr32.cpu().numpy(), r2) and np.array_equal(adj.col32.cpu().numpy(), c2)
+    assert adj.rowptr32[8].item() - adj.rowptr32[7].item() == 1                # self loop only
+
+
+@pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth256"])
+@pytest.mark.parametrize("factor,key", [(0.5, "truth05"), (1, "truth1")])
+def test_cont2dist_bit_exact(case, factor, key):
+    import hicgat
+    g, y, _ = _golden_graph(case)
+    t = hicgat.cont2dist(y, factor)
+    assert np.array_equal(t.cpu().numpy(), g[key])
+    tr = hicgat.Truth.from_contacts(y, factor)
+    assert np.array_equal(tr.dense().cpu().numpy(), g[key].astype(np.float32))
+    assert tr.symmetric and tr.ld % 128 == 0
+
+
+# ---------------------------------------------------------------- GATConv (a2, a4, a5 + bwd)
+def _random_graph(n, p, seed):
+    rng = np.random.default_rng(seed)
+    a = (rng.random((n, n)) < p).astype(np.float64)
+    a = np.triu(a, 1)
+    return a + a.T
+
+
+def _gat_pair(seed=0, heads=2, out=256, fin=512):
+    import hicgat
+    from oracle import gat as og
+    torch.manual_seed(seed)
+    ref = og.GATConv(fin, out, heads=heads)
+    torch.manual_seed(seed)
+    mine = hicgat.GATConv(fin, out, heads=heads)
+    for (k1, v1), (k2, v2) in zip(ref.state_dict().items(), mine.state_dict().items()):
+        assert k1 == k2 and torch.equal(v1, v2)
+    with torch.no_grad():
+        mine.bias.copy_(torch.randn_like(mine.bias) * 0.1)
+        ref.bias.copy_(mine.bias)
+    return ref, mine.to(DEV)
+
+
+@pytest.mark.parametrize("n,p", [(58, 1.0), (130, 0.3), (257, 0.02), (600, 0.5)])
+def test_gatconv_forward_backward_matches_oracle(n, p):
+    import hicgat
+    a = _random_graph(n, p, n)
+    if n == 257:
+        a[5, :] = 0
+        a[:, 5] = 0                      # isolated node: row = self loop only
+    ref, mine = _gat_pair(seed=n)
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    rng = np.random.default_rng(n)
+    x = torch.tensor((0.1 * rng.standard_normal((n, 512))).astype(np.float32))
+    g = torch.tensor(rng.standard_normal((n, 512)).astype(np.float32))
+    xr = x.clone().requires_grad_(True)
+    out_r = ref(xr, (adj.storage.rowptr(), adj.storage.col()))
+    (out_r * g).sum().backward()
+    xm = x.to(DEV).requires_grad_(True)
+    out_m = mine(xm, adj)
+    (out_m * g.to(DEV)).sum().backward()
+    np.testing.assert_allclose(out_m.detach().cpu().numpy(), out_r.detach().numpy(), rtol=1e-5, atol=1e-6)
+    assert _rel(xm.grad.cpu(), xr.grad) < 1e-4
+    for (name, pr), (_, pm) in zip(ref.named_parameters(), mine.named_parameters()):
+        assert _rel(pm.grad.cpu(), pr.grad) < 1e-4, name
+
+
+def test_gat_linear_att_matches_torch():
+    import hicgat
+    from hicgat import _lib
+    lib = _lib.lib()
+    torch.manual_seed(1)
+    for n in (1, 63, 64, 65, 1000):
+        x = torch.randn(n, 512, device=DEV)
+        W = torch.randn(512, 512, device=DEV) * 0.05
+        al = torch.randn(1, 2, 256, device=DEV)
+        ar = torch.randn(1, 2, 256, device=DEV)
+        h = torch.empty(n, 512, device=DEV)
+        a_s = torch.empty(n, 2, device=DEV)
+        a_d = torch.empty(n, 2, device=DEV)
+        _lib.check(lib.hicgat_gat_linear_att(_lib.ptr(x), _lib.ptr(W), _lib.ptr(al), _lib.ptr(ar), n, 512, 2,
+                                             256, _lib.ptr(h), _lib.ptr(a_s), _lib.ptr(a_d), _lib.stream()), "lin")
+        href = (x.double() @ W.double().t())
+        assert _rel(h.cpu(), href.cpu()) < 2e-6
+        hs = href.view(n, 2, 256)
+        assert _rel(a_s.cpu(), (hs * al.double()).sum(-1).cpu()) < 1e-5
+        assert _rel(a_d.cpu(), (hs * ar.double()).sum(-1).cpu()) < 1e-5
+    assert hicgat  # silence
+
+
+def test_gat_agg_long_rows_and_softmax_extremes():
+    """Rows far longer than a wave chunk (2000 neighbours, not a multiple of 8) and logits with a
+    large spread (the max subtraction must keep exp finite)."""
+    import hicgat
+    n = 2003
+    a = np.ones((n, n)) - np.eye(n)
+    ref, mine = _gat_pair(seed=5)
+    with torch.no_grad():
+        ref.att_l.mul_(40.0)
+        mine.att_l.copy_(ref.att_l.to(DEV))
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    x = torch.tensor((0.1 * np.random.default_rng(0).standard_normal((n, 512))).astype(np.float32))
+    out_r = ref(x, (adj.storage.rowptr(), adj.storage.col()))
+    out_m = mine(x.to(DEV), adj)
+    np.testing.assert_allclose(out_m.detach().cpu().numpy(), out_r.detach().numpy(), rtol=1e-5, atol=2e-6)
+    assert torch.isfinite(out_m).all()
+
+
+# ---------------------------------------------------------------- a7-a9: distance + loss
+@pytest.mark.parametrize("n", [1, 2, 58, 129, 300])
+def test_pairdist_fwd_bwd_matches_torch(n):
+    import hicgat
+    torch.manual_seed(n)
+    c = torch.randn(n, 3, dtype=torch.float64)
+    g = torch.randn(n, n, dtype=torch.float64)
+    cr = c.clone().requires_grad_(True)
+    dr = torch.cdist(cr, cr, compute_mode="donot_use_mm_for_euclid_dist")
+    (dr * g).sum().backward()
+    cm = c.float().to(DEV).requires_grad_(True)
+    dm = hicgat.ops.pairwise_dist(cm)
+    (dm * g.float().to(DEV)).sum().backward()
+    assert _rel(dm.detach().cpu(), dr.detach()) < 1e-6
+    assert torch.all(torch.diagonal(dm) == 0)
+    if n > 1:
+        assert _rel(cm.grad.cpu(), cr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n", [2, 58, 128, 129, 400])
+@pytest.mark.parametrize("kind", ["mse", "combined"])
+def test_fused_loss_matches_oracle(n, kind):
+    import hicgat
+    from oracle import loop as ol
+    rng = np.random.default_rng(n)
+    t = rng.random((n, n))
+    t = (t + t.T) / 2
+    np.fill_diagonal(t, 0)
+    truth = torch.tensor(t, dtype=torch.float64)
+    c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32))
+    cr = c.clone().requires_grad_(True)
+    out = torch.cdist(cr.double(), cr.double(), compute_mode="donot_use_mm_for_euclid_dist")
+    if kind == "mse":
+        lr = ol.mse_loss(out.float(), truth)
+    else:
+        lr = torch.nn.functional.mse_loss(out, truth)   # fp64 value; grad of mse only
+    lr.backward()
+    tr = hicgat.Truth(truth.to(DEV))
+    cm = c.to(DEV).requires_grad_(True)
+    lm, stats = hicgat.ops.fused_dist_loss(cm, tr, kind)
+    lm.backward()
+    st = stats.cpu().numpy()
+    mse_ref = float(torch.nn.functional.mse_loss(out.detach(), truth))
+    assert abs(st[6] - mse_ref) <= 1e-5 * mse_ref
+    if n > 2:
+        r_ref = ol.pearson_r(c.double(), truth)
+        assert abs(st[7] - r_ref) < 1e-6
+        if kind == "combined":
+            alpha = min(1.0, 0.1 + 1.0 / (float(np.float32(st[6])) + 1e-6))
+            assert abs(st[8] - alpha) < 1e-12
+            assert abs(lm.item() - (np.float32(st[6]) + alpha * (1 - r_ref))) < 1e-5
+    assert _rel(cm.grad.cpu(), cr.grad) < 1e-5
+    assert abs(cm.grad.sum(0)).max().item() < 1e-5 * max(cm.grad.abs().max().item(), 1e-30) * n
+
+
+def test_fused_loss_tile_ranges_sum_to_whole():
+    """The multi-GPU contract: disjoint tile ranges give stats/dcoords that add up to the full
+    call (moments exactly up to fp64 reassociation, dcoords to fp32 rounding)."""
+    import hicgat
+    from hicgat import _lib
+    n = 700
+    rng = np.random.default_rng(0)
+    t = rng.random((n, n))
+    t = (t + t.T) / 2
+    np.fill_diagonal(t, 0)
+    tr = hicgat.Truth(torch.tensor(t, device=DEV))
+    c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32), device=DEV)
+    tiles = _lib.load().hicgat_pairdist_num_tiles(n, 0)
+    full_l, full_s = hicgat.ops.fused_dist_loss(c.clone().requires_grad_(True), tr)
+    parts = [(0, tiles // 3), (tiles // 3, tiles // 2), (tiles // 2, tiles)]
+    acc = torch.zeros(6, dtype=torch.float64)
+    g = torch.zeros(n, 3)
+    for b, e in parts:
+        cc = c.clone().requires_grad_(True)
+        l, s = hicgat.ops.fused_dist_loss(cc, tr, tile_range=(b, e))
+        l.backward()
+        acc += s[:6].cpu()
+        g += cc.grad.cpu()
+    assert torch.allclose(acc, full_s[:6].cpu(), rtol=1e-12)
+    cf = c.clone().requires_grad_(True)
+    hicgat.ops.fused_dist_loss(cf, tr)[0].backward()
+    assert _rel(g, cf.grad.cpu()) < 1e-6
+
+
+# ---------------------------------------------------------------- a10: Adam
+def test_adam_bit_exact_vs_torch_cpu_restatement():
+    import hicgat
+    from oracle import loop as ol
+    rng = np.random.default_rng(0)
+    n = 100003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    params = [torch.nn.Parameter(torch.tensor(p0, device=DEV))]
+    opt = hicgat.FlatAdam(params, lr=1e-3)
+    p, m, v = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for step in range(1, 8):
+        g = rng.standard_normal(n).astype(np.float32)
+        opt.grad[:n].copy_(torch.tensor(g))
+        opt.step()
+        p, m, v = ol.adam_reference_step(p, g, m, v, step)
+        assert np.array_equal(params[0].detach().cpu().numpy(), p), step
+
+
+# ---------------------------------------------------------------- models vs reference fixtures
+@pytest.mark.parametrize("name", ["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2"])
+def test_model_matches_reference_fixture(name):
+    import hicgat
+    fx = load_golden(f"model_{name}.npz")
+    g = load_golden("graph_chr19_1mb.npz")
+    torch.manual_seed(0)
+    model = hicgat.MODELS[name]()
+    for k, v in model.state_dict().items():
+        assert np.array_equal(v.numpy(), fx[f"state::{k}"]), k          # same init from the seed
+    model = model.to(DEV)
+    y = torch.tensor(g["matrix"], device=DEV)
+    y.fill_diagonal_(0)
+    adj = hicgat.Adj.from_dense_device(y)
+    x = torch.tensor(fx["x"], device=DEV)
+    out = model(x, adj)
+    # D: our cdist is exact; the reference used the mm formula -> absolute check
+    np.testing.assert_allclose(out.detach().cpu().numpy(), fx["out"], rtol=1e-5, atol=2e-5)
+    coords = model.get_model(x, adj)
+    np.testing.assert_allclose(coords.detach().cpu().numpy(), fx["coords"], rtol=1e-5, atol=1e-6)
+    tr = hicgat.Truth.from_contacts(y, 0.5)
+    loss, stats, _ = model.loss(x, adj, tr, "combined")
+    assert abs(stats[6].item() - float(fx["mse"])) <= 1e-5 * float(fx["mse"])
+    assert abs(stats[7].item() - float(fx["pearson"])) < 1e-5
+    assert abs(loss.item() - float(fx["total"])) < 1e-5 * float(fx["total"])
+    model.zero_grad()
+    lm, _, _ = model.loss(x, adj, tr, "mse")
+    lm.backward()
+    for k, p in model.named_parameters():
+        ref = fx[f"grad::{k}"]
+        assert _rel(p.grad.cpu(), ref) < 2e-4, k
+
+
+def test_train_loop_tracks_reference_fixture():
+    """HiC-GNN_main.py loop, fixed K = 25: loss curve vs the reference run.  The first steps agree
+    to fp32 rounding; Adam's sign sensitivity makes later steps drift, so the
+    bound widens with the step index."""
+    import hicgat
+    fx = load_golden("train_GATNetSelectiveResidualsUpdated.npz")
+    mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz")
+    g = load_golden("graph_chr19_1mb.npz")
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    y = torch.tensor(g["matrix"], device=DEV)
+    y.fill_diagonal_(0)
+    data = hicgat.Data(x=torch.tensor(mfx["x"], device=DEV), edge_index=hicgat.Adj.from_dense_device(y), y=y)
+    tr = hicgat.Truth.from_contacts(y, 0.5)
+    _, hist = hicgat.train.train(model, data, tr, steps=int(fx["steps"]))
+    ref = fx["loss"]
+    rel = np.abs(np.array(hist) - ref) / ref
+    assert rel[0] < 1e-5 and rel[1] < 1e-5 and rel[2] < 1e-4
+    assert np.all(rel < 0.05)
+
+
+def test_dscc_matches_scipy():
+    import hicgat
+    from scipy.stats import spearmanr
+    g = load_golden("graph_chr19_500kb.npz")
+    rng = np.random.default_rng(0)
+    n = g["truth05"].shape[0]
+    c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32), device=DEV)
+    t = torch.tensor(g["truth05"], device=DEV)
+    rho = hicgat.metrics.dscc(c, t)
+    iu = np.triu_indices(n, 1)
+    d = torch.cdist(c.cpu(), c.cpu(), compute_mode="donot_use_mm_for_euclid_dist").numpy()
+    ref = spearmanr(g["truth05"][iu], d[iu])[0]
+    assert abs(rho - ref) < 1e-9
+
+
+# ---------------------------------------------------------------- full-size properties
+def test_full_size_synth20000_properties():
+    """At BASELINE's N = 20000 / 1 % size: (i) 24 sampled rows of the GAT aggregation against an
+    fp64 host evaluation of those rows, (ii) softmax weights sum to 1 (h == const rows give
+    out == const + bias), (iii) translation invariance of the distance-loss gradient."""
+    import hicgat
+    from hicgat import _lib, synth
+    n = 20000
+    i, j, c = synth.contact_pairs(n, density=0.01, seed=0)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    nnz = adj.device_nnz
+    assert abs((nnz - n) / (n * (n - 1)) - 0.01) < 2e-4
+    torch.manual_seed(0)
+    conv = hicgat.GATConv(512, 256, heads=2).to(DEV)
+    x = torch.tensor(synth.features(n), device=DEV)
+    with torch.no_grad():
+        out = conv(x, adj)
+        h = x.double() @ conv.lin_l.weight.double().t()
+        hv = h.view(n, 2, 256)
+        a_s = (hv * conv.att_l.double()).sum(-1)
+        a_d = (hv * conv.att_r.double()).sum(-1)
+    rp = adj.rowptr32.cpu().numpy()
+    cl = adj.col32.cpu().numpy()
+    for r in np.random.default_rng(1).choice(n, 24, replace=False):
+        nb = torch.tensor(cl[rp[r]:rp[r + 1]].astype(np.int64), device=DEV)
+        e = torch.nn.functional.leaky_relu(a_s[nb] + a_d[r], 0.2)
+        al = torch.softmax(e, 0)
+        ref = (al.unsqueeze(-1) * hv[nb]).sum(0).reshape(-1) + conv.bias.double()
+        assert _rel(out[r].cpu(), ref.cpu()) < 1e-5
+    lib = _lib.lib()
+    hconst = torch.full((n, 512), 0.75, device=DEV)
+    a_s = torch.randn(n, 2, device=DEV)
+    a_d = torch.randn(n, 2, device=DEV)
+    bias = torch.randn(512, device=DEV)
+    o = torch.empty(n, 512, device=DEV)
+    rm = torch.empty(n, 2, device=DEV)
+    rs = torch.empty(n, 2, device=DEV)
+    _lib.check(lib.hicgat_gat_agg_fwd(_lib.ptr(adj.rowptr32), _lib.ptr(adj.col32), n, nnz, 2, 256,
+                                      _lib.ptr(hconst), _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(bias), 0.2,
+                                      _lib.ptr(o), _lib.ptr(rm), _lib.ptr(rs), _lib.stream()), "agg")
+    assert torch.allclose(o, 0.75 + bias.expand_as(o), rtol=0, atol=2e-6)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    cc = torch.randn(n, 3, device=DEV).requires_grad_(True)
+    loss, stats = hicgat.ops.fused_dist_loss(cc, tr)
+    loss.backward()
+    gsum = cc.grad.double().sum(0).abs().max().item()
+    assert gsum < 1e-4 * cc.grad.abs().max().item() * np.sqrt(n)
+    assert np.isfinite(stats.cpu().numpy()[:8]).all()

@@ -1,0 +1,88 @@
+"""CPU: the C-ABI library loads and exports every symbol of include/hicgat.h (no compute calls),
+and the host-side logic (list -> matrix, PDB writer, synthetic generator, tile counts)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT, load_golden
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "hicgat.h")) as fh:
+        text = fh.read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(hicgat_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from hicgat import _lib
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert lib.hicgat_version() == 1
+    assert b"unsupported" in lib.hicgat_strerror(-3)
+
+
+def test_query_functions_need_no_gpu():
+    from hicgat import _lib
+    lib = _lib.load()
+    assert lib.hicgat_pairdist_num_tiles(20000, 0) == 157 * 158 // 2
+    assert lib.hicgat_pairdist_num_tiles(20000, 1) == 157 * 157
+    assert lib.hicgat_pairdist_num_tiles(0, 0) == 0
+    assert lib.hicgat_pairdist_workspace_bytes(58, 1) > 0
+
+
+def test_ops_fail_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import hicgat
+    with pytest.raises(hicgat._lib.HicgatUnavailable):
+        hicgat.ops.pairwise_dist(torch.zeros(4, 3))
+
+
+@pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth256"])
+def test_convert_to_matrix_bit_exact(case):
+    import hicgat
+    g = load_golden(f"graph_{case}.npz")
+    assert np.array_equal(hicgat.convert_to_matrix(g["list"]), g["matrix"])
+
+
+def test_adj_host_surface_matches_reference_csr():
+    import hicgat
+    g = load_golden("graph_chr19_500kb.npz")
+    a = g["matrix"].copy()
+    np.fill_diagonal(a, 0)
+    iu = np.argwhere(np.triu(a != 0, 1))
+    adj = hicgat.Adj(torch.tensor(iu[:, 0]), torch.tensor(iu[:, 1]), torch.ones(len(iu)), (a.shape[0], a.shape[0]))
+    sym = adj.to_symmetric()
+    assert np.array_equal(sym.storage.rowptr().numpy(), g["rowptr"])
+    assert np.array_equal(sym.storage.col().numpy(), g["col"])
+
+
+@pytest.mark.parametrize("pdb", ["GM12878_1mb_chr19_list_structure.pdb",
+                                 "GM12878_500kb_chr19_list_generalized_structure.pdb"])
+def test_write_pdb_byte_exact_with_reference_output(tmp_path, pdb):
+    from hicgat import io
+    src = os.path.join(GOLDEN, pdb)
+    xyz = io.read_pdb_coords(src)
+    out = tmp_path / "o.pdb"
+    io.write_pdb(xyz, str(out))
+    assert out.read_bytes() == open(src, "rb").read()
+
+
+def test_synthetic_generator_density_and_determinism():
+    from hicgat import synth
+    i, j, c = synth.contact_pairs(3000, density=0.01, seed=0)
+    i2, j2, c2 = synth.contact_pairs(3000, density=0.01, seed=0)
+    assert np.array_equal(i, i2) and np.array_equal(j, j2) and np.array_equal(c, c2)
+    dens = 2 * len(i) / (3000 * 2999)
+    assert abs(dens - 0.01) < 5e-4
+    assert np.all(i < j) and np.all(c >= 1)
+    i, j, c = synth.contact_pairs(200, density=None, seed=0)
+    assert len(i) == 200 * 199 // 2

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One gpurun call: GPU parity tests, smoke, a short bench and a rocprofv3 kernel-trace summary.
+# Assertion failures (exit 1) do not stop the script; a crash, abort, fault or timeout does.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -n 25 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc" >&2; exit $rc; fi
+  return 0
+}
+STAGES=${STAGES:-"tests smoke bench prof"}
+for s in $STAGES; do
+  case $s in
+    tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+               python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+  esac
+done
