@@ -118,7 +118,7 @@ def main():
     args = ap.parse_args()
 
     import hicgat
-    from hicgat import ops
+    from hicgat import kernels
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -150,7 +150,7 @@ def main():
         torch.distributed.barrier()
     log(f"[bench] warmup done ({args.warmup} steps)")
 
-    ops.TIMERS = {}
+    kernels.TIMERS = {}
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -161,7 +161,7 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         torch.distributed.barrier()
-    timers, ops.TIMERS = ops.TIMERS, None
+    timers, kernels.TIMERS = kernels.TIMERS, None
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

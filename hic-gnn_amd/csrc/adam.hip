@@ -18,7 +18,7 @@ struct AdamConsts {
 __device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, const AdamConsts &k) {
   m = fmaf(k.w1, g - m, m);
   v = fmaf(k.c2 * g, g, v * k.b2);
-  const float denom = __fsqrt_rn(v) / k.bc2s + k.eps;
+  const float denom = sqrt_rn_f32(v) / k.bc2s + k.eps;
   p = p + __fdiv_rn(k.neg_step * m, denom);
 }
 

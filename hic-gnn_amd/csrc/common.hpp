@@ -33,6 +33,30 @@ __device__ __forceinline__ float half_wave_sum(float v) {
   return v;
 }
 
+// Correctly rounded square roots.  v_sqrt_f32 / the default f64 lowering are within 1 ulp but
+// not IEEE-exact; torch's CPU sqrt (and pow(x, 0.5)) is.  Given y within 1 ulp of sqrt(x), the
+// neighbour y-1ulp is the answer iff x <= (y-1ulp)*y, and y+1ulp iff x > (y+1ulp)*y (the exact
+// products sit inside the rounding midpoints by far less than one ulp of x).
+__device__ __forceinline__ float sqrt_rn_f32(float x) {
+  if (!(x > 0.f) || x == INFINITY) return __builtin_sqrtf(x);
+  const bool tiny = x < 0x1.0p-96f;
+  const float xs = tiny ? x * 0x1.0p+32f : x;
+  float y = __builtin_amdgcn_sqrtf(xs);
+  const float yd = __int_as_float(__float_as_int(y) - 1), yu = __int_as_float(__float_as_int(y) + 1);
+  if (fmaf(-yd, y, xs) <= 0.f) y = yd;
+  else if (fmaf(-yu, y, xs) > 0.f) y = yu;
+  return tiny ? y * 0x1.0p-16f : y;
+}
+__device__ __forceinline__ double sqrt_rn_f64(double x) {
+  if (!(x > 0.0) || x == (double)INFINITY) return __builtin_sqrt(x);
+  double y = __builtin_sqrt(x);
+  const double yd = __longlong_as_double(__double_as_longlong(y) - 1);
+  const double yu = __longlong_as_double(__double_as_longlong(y) + 1);
+  if (fma(-yd, y, x) <= 0.0) y = yd;
+  else if (fma(-yu, y, x) > 0.0) y = yu;
+  return y;
+}
+
 // torch.nn.functional.leaky_relu: x > 0 ? x : x * slope.
 __device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
 

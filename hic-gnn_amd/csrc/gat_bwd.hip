@@ -20,15 +20,13 @@
 namespace hicgat {
 
 __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
-    const int *__restrict__ rowptr, const int *__restrict__ col, int N, const float *__restrict__ h,
-    const float *__restrict__ a_src, const float *__restrict__ a_dst,
-    const float *__restrict__ rmax, const float *__restrict__ rsum,
-    const float *__restrict__ dout, float ns, float *__restrict__ delta,
-    float *__restrict__ da_dst) {
+    const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
+    const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ dout, float ns, float *__restrict__ row_stats) {
   constexpr int U = 8;
   const int lane = lane_id();
-  const int i = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (i >= N) return;
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (i >= row_end) return;
   const int beg = rowptr[i], end = rowptr[i + 1];
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
@@ -37,8 +35,8 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
   const int hh = lane >> 5, kk = (lane >> 2) & 7;
   const bool owner = (lane & 3) == 0;
   const float adh = a_dst[2 * (size_t)i + hh];
-  const float mh = rmax[2 * (size_t)i + hh];
-  const float denh = rsum[2 * (size_t)i + hh] + 1e-16f;
+  const float mh = row_stats[8 * (size_t)i + hh];
+  const float denh = row_stats[8 * (size_t)i + 2 + hh] + 1e-16f;
   float S1 = 0.f, S2 = 0.f, S3 = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
@@ -73,33 +71,28 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
   S1 = half_wave_sum(S1);
   S2 = half_wave_sum(S2);
   S3 = half_wave_sum(S3);
-  if ((lane & 31) == 0) {
-    delta[2 * (size_t)i + hh] = S1;
-    da_dst[2 * (size_t)i + hh] = S2 - S1 * S3;
-  }
+  const float dl0 = readlane_f(S1, 0), dl1 = readlane_f(S1, 32);
+  const float dd0 = readlane_f(S2 - S1 * S3, 0), dd1 = readlane_f(S2 - S1 * S3, 32);
+  if (lane == 0) reinterpret_cast<float4 *>(row_stats)[2 * (size_t)i + 1] = make_float4(dl0, dl1, dd0, dd1);
 }
 
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
-    const int *__restrict__ rowptr, const int *__restrict__ col, int N, const float *__restrict__ h,
-    const float *__restrict__ a_src, const float *__restrict__ a_dst,
-    const float *__restrict__ rmax, const float *__restrict__ rsum,
-    const float *__restrict__ delta, const float *__restrict__ da_dst,
-    const float *__restrict__ dout, const float *__restrict__ att_s,
-    const float *__restrict__ att_d, float ns, float *__restrict__ dh,
-    float *__restrict__ da_src) {
+    const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
+    const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ row_stats, const float *__restrict__ dout,
+    const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
+    float *__restrict__ dh, float *__restrict__ da_src) {
   constexpr int U = 8;
   const int lane = lane_id();
-  const int r = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (r >= N) return;
+  const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (r >= row_end) return;
   const int beg = rowptr[r], end = rowptr[r + 1];
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
   const float4 hr0 = h4[(size_t)r * 128 + lane], hr1 = h4[(size_t)r * 128 + 64 + lane];
   const float2 asr = *reinterpret_cast<const float2 *>(a_src + 2 * (size_t)r);
   const float2 *ad2 = reinterpret_cast<const float2 *>(a_dst);
-  const float2 *mx2 = reinterpret_cast<const float2 *>(rmax);
-  const float2 *sm2 = reinterpret_cast<const float2 *>(rsum);
-  const float2 *dl2 = reinterpret_cast<const float2 *>(delta);
+  const float4 *rs4 = reinterpret_cast<const float4 *>(row_stats);
   const int hh = lane >> 5, kk = (lane >> 2) & 7;
   const bool owner = (lane & 3) == 0;
   float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
@@ -110,10 +103,12 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     float al0 = 0.f, al1 = 0.f, A0 = 0.f, A1 = 0.f, B0 = 0.f, B1 = 0.f;
     if (e < end) {
       inb = col[e];
-      const float2 ad = ad2[inb], mx = mx2[inb], sm = sm2[inb], dl = dl2[inb];
+      const float2 ad = ad2[inb];
+      const float4 ms = rs4[2 * (size_t)inb];                                 // max0 max1 sum0 sum1
+      const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)inb + 4);  // delta
       const float e0 = asr.x + ad.x, e1 = asr.y + ad.y;
-      al0 = expf(lrelu(e0, ns) - mx.x) / (sm.x + 1e-16f);
-      al1 = expf(lrelu(e1, ns) - mx.y) / (sm.y + 1e-16f);
+      al0 = expf(lrelu(e0, ns) - ms.x) / (ms.z + 1e-16f);
+      al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
       A0 = al0 * (e0 > 0.f ? 1.f : ns);
       A1 = al1 * (e1 > 0.f ? 1.f : ns);
       B0 = A0 * dl.x;
@@ -145,7 +140,7 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   }
   Sda = half_wave_sum(Sda);
   const float ds0 = readlane_f(Sda, 0), ds1 = readlane_f(Sda, 32);
-  const float2 dd = *reinterpret_cast<const float2 *>(da_dst + 2 * (size_t)r);
+  const float2 dd = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)r + 6);
   const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
   const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
   const float4 as0 = s4[lane], as1 = s4[64 + lane], at0 = t4[lane], at1 = t4[64 + lane];
@@ -170,7 +165,7 @@ constexpr int kParamBlocks = 512;
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
                                                          const float *__restrict__ dout,
                                                          const float *__restrict__ da_src,
-                                                         const float *__restrict__ da_dst, int N,
+                                                         const float *__restrict__ row_stats, int N,
                                                          int H, int C, int rows_per_block,
                                                          float *__restrict__ part) {
   const int D = H * C, Q = D / 4;
@@ -184,7 +179,7 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
     for (int n = r0; n < r1; ++n) {
       const float4 hv = h4[(size_t)n * Q + q], gv = g4[(size_t)n * Q + q];
       s = f4_fma(da_src[(size_t)n * H + hd], hv, s);
-      t = f4_fma(da_dst[(size_t)n * H + hd], hv, t);
+      t = f4_fma(row_stats[(size_t)n * 4 * H + 3 * H + hd], hv, t);
       b.x += gv.x; b.y += gv.y; b.z += gv.z; b.w += gv.w;
     }
     p4[q] = s;
@@ -210,39 +205,38 @@ __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict
 using namespace hicgat;
 
 extern "C" int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int H,
-                                      int C, const float *h, const float *a_src,
-                                      const float *a_dst, const float *row_max,
-                                      const float *row_sum, const float *dout, float neg_slope,
-                                      float *delta, float *da_dst, hicgat_stream_t stream) {
-  if (N < 0) return HICGAT_EINVAL;
+                                      int C, int row_begin, int row_end, const float *h,
+                                      const float *a_src, const float *a_dst, const float *dout,
+                                      float neg_slope, float *row_stats, hicgat_stream_t stream) {
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (N == 0) return HICGAT_OK;
-  if (!rowptr || !col || !h || !a_src || !a_dst || !row_max || !row_sum || !dout || !delta || !da_dst)
-    return HICGAT_EINVAL;
-  hipLaunchKernelGGL(agg_bwd_dst_h2c256_kernel, dim3((N + 3) / 4), dim3(256), 0,
-                     (hipStream_t)stream, rowptr, col, N, h, a_src, a_dst, row_max, row_sum, dout,
-                     neg_slope, delta, da_dst);
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !dout || !row_stats) return HICGAT_EINVAL;
+  const int rows = row_end - row_begin;
+  hipLaunchKernelGGL(agg_bwd_dst_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst, dout,
+                     neg_slope, row_stats);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
 extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H,
-                                      int C, const float *h, const float *a_src,
-                                      const float *a_dst, const float *row_max,
-                                      const float *row_sum, const float *delta,
-                                      const float *da_dst, const float *dout,
+                                      int C, int row_begin, int row_end, const float *h,
+                                      const float *a_src, const float *a_dst,
+                                      const float *row_stats, const float *dout,
                                       const float *att_src, const float *att_dst,
                                       float neg_slope, float *dh, float *da_src,
                                       hicgat_stream_t stream) {
-  if (N < 0) return HICGAT_EINVAL;
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (N == 0) return HICGAT_OK;
-  if (!rowptr || !col || !h || !a_src || !a_dst || !row_max || !row_sum || !delta || !da_dst ||
-      !dout || !att_src || !att_dst || !dh || !da_src)
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !row_stats || !dout || !att_src || !att_dst ||
+      !dh || !da_src)
     return HICGAT_EINVAL;
-  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((N + 3) / 4), dim3(256), 0,
-                     (hipStream_t)stream, rowptr, col, N, h, a_src, a_dst, row_max, row_sum, delta,
-                     da_dst, dout, att_src, att_dst, neg_slope, dh, da_src);
+  const int rows = row_end - row_begin;
+  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
+                     row_stats, dout, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -253,12 +247,12 @@ extern "C" size_t hicgat_gat_param_grad_workspace_bytes(int N, int D) {
 }
 
 extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
-                                     const float *da_dst, int N, int H, int C, float *datt_src,
+                                     const float *row_stats, int N, int H, int C, float *datt_src,
                                      float *datt_dst, float *dbias, void *workspace,
                                      size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || H <= 0 || C <= 0 || (C % 4) != 0) return HICGAT_EINVAL;
   const int D = H * C;
-  if (!h || !dout || !da_src || !da_dst || !datt_src || !datt_dst || !dbias || !workspace)
+  if (!h || !dout || !da_src || !row_stats || !datt_src || !datt_dst || !dbias || !workspace)
     return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_gat_param_grad_workspace_bytes(N, D)) return HICGAT_EINVAL;
   const int rpb = N > 0 ? (N + kParamBlocks - 1) / kParamBlocks : 1;
@@ -266,7 +260,7 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
   float *part = static_cast<float *>(workspace);
   if (nblk > 0) {
     hipLaunchKernelGGL(param_grad_stage1, dim3(nblk), dim3(128), 0, (hipStream_t)stream, h, dout,
-                       da_src, da_dst, N, H, C, rpb, part);
+                       da_src, row_stats, N, H, C, rpb, part);
     HICGAT_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 255) / 256), dim3(256), 0,

@@ -6,7 +6,9 @@
 // writes anything per edge.
 //
 // Layout: h [N, D] fp32 row-major (D = H*C = 512 -> one 2 KiB row), a_src/a_dst [N, H],
-// CSR int32 (rowptr [N+1], col [nnz]) with the self loops already inserted.
+// CSR int32 (rowptr [N+1], col [nnz]) with the self loops already inserted, row_stats [N, 4H]
+// = (max[H], sum[H], delta[H], da_dst[H]) per row.  A launch covers rows [row_begin, row_end)
+// (a rank's destination shard); every per-row array is indexed by the global row id.
 #include "common.hpp"
 
 namespace hicgat {
@@ -48,14 +50,14 @@ __global__ __launch_bounds__(256) void att_logits_kernel(const float *__restrict
 // neighbour index and both alphas broadcast from lane k through SGPRs (v_readlane), so each
 // gather is one scalar base + per-lane offset global_load_dwordx4, 8 neighbours in flight.
 __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
-    const int *__restrict__ rowptr, const int *__restrict__ col, int N, const float *__restrict__ h,
-    const float *__restrict__ a_src, const float *__restrict__ a_dst,
-    const float *__restrict__ bias, float ns, float *__restrict__ out, float *__restrict__ rmax,
-    float *__restrict__ rsum) {
+    const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
+    const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ bias, float ns, float *__restrict__ out,
+    float *__restrict__ row_stats) {
   constexpr int U = 8;  // neighbours in flight per lane
   const int lane = lane_id();
-  const int i = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (i >= N) return;
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (i >= row_end) return;
   const int beg = rowptr[i], end = rowptr[i + 1];
   const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
   const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
@@ -113,12 +115,7 @@ __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
   acc1.x += b1.x; acc1.y += b1.y; acc1.z += b1.z; acc1.w += b1.w;
   o4[(size_t)i * 128 + lane] = acc0;
   o4[(size_t)i * 128 + 64 + lane] = acc1;
-  if (lane == 0) {
-    rmax[2 * (size_t)i] = m0;
-    rmax[2 * (size_t)i + 1] = m1;
-    rsum[2 * (size_t)i] = s0;
-    rsum[2 * (size_t)i + 1] = s1;
-  }
+  if (lane == 0) reinterpret_cast<float4 *>(row_stats)[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
 }
 
 }  // namespace hicgat
@@ -138,16 +135,17 @@ extern "C" int hicgat_gat_att_logits(const float *h, const float *att_src, const
 }
 
 extern "C" int hicgat_gat_agg_fwd(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H,
-                                  int C, const float *h, const float *a_src, const float *a_dst,
-                                  const float *bias, float neg_slope, float *out, float *row_max,
-                                  float *row_sum, hicgat_stream_t stream) {
-  if (N < 0 || nnz < 0) return HICGAT_EINVAL;
+                                  int C, int row_begin, int row_end, const float *h,
+                                  const float *a_src, const float *a_dst, const float *bias,
+                                  float neg_slope, float *out, float *row_stats,
+                                  hicgat_stream_t stream) {
+  if (N < 0 || nnz < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (N == 0) return HICGAT_OK;
-  if (!rowptr || !col || !h || !a_src || !a_dst || !bias || !out || !row_max || !row_sum)
-    return HICGAT_EINVAL;
-  hipLaunchKernelGGL(agg_fwd_h2c256_kernel, dim3((N + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     rowptr, col, N, h, a_src, a_dst, bias, neg_slope, out, row_max, row_sum);
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !bias || !out || !row_stats) return HICGAT_EINVAL;
+  const int rows = row_end - row_begin;
+  hipLaunchKernelGGL(agg_fwd_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     rowptr, col, row_begin, row_end, h, a_src, a_dst, bias, neg_slope, out, row_stats);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -82,10 +82,10 @@ __device__ __forceinline__ double torch_pow_scalar(double x, double f) {
   // ATen pow(Tensor, Scalar): exp 1 -> copy, 0 -> 1, and the optimized special exponents.
   if (f == 1.0) return x;
   if (f == 0.0) return 1.0;
-  if (f == 0.5) return sqrt(x);
+  if (f == 0.5) return sqrt_rn_f64(x);
   if (f == 2.0) return x * x;
   if (f == 3.0) return x * x * x;
-  if (f == -0.5) return 1.0 / sqrt(x);
+  if (f == -0.5) return 1.0 / sqrt_rn_f64(x);
   if (f == -1.0) return 1.0 / x;
   if (f == -2.0) return 1.0 / (x * x);
   return pow(x, f);

@@ -24,12 +24,12 @@ SIGNATURES = {
     "hicgat_cont2dist_workspace_bytes": (c_sz, [c_int]),
     "hicgat_gat_linear_att": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_gat_att_logits": (c_int, [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
-    "hicgat_gat_agg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_f,
-                                   c_p, c_p, c_p, c_p]),
-    "hicgat_gat_agg_bwd_dst": (c_int, [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p,
-                                       c_f, c_p, c_p, c_p]),
-    "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p,
-                                       c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_agg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p,
+                                   c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_agg_bwd_dst": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                       c_f, c_p, c_p]),
+    "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                       c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),

@@ -1,0 +1,128 @@
+"""Destination-row sharded training step over P ranks (one GPU each, RCCL over xGMI).
+
+BASELINE.json north star: "partition across the 8 GPUs of one node by sharding destination nodes
+with an RCCL all-gather of the 512-d node embeddings".  The reference is single-process (SURVEY
+section 2: no collectives anywhere), so every exchange below is new:
+
+  rank p owns rows [p*R, min(N, (p+1)*R)), R = ceil(N/P) (contiguous, so the gathered buffers are
+  in global row order: buffer row == global node id; the CSR, x and the truth are replicated).
+  forward:  h_p = x_p W^T (MFMA)  -> all_gather(h)              [N, 512] fp32, 41 MB at N=20000
+            a_src, a_dst for all rows from the gathered h (one cheap pass, no collective)
+            GAT aggregation for own rows -> MLP tail on own rows -> all_gather(coords) [N, 3]
+            fused distance/MSE over this rank's share of the upper-triangle tiles
+            all_reduce(loss moments fp64) + all_reduce(dcoords) ; finalize loss
+  backward: tail backward on own rows -> dout_p -> all_gather(dout)  [N, 512]
+            GAT bwd pass 1 on own rows -> all_gather(row stats: max, sum, delta, da_dst)
+            GAT bwd pass 2 on own rows -> dh_p (complete: own rows gather dout of all neighbours)
+            dW_p = dh_p^T x_p, datt/dbias partial -> all_reduce(one flat fp32 grad buffer)
+            identical Adam step on every rank (weights stay replicated).
+Strong scaling: the step is the same whole-graph step as on one GPU; results equal the 1-GPU
+step up to the summation order of the all-reduces (tests/test_dist_gloo.py).
+
+The trainer only talks to a kernel object (``hicgat.kernels.HipKernels`` in production), so the
+partitioning and collectives are testable on CPU with gloo and a torch stand-in.
+"""
+import torch
+import torch.distributed as dist
+
+from .optim import FlatAdam
+
+
+def _all_gather(out, inp, group):
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, inp, group=group)
+    else:
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
+
+
+class ShardedTrainer:
+    def __init__(self, model, x, adj, truth, lr=1e-3, kind="mse", group=None, kern=None):
+        if kern is None:
+            from .kernels import default
+            kern = default()
+        self.K = kern
+        self.model = model
+        self.group = group
+        self.P = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.kind = {"mse": 0, "combined": 1}[kind]
+        N = x.shape[0]
+        P = self.P
+        R = (N + P - 1) // P
+        self.N, self.R = N, R
+        self.r0 = min(N, self.rank * R)
+        self.r1 = min(N, self.r0 + R)
+        self.local_rows = self.r1 - self.r0
+        dev = x.device
+        conv = model.conv
+        self.W, self.att_l, self.att_r, self.bias = conv.lin_l.weight, conv.att_l, conv.att_r, conv.bias
+        self.ns = conv.negative_slope
+        self.H = conv.heads
+        D = conv.heads * conv.out_channels
+        self.x_loc = x[self.r0:self.r1].contiguous().float()
+        self.rowptr, self.col = adj.rowptr32, adj.col32
+        rp = self.rowptr
+        self.local_nnz = int(rp[self.r1].item() - rp[self.r0].item())
+        self.truth = truth
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.h_in = torch.zeros((R, D), **f32)
+        self.h = torch.zeros((P * R, D), **f32)
+        self.out = torch.zeros((P * R, D), **f32)
+        self.dout_in = torch.zeros((R, D), **f32)
+        self.dout = torch.zeros((P * R, D), **f32)
+        self.dh = torch.zeros((P * R, D), **f32)
+        self.da_src = torch.zeros((P * R, self.H), **f32)
+        self.rs = torch.zeros((P * R, 4 * self.H), **f32)
+        self.rs_in = torch.zeros((R, 4 * self.H), **f32)
+        self.rs_full = torch.zeros((P * R, 4 * self.H), **f32)
+        self.c_in = torch.zeros((R, 3), **f32)
+        self.coords = torch.zeros((P * R, 3), **f32)
+        self.dcoords = torch.zeros((N, 3), **f32)
+        self.stats = torch.zeros(10, dtype=torch.float64, device=dev)
+        self.loss = torch.zeros((), **f32)
+        T = kern.num_tiles(N)
+        self.t0 = T * self.rank // P
+        self.t1 = T * (self.rank + 1) // P
+        self.opt = FlatAdam(model.parameters(), lr=lr, kern=kern)
+
+    def step(self):
+        K, g, r0, r1, N = self.K, self.group, self.r0, self.r1, self.N
+        n_loc = r1 - r0
+        self.opt.zero_grad()
+        self.model.train()
+        # ---- forward ------------------------------------------------------------------------
+        h_loc, _, _ = K.linear_att(self.x_loc, self.W.detach(), self.att_l.detach(), self.att_r.detach())
+        self.h_in[:n_loc].copy_(h_loc)
+        _all_gather(self.h, self.h_in, g)
+        a_src, a_dst = K.att_logits(self.h, self.att_l.detach(), self.att_r.detach())
+        K.agg_fwd(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.out,
+                  self.rs)
+        o = self.out[r0:r1].detach().requires_grad_(True)
+        coords_loc = self.model.tail(o)
+        self.c_in[:n_loc].copy_(coords_loc.detach())
+        _all_gather(self.coords, self.c_in, g)
+        coords = self.coords[:N]
+        K.fused_loss(coords, self.truth.buf, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords)
+        dist.all_reduce(self.stats[:6], group=g)
+        dist.all_reduce(self.dcoords, group=g)
+        K.loss_finalize(self.truth.buf, N, self.kind, self.stats, self.loss)
+        # ---- backward -----------------------------------------------------------------------
+        coords_loc.backward(self.dcoords[r0:r1])
+        self.dout_in[:n_loc].copy_(o.grad)
+        _all_gather(self.dout, self.dout_in, g)
+        K.agg_bwd_dst(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.dout, self.ns, self.rs)
+        self.rs_in[:n_loc].copy_(self.rs[r0:r1])
+        _all_gather(self.rs_full, self.rs_in, g)
+        K.agg_bwd_src(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.rs_full, self.dout,
+                      self.att_l.detach(), self.att_r.detach(), self.ns, self.dh, self.da_src)
+        datt_l, datt_r, dbias = K.param_grad(self.h[r0:r1], self.dout[r0:r1], self.da_src[r0:r1],
+                                             self.rs_full[r0:r1], self.H)
+        with torch.no_grad():
+            self.W.grad.addmm_(self.dh[r0:r1].t(), self.x_loc)
+            self.att_l.grad.add_(datt_l.view_as(self.att_l))
+            self.att_r.grad.add_(datt_r.view_as(self.att_r))
+            if self.bias is not None:
+                self.bias.grad.add_(dbias)
+        dist.all_reduce(self.opt.grad, group=g)
+        self.opt.step()
+        return self.loss, self.stats, coords

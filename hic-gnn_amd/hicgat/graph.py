@@ -22,8 +22,10 @@ def convert_to_matrix(adj):
     """utils.py:10-26: (bin_i, bin_j, count) list -> dense symmetric matrix, zero rows removed.
 
     Bins are ranked among the unique ids (``np.argwhere(adj[k,0] == idx)``), later repeats of a
-    pair overwrite earlier ones, ``triu(mat) + tril(mat.T, 1)`` mirrors the upper triangle and
-    every all-zero column (and the same rows) is deleted."""
+    pair overwrite earlier ones, ``triu(mat) + tril(mat.T, 1)`` is formed exactly as the reference
+    does (``tril(., 1)`` also keeps the first super-diagonal, so the diagonal doubles and a list
+    with lower-triangle entries gives an asymmetric matrix) and every all-zero column (and the
+    same rows) is deleted."""
     adj = np.asarray(adj, dtype=np.float64)
     ids = np.unique(np.concatenate((adj[:, 0], adj[:, 1])))
     mat = np.zeros((len(ids), len(ids)))

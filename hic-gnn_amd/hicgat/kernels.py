@@ -1,0 +1,151 @@
+"""Row-level launchers of the libhicgat.so kernels (one method per C-ABI entry point family).
+
+``HipKernels`` is what the product runs.  Every method takes and returns device tensors and is
+stream-ordered on torch's current stream; the ``timed`` names feed bench.py's live roofline.
+The distributed trainer (``hicgat.dist``) is written against this interface only, so its
+partitioning / collective logic can be exercised on CPU in tests with a stand-in object.
+"""
+import torch
+
+from . import _lib
+
+# name -> list of (start, end) torch.cuda.Event pairs recorded around launches (bench.py)
+TIMERS = None
+
+
+class _timed:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if TIMERS is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *a):
+        if TIMERS is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            TIMERS.setdefault(self.name, []).append((self.e0, e1))
+
+
+P = _lib.ptr
+
+
+class HipKernels:
+    """The MI355X implementation of the kernel interface."""
+
+    def __init__(self):
+        self.lib = _lib.lib()
+
+    # -- a2 ---------------------------------------------------------------------------------------
+    def linear_att(self, x, W, att_l, att_r):
+        N, F = x.shape
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        h = torch.empty((N, H * C), dtype=torch.float32, device=x.device)
+        a_src = torch.empty((N, H), dtype=torch.float32, device=x.device)
+        a_dst = torch.empty_like(a_src)
+        with _timed("gat_linear_att"):
+            _lib.check(self.lib.hicgat_gat_linear_att(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(h), P(a_src),
+                                                      P(a_dst), _lib.stream(x.device)), "hicgat_gat_linear_att")
+        return h, a_src, a_dst
+
+    def att_logits(self, h, att_l, att_r):
+        N = h.shape[0]
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        a_src = torch.empty((N, H), dtype=torch.float32, device=h.device)
+        a_dst = torch.empty_like(a_src)
+        _lib.check(self.lib.hicgat_gat_att_logits(P(h), P(att_l), P(att_r), N, H, C, P(a_src), P(a_dst),
+                                                  _lib.stream(h.device)), "hicgat_gat_att_logits")
+        return a_src, a_dst
+
+    # -- a4 + a5 ----------------------------------------------------------------------------------
+    def agg_fwd(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats):
+        N = h.shape[0]
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        with _timed("gat_agg_fwd"):
+            _lib.check(self.lib.hicgat_gat_agg_fwd(P(rowptr), P(col), N, col.numel(), H, C, r0, r1, P(h), P(a_src),
+                                                   P(a_dst), P(bias), float(ns), P(out), P(row_stats),
+                                                   _lib.stream(h.device)), "hicgat_gat_agg_fwd")
+
+    def agg_bwd_dst(self, rowptr, col, r0, r1, h, a_src, a_dst, dout, ns, row_stats):
+        N = h.shape[0]
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        with _timed("gat_agg_bwd_dst"):
+            _lib.check(self.lib.hicgat_gat_agg_bwd_dst(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
+                                                       P(a_dst), P(dout), float(ns), P(row_stats),
+                                                       _lib.stream(h.device)), "hicgat_gat_agg_bwd_dst")
+
+    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src):
+        N = h.shape[0]
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        with _timed("gat_agg_bwd_src"):
+            _lib.check(self.lib.hicgat_gat_agg_bwd_src(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
+                                                       P(a_dst), P(row_stats), P(dout), P(att_l), P(att_r),
+                                                       float(ns), P(dh), P(da_src), _lib.stream(h.device)),
+                       "hicgat_gat_agg_bwd_src")
+
+    def param_grad(self, h, dout, da_src, row_stats, H):
+        """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D])."""
+        N, D = h.shape
+        C = D // H
+        dev = h.device
+        datt_l = torch.empty(D, dtype=torch.float32, device=dev)
+        datt_r = torch.empty_like(datt_l)
+        dbias = torch.empty_like(datt_l)
+        ws = _lib.workspace(self.lib.hicgat_gat_param_grad_workspace_bytes(N, D), dev)
+        _lib.check(self.lib.hicgat_gat_param_grad(P(h), P(dout), P(da_src), P(row_stats), N, H, C, P(datt_l),
+                                                  P(datt_r), P(dbias), P(ws), ws.numel(), _lib.stream(dev)),
+                   "hicgat_gat_param_grad")
+        return datt_l, datt_r, dbias
+
+    # -- a7..a9 -----------------------------------------------------------------------------------
+    def num_tiles(self, n):
+        return int(self.lib.hicgat_pairdist_num_tiles(n, 0))
+
+    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords):
+        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, 1), coords.device)
+        with _timed("pairdist_mse_fused"):
+            _lib.check(self.lib.hicgat_pairdist_mse_fused(P(coords), P(tbuf), n, tbuf.shape[1], int(t0), int(t1),
+                                                          int(kind), P(stats), P(loss), P(dcoords), P(ws),
+                                                          ws.numel(), _lib.stream(coords.device)),
+                       "hicgat_pairdist_mse_fused")
+
+    def loss_finalize(self, tbuf, n, kind, stats, loss):
+        _lib.check(self.lib.hicgat_pairdist_finalize(P(tbuf), n, tbuf.shape[1], int(kind), P(stats), P(loss),
+                                                     _lib.stream(tbuf.device)), "hicgat_pairdist_finalize")
+
+    def pairdist_fwd(self, coords):
+        n = coords.shape[0]
+        D = torch.empty((n, n), dtype=torch.float32, device=coords.device)
+        _lib.check(self.lib.hicgat_pairdist_fwd(P(coords), n, P(D), n, _lib.stream(coords.device)),
+                   "hicgat_pairdist_fwd")
+        return D
+
+    def pairdist_bwd(self, coords, G):
+        n = coords.shape[0]
+        dc = torch.empty_like(coords)
+        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, 0), coords.device)
+        _lib.check(self.lib.hicgat_pairdist_bwd(P(coords), P(G), n, G.shape[1], P(dc), P(ws), ws.numel(),
+                                                _lib.stream(coords.device)), "hicgat_pairdist_bwd")
+        return dc
+
+    # -- a10 --------------------------------------------------------------------------------------
+    def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
+        with _timed("adam"):
+            _lib.check(self.lib.hicgat_adam_step(P(flat), P(grad), P(m), P(v), int(n), float(lr), float(b1),
+                                                 float(b2), float(eps), int(step), _lib.stream(flat.device)),
+                       "hicgat_adam_step")
+
+
+_default = None
+
+
+def default():
+    global _default
+    if _default is None:
+        _default = HipKernels()
+    return _default

@@ -7,27 +7,7 @@
 """
 import torch
 
-from . import _lib
-
-# Optional live kernel timing (bench.py): name -> list of (start, end) torch.cuda.Event pairs,
-# recorded on the stream each kernel is launched on.
-TIMERS = None
-
-
-class _timed:
-    def __init__(self, name):
-        self.name = name
-
-    def __enter__(self):
-        if TIMERS is not None:
-            self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
-
-    def __exit__(self, *a):
-        if TIMERS is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            TIMERS.setdefault(self.name, []).append((self.e0, e1))
+from . import _lib, kernels
 
 
 def _dev_check(*ts):
@@ -39,70 +19,38 @@ def _dev_check(*ts):
 class _GATConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, att_l, att_r, bias, rowptr, col, negative_slope):
-        lib = _lib.lib()
+        _lib.lib()
         _dev_check(x, W, att_l, att_r, bias, rowptr, col)
-        x = x.contiguous()
+        K = kernels.default()
+        x = x.contiguous().float()
         W = W.contiguous()
-        N, F = x.shape
-        H, C = att_l.shape[-2], att_l.shape[-1]
-        D = H * C
-        dev = x.device
-        s = _lib.stream(dev)
-        h = torch.empty((N, D), dtype=torch.float32, device=dev)
-        a_src = torch.empty((N, H), dtype=torch.float32, device=dev)
-        a_dst = torch.empty_like(a_src)
         al = att_l.contiguous()
         ar = att_r.contiguous()
-        with _timed("gat_linear_att"):
-            _lib.check(lib.hicgat_gat_linear_att(_lib.ptr(x), _lib.ptr(W), _lib.ptr(al), _lib.ptr(ar), N, F,
-                                                 H, C, _lib.ptr(h), _lib.ptr(a_src), _lib.ptr(a_dst), s),
-                       "hicgat_gat_linear_att")
-        b = bias if bias is not None else torch.zeros(D, dtype=torch.float32, device=dev)
-        out = torch.empty((N, D), dtype=torch.float32, device=dev)
-        rmax = torch.empty((N, H), dtype=torch.float32, device=dev)
-        rsum = torch.empty_like(rmax)
-        with _timed("gat_agg_fwd"):
-            _lib.check(lib.hicgat_gat_agg_fwd(_lib.ptr(rowptr), _lib.ptr(col), N, col.numel(), H, C,
-                                              _lib.ptr(h), _lib.ptr(a_src), _lib.ptr(a_dst), _lib.ptr(b),
-                                              float(negative_slope), _lib.ptr(out), _lib.ptr(rmax),
-                                              _lib.ptr(rsum), s), "hicgat_gat_agg_fwd")
-        ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, rmax, rsum, rowptr, col)
+        N = x.shape[0]
+        H = al.shape[-2]
+        h, a_src, a_dst = K.linear_att(x, W, al, ar)
+        D = h.shape[1]
+        b = bias if bias is not None else torch.zeros(D, dtype=torch.float32, device=x.device)
+        out = torch.empty((N, D), dtype=torch.float32, device=x.device)
+        row_stats = torch.empty((N, 4 * H), dtype=torch.float32, device=x.device)
+        K.agg_fwd(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, out, row_stats)
+        ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col)
         ctx.has_bias = bias is not None
         ctx.ns = float(negative_slope)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _lib.lib()
-        x, W, al, ar, h, a_src, a_dst, rmax, rsum, rowptr, col = ctx.saved_tensors
+        K = kernels.default()
+        x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col = ctx.saved_tensors
         dout = dout.contiguous()
-        N, F = x.shape
-        H, C = al.shape[-2], al.shape[-1]
-        D = H * C
-        dev = x.device
-        s = _lib.stream(dev)
-        delta = torch.empty((N, H), dtype=torch.float32, device=dev)
-        da_dst = torch.empty_like(delta)
-        with _timed("gat_agg_bwd_dst"):
-            _lib.check(lib.hicgat_gat_agg_bwd_dst(_lib.ptr(rowptr), _lib.ptr(col), N, H, C, _lib.ptr(h),
-                                                  _lib.ptr(a_src), _lib.ptr(a_dst), _lib.ptr(rmax),
-                                                  _lib.ptr(rsum), _lib.ptr(dout), ctx.ns, _lib.ptr(delta),
-                                                  _lib.ptr(da_dst), s), "hicgat_gat_agg_bwd_dst")
-        dh = torch.empty((N, D), dtype=torch.float32, device=dev)
-        da_src = torch.empty_like(delta)
-        with _timed("gat_agg_bwd_src"):
-            _lib.check(lib.hicgat_gat_agg_bwd_src(_lib.ptr(rowptr), _lib.ptr(col), N, H, C, _lib.ptr(h),
-                                                  _lib.ptr(a_src), _lib.ptr(a_dst), _lib.ptr(rmax),
-                                                  _lib.ptr(rsum), _lib.ptr(delta), _lib.ptr(da_dst),
-                                                  _lib.ptr(dout), _lib.ptr(al), _lib.ptr(ar), ctx.ns,
-                                                  _lib.ptr(dh), _lib.ptr(da_src), s), "hicgat_gat_agg_bwd_src")
-        datt_l = torch.empty((D,), dtype=torch.float32, device=dev)
-        datt_r = torch.empty_like(datt_l)
-        dbias = torch.empty_like(datt_l)
-        ws = _lib.workspace(lib.hicgat_gat_param_grad_workspace_bytes(N, D), dev)
-        _lib.check(lib.hicgat_gat_param_grad(_lib.ptr(h), _lib.ptr(dout), _lib.ptr(da_src), _lib.ptr(da_dst),
-                                             N, H, C, _lib.ptr(datt_l), _lib.ptr(datt_r), _lib.ptr(dbias),
-                                             _lib.ptr(ws), ws.numel(), s), "hicgat_gat_param_grad")
+        N = x.shape[0]
+        H = al.shape[-2]
+        K.agg_bwd_dst(rowptr, col, 0, N, h, a_src, a_dst, dout, ctx.ns, row_stats)
+        dh = torch.empty_like(h)
+        da_src = torch.empty_like(a_src)
+        K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+        datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
         dW = dh.t().mm(x) if ctx.needs_input_grad[1] else None
         dx = dh.mm(W) if ctx.needs_input_grad[0] else None
         return (dx, dW, datt_l.view(al.shape), datt_r.view(ar.shape),
@@ -118,27 +66,16 @@ def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2):
 class _PairDistFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, coords):
-        lib = _lib.lib()
+        _lib.lib()
         _dev_check(coords)
         c = coords.contiguous().float()
-        n = c.shape[0]
-        D = torch.empty((n, n), dtype=torch.float32, device=c.device)
-        _lib.check(lib.hicgat_pairdist_fwd(_lib.ptr(c), n, _lib.ptr(D), n, _lib.stream(c.device)),
-                   "hicgat_pairdist_fwd")
         ctx.save_for_backward(c)
-        return D
+        return kernels.default().pairdist_fwd(c)
 
     @staticmethod
     def backward(ctx, dD):
-        lib = _lib.lib()
         (c,) = ctx.saved_tensors
-        n = c.shape[0]
-        g = dD.contiguous().float()
-        dc = torch.empty_like(c)
-        ws = _lib.workspace(lib.hicgat_pairdist_workspace_bytes(n, 0), c.device)
-        _lib.check(lib.hicgat_pairdist_bwd(_lib.ptr(c), _lib.ptr(g), n, n, _lib.ptr(dc), _lib.ptr(ws),
-                                           ws.numel(), _lib.stream(c.device)), "hicgat_pairdist_bwd")
-        return dc
+        return kernels.default().pairdist_bwd(c, dD.contiguous().float())
 
 
 def pairwise_dist(coords):
@@ -149,16 +86,10 @@ def pairwise_dist(coords):
 class _FusedLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, coords, tbuf, n, loss_kind, tile_begin, tile_end, stats):
-        lib = _lib.lib()
         c = coords.contiguous().float()
         dc = torch.empty_like(c)
         loss = torch.empty((), dtype=torch.float32, device=c.device)
-        ws = _lib.workspace(lib.hicgat_pairdist_workspace_bytes(n, 1), c.device)
-        with _timed("pairdist_mse_fused"):
-            _lib.check(lib.hicgat_pairdist_mse_fused(_lib.ptr(c), _lib.ptr(tbuf), n, tbuf.shape[1], tile_begin,
-                                                     tile_end, loss_kind, _lib.ptr(stats), _lib.ptr(loss),
-                                                     _lib.ptr(dc), _lib.ptr(ws), ws.numel(),
-                                                     _lib.stream(c.device)), "hicgat_pairdist_mse_fused")
+        kernels.default().fused_loss(c, tbuf, n, loss_kind, tile_begin, tile_end, stats, loss, dc)
         ctx.save_for_backward(dc)
         return loss
 
@@ -175,6 +106,8 @@ def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
 
     ``truth`` is a ``graph.Truth`` (symmetric).  ``stats`` (float64 [10], device) receives the
     moments, mse, r, alpha and total (see include/hicgat.h)."""
+    _lib.lib()
+    _dev_check(coords)
     if not truth.symmetric:
         raise NotImplementedError("fused loss needs a symmetric truth matrix; use pairwise_dist + MSELoss")
     if stats is None:

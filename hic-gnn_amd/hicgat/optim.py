@@ -7,11 +7,12 @@ lin_l / lin_r) are one tensor and appear once, as in ``model.parameters()``.
 """
 import torch
 
-from . import _lib
+from . import kernels
 
 
 class FlatAdam:
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, kern=None):
+        self.kern = kern
         self.params = [p for p in params if p.requires_grad]
         dev = self.params[0].device
         n = sum(p.numel() for p in self.params)
@@ -41,12 +42,9 @@ class FlatAdam:
     @torch.no_grad()
     def step(self):
         self.step_count += 1
-        lib = _lib.lib()
-        _lib.check(lib.hicgat_adam_step(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.exp_avg),
-                                        _lib.ptr(self.exp_avg_sq), self.numel, float(self.lr),
-                                        float(self.betas[0]), float(self.betas[1]), float(self.eps),
-                                        self.step_count, _lib.stream(self.flat.device)),
-                   "hicgat_adam_step")
+        kern = self.kern if self.kern is not None else kernels.default()
+        kern.adam(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.lr, self.betas[0],
+                  self.betas[1], self.eps, self.step_count)
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),

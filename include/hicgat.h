@@ -74,36 +74,43 @@ int hicgat_gat_att_logits(const float *h, const float *att_src, const float *att
  *   e_ij = leaky_relu(a_src[j] + a_dst[i], neg_slope)
  *   alpha_ij = exp(e_ij - max_i) / (sum_i + 1e-16)        (torch_geometric.utils.softmax, ptr path)
  *   out[i] = sum_j alpha_ij * h[j] + bias                  (segment_csr sum; concat=True)
- * Saves row_max/row_sum [N, H] for the backward.  Fast path: H*C == 512 with C % 256 == 0 or
- * H == 1..8 with C % 4 == 0 (generic path otherwise). */
+ * Only rows [row_begin, row_end) are computed (a rank's destination shard; 0..N on one GPU);
+ * every per-row array is indexed by the GLOBAL row id: h, a_src, a_dst [N, .] (the neighbour
+ * rows of the shard must be present), out [N, H*C] (rows of the range written),
+ * row_stats [N, 4H] = (max[H], sum[H], delta[H], da_dst[H]) -- max/sum written here, delta/da_dst
+ * by hicgat_gat_agg_bwd_dst.  Supported: H == 2, C == 256 (the GATConv(512, 256, heads=2) of
+ * models.py:619); other shapes return HICGAT_EUNSUPPORTED. */
 int hicgat_gat_agg_fwd(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
-                       const float *h, const float *a_src, const float *a_dst, const float *bias,
-                       float neg_slope, float *out, float *row_max, float *row_sum,
-                       hicgat_stream_t stream);
+                       int row_begin, int row_end, const float *h, const float *a_src,
+                       const float *a_dst, const float *bias, float neg_slope, float *out,
+                       float *row_stats, hicgat_stream_t stream);
 
 /* ---- a10 (part): backward of a4+a5 ----------------------------------------------------------
- * Pass 1 (destination side, row i):  g_ij = <dout[i,h,:], h[j,h,:]>,
- *   delta[i,h] = sum_j alpha_ij g_ij,  da_dst[i,h] = sum_j alpha_ij lrelu'(e_ij) (g_ij - delta[i,h]).
- * Pass 2 (source side, row r; symmetric graph so N(r) lists every i that has r as a neighbour):
+ * Pass 1 (destination side, rows of the range):  g_ij = <dout[i,h,:], h[j,h,:]>,
+ *   delta[i,h] = sum_j alpha_ij g_ij,  da_dst[i,h] = sum_j alpha_ij lrelu'(e_ij) (g_ij - delta[i,h])
+ *   -> row_stats[i, 2H..4H).
+ * Pass 2 (source side, rows r of the range; the graph is symmetric so N(r) lists every i that
+ *   has r as a neighbour; needs dout, row_stats of all those i):
  *   dh[r] = sum_i alpha_ir dout[i] + da_src[r] (x) att_l + da_dst[r] (x) att_r,
  *   da_src[r,h] = sum_i alpha_ir lrelu'(e_ir) (g_ir - delta[i,h]).
  * Requires a structurally symmetric CSR (utils.py:71 to_symmetric guarantees it). */
 int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
-                           const float *h, const float *a_src, const float *a_dst,
-                           const float *row_max, const float *row_sum, const float *dout,
-                           float neg_slope, float *delta, float *da_dst, hicgat_stream_t stream);
+                           int row_begin, int row_end, const float *h, const float *a_src,
+                           const float *a_dst, const float *dout, float neg_slope,
+                           float *row_stats, hicgat_stream_t stream);
 int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
-                           const float *h, const float *a_src, const float *a_dst,
-                           const float *row_max, const float *row_sum, const float *delta,
-                           const float *da_dst, const float *dout, const float *att_src,
-                           const float *att_dst, float neg_slope, float *dh, float *da_src,
-                           hicgat_stream_t stream);
-/* Column reductions for the GATConv parameter gradients (deterministic, two-stage):
- *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with da_dst;
+                           int row_begin, int row_end, const float *h, const float *a_src,
+                           const float *a_dst, const float *row_stats, const float *dout,
+                           const float *att_src, const float *att_dst, float neg_slope, float *dh,
+                           float *da_src, hicgat_stream_t stream);
+/* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
+ * shard's first row for a partial sum; deterministic, two-stage):
+ *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;
  *   dbias[c] = sum_n dout[n,c].  workspace: hicgat_gat_param_grad_workspace_bytes(N, H*C). */
-int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src, const float *da_dst,
-                          int N, int H, int C, float *datt_src, float *datt_dst, float *dbias,
-                          void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
+                          const float *row_stats, int N, int H, int C, float *datt_src,
+                          float *datt_dst, float *dbias, void *workspace, size_t workspace_bytes,
+                          hicgat_stream_t stream);
 size_t hicgat_gat_param_grad_workspace_bytes(int N, int D);
 
 /* ---- a7: torch.cdist(c, c, p=2) (models.py:661) and its backward -----------------------------

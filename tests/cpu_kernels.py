@@ -1,0 +1,155 @@
+"""Torch-CPU stand-in for ``hicgat.kernels.HipKernels`` (TEST INFRASTRUCTURE ONLY).
+
+Implements every kernel contract of include/hicgat.h with plain torch ops on CPU tensors, so that
+``hicgat.dist.ShardedTrainer``'s partitioning and collectives can run under gloo in CI.  The math
+follows the oracle (PyG 1.7.2 semantics); accumulation is float64 where it is cheap, so the
+sharded-vs-single comparison isolates the bookkeeping, not rounding.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from oracle import loop as ol
+
+BT = 128
+
+
+def _rows(rowptr, r0, r1):
+    rp = rowptr.long()
+    deg = rp[r0 + 1:r1 + 1] - rp[r0:r1]
+    row = torch.repeat_interleave(torch.arange(r0, r1), deg)
+    col_idx = torch.arange(int(rp[r0]), int(rp[r1]))
+    return row, col_idx
+
+
+def _tri(I, J, nb):
+    return I * nb - I * (I - 1) // 2 + (J - I)
+
+
+class CpuKernels:
+    def linear_att(self, x, W, att_l, att_r):
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        h = (x.double() @ W.double().t()).float()
+        hv = h.view(-1, H, C).double()
+        return h, (hv * att_l.double()).sum(-1).float(), (hv * att_r.double()).sum(-1).float()
+
+    def att_logits(self, h, att_l, att_r):
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        hv = h.view(-1, H, C).double()
+        return (hv * att_l.double()).sum(-1).float(), (hv * att_r.double()).sum(-1).float()
+
+    def agg_fwd(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats):
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        e = F.leaky_relu(a_src[j] + a_dst[row], ns)
+        n = r1 - r0
+        idx = (row - r0).view(-1, 1).expand_as(e)
+        m = torch.full((n, H), float("-inf")).scatter_reduce(0, idx, e, reduce="amax", include_self=True)
+        u = torch.exp(e - m[row - r0])
+        s = torch.zeros((n, H)).index_add(0, row - r0, u)
+        al = u / (s[row - r0] + 1e-16)
+        msg = h[j].view(-1, H, C).double() * al.double().unsqueeze(-1)
+        agg = torch.zeros((n, H, C), dtype=torch.float64).index_add(0, row - r0, msg)
+        out[r0:r1] = (agg.view(n, H * C) + bias.double()).float()
+        row_stats[r0:r1, 0:H] = m
+        row_stats[r0:r1, H:2 * H] = s
+
+    def _alpha(self, a_src, a_dst, row_stats, i, j, ns, H):
+        e = a_src[j] + a_dst[i]
+        m = row_stats[i, 0:H]
+        s = row_stats[i, H:2 * H]
+        al = torch.exp(F.leaky_relu(e, ns) - m) / (s + 1e-16)
+        lp = torch.where(e > 0, torch.ones_like(e), torch.full_like(e, ns))
+        return al.double(), lp.double()
+
+    def agg_bwd_dst(self, rowptr, col, r0, r1, h, a_src, a_dst, dout, ns, row_stats):
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        al, lp = self._alpha(a_src, a_dst, row_stats, row, j, ns, H)
+        gij = (dout[row].view(-1, H, C).double() * h[j].view(-1, H, C).double()).sum(-1)
+        n = r1 - r0
+        s1 = torch.zeros((n, H), dtype=torch.float64).index_add(0, row - r0, al * gij)
+        s2 = torch.zeros((n, H), dtype=torch.float64).index_add(0, row - r0, al * lp * gij)
+        s3 = torch.zeros((n, H), dtype=torch.float64).index_add(0, row - r0, al * lp)
+        row_stats[r0:r1, 2 * H:3 * H] = s1.float()
+        row_stats[r0:r1, 3 * H:4 * H] = (s2 - s1 * s3).float()
+
+    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src):
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        r, ei = _rows(rowptr, r0, r1)
+        i = col.long()[ei]                      # neighbours of r = rows that have r as a neighbour
+        al, lp = self._alpha(a_src, a_dst, row_stats, i, r, ns, H)
+        gir = (dout[i].view(-1, H, C).double() * h[r].view(-1, H, C).double()).sum(-1)
+        delta = row_stats[i, 2 * H:3 * H].double()
+        n = r1 - r0
+        dsrc = torch.zeros((n, H), dtype=torch.float64).index_add(0, r - r0, al * lp * (gir - delta))
+        acc = torch.zeros((n, H, C), dtype=torch.float64).index_add(
+            0, r - r0, al.unsqueeze(-1) * dout[i].view(-1, H, C).double())
+        ddst = row_stats[r0:r1, 3 * H:4 * H].double()
+        acc = acc + dsrc.unsqueeze(-1) * att_l.double() + ddst.unsqueeze(-1) * att_r.double()
+        dh[r0:r1] = acc.view(n, H * C).float()
+        da_src[r0:r1] = dsrc.float()
+
+    def param_grad(self, h, dout, da_src, row_stats, H):
+        n, D = h.shape
+        C = D // H
+        hv = h.view(n, H, C).double()
+        datt_l = (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
+        datt_r = (row_stats[:, 3 * H:4 * H].double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
+        return datt_l, datt_r, dout.double().sum(0).float()
+
+    def num_tiles(self, n):
+        nb = (n + BT - 1) // BT
+        return nb * (nb + 1) // 2
+
+    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords):
+        nb = (n + BT - 1) // BT
+        T = tbuf[:, :n].double()
+        c = coords.double()
+        iu = torch.triu_indices(n, n, 1)
+        ii, jj = iu[0], iu[1]
+        tid = _tri(ii // BT, jj // BT, nb)
+        keep = (tid >= t0) & (tid < t1)
+        ii, jj = ii[keep], jj[keep]
+        diff = c[ii] - c[jj]
+        d = diff.norm(dim=1)
+        t = T[ii, jj]
+        r = d - t
+        stats[0] = (r * r).sum()
+        stats[1] = d.sum()
+        stats[2] = (d * d).sum()
+        stats[3] = (d * t).sum()
+        stats[4] = t.sum()
+        stats[5] = (t * t).sum()
+        w = torch.where(d > 0, r / d, torch.zeros_like(d)) * (4.0 / (n * n))
+        g = torch.zeros((n, 3), dtype=torch.float64)
+        g.index_add_(0, ii, w.unsqueeze(1) * diff)
+        g.index_add_(0, jj, -w.unsqueeze(1) * diff)
+        dcoords.copy_(g.float())
+        self.loss_finalize(tbuf, n, kind, stats, loss)
+
+    def loss_finalize(self, tbuf, n, kind, stats, loss):
+        s = stats.double()
+        dg = float((torch.diagonal(tbuf[:, :n]).double() ** 2).sum())
+        mse = (2 * float(s[0]) + dg) / (n * n)
+        M = n * (n - 1) / 2
+        cov = float(s[3]) - float(s[1]) * float(s[4]) / M
+        vd = float(s[2]) - float(s[1]) ** 2 / M
+        vt = float(s[5]) - float(s[4]) ** 2 / M
+        r = cov / np.sqrt(vd * vt) if vd > 0 and vt > 0 else float("nan")
+        msef = float(np.float32(mse))
+        alpha = min(1.0, 0.1 + 1.0 / (msef + 1e-6))
+        total = float(np.float32(msef) + np.float32(alpha * (1 - r)))
+        stats[6], stats[7], stats[8], stats[9] = mse, r, alpha, total
+        loss.fill_(total if kind == 1 else msef)
+
+    def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
+        p2, m2, v2 = ol.adam_reference_step(flat.numpy(), grad.numpy(), m.numpy(), v.numpy(), step, lr, b1, b2, eps)
+        flat.copy_(torch.from_numpy(p2))
+        m.copy_(torch.from_numpy(m2))
+        v.copy_(torch.from_numpy(v2))

@@ -1,0 +1,102 @@
+"""GPU: hicgat.dist.ShardedTrainer on the HIP kernels.
+
+* 1 rank over RCCL ("nccl") vs the single-GPU autograd step (same loss, same gradients);
+* 2 ranks sharing the one GPU over gloo (CUDA tensors) vs 1 rank: the row shards, the all-gathers
+  of h / coords / dout / row stats and the gradient all-reduce give the 1-rank step.
+The 8-GPU RCCL run itself is the driver's scaling bench.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(n, dev):
+    for p in (os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hic-gnn_amd"), HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import hicgat
+    from hicgat import synth
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=3)
+    A = synth.dense_contacts(n, i, j, c, device=dev)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    truth = hicgat.Truth.from_contacts(A, 0.5)
+    x = torch.tensor(synth.features(n, seed=3), device=dev)
+    return hicgat, adj, truth, x
+
+
+def _worker(rank, world, port, backend, n, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hicgat, adj, truth, x = _inputs(n, dev)
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3)
+        loss, stats, _ = tr.step()
+        grad1 = tr.opt.grad.clone().cpu()
+        l1 = float(loss)
+        loss2, _, _ = tr.step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            torch.save({"loss": [l1, float(loss2)], "grad1": grad1, "stats": stats.cpu()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, backend, n, tmp_path):
+    out = str(tmp_path / f"{backend}{world}.pt")
+    mp.spawn(_worker, args=(world, _port(), backend, n, out), nprocs=world, join=True)
+    return torch.load(out, weights_only=True)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path):
+    n = 777
+    res = _run(1, "nccl", n, tmp_path)
+    hicgat, adj, truth, x = _inputs(n, "cuda")
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+    opt = hicgat.FlatAdam(model.parameters(), lr=1e-3)
+    loss, stats, _ = hicgat.train.train_step(model, opt, x, adj, truth)
+    assert abs(float(loss) - res["loss"][0]) <= 1e-6 * abs(float(loss))
+    g = opt.grad.cpu()
+    assert (g - res["grad1"]).abs().max().item() <= 1e-5 * g.abs().max().item()
+
+
+def test_sharded_two_ranks_equal_one_rank(tmp_path):
+    n = 777
+    one = _run(1, "gloo", n, tmp_path)
+    two = _run(2, "gloo", n, tmp_path)
+    assert abs(two["loss"][0] - one["loss"][0]) <= 1e-6 * abs(one["loss"][0])
+    assert torch.allclose(two["stats"][:8], one["stats"][:8], rtol=1e-9)
+    g1, g2 = one["grad1"], two["grad1"]
+    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
+    np.testing.assert_allclose(two["loss"], one["loss"], rtol=1e-3)

@@ -80,7 +80,9 @@ def test_cont2dist_bit_exact(case, factor, key):
     assert np.array_equal(t.cpu().numpy(), g[key])
     tr = hicgat.Truth.from_contacts(y, factor)
     assert np.array_equal(tr.dense().cpu().numpy(), g[key].astype(np.float32))
-    assert tr.symmetric and tr.ld % 128 == 0
+    assert tr.ld % 128 == 0
+    # convert_to_matrix's triu + tril(T, 1) is asymmetric when the list has lower-triangle entries
+    assert tr.symmetric == bool(np.array_equal(g[key], g[key].T))
 
 
 # ---------------------------------------------------------------- GATConv (a2, a4, a5 + bwd)
@@ -274,8 +276,30 @@ def test_adam_bit_exact_vs_torch_cpu_restatement():
 
 
 # ---------------------------------------------------------------- models vs reference fixtures
+def _oracle_exact(name, fx, g):
+    """The oracle model with the fixture's weights, distances by the exact formula."""
+    from oracle import gat as og
+    m = og.MODELS[name]()
+    m.load_state_dict({k[len("state::"):]: torch.tensor(v) for k, v in fx.items() if k.startswith("state::")})
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        adj = (torch.tensor(g["rowptr"]), torch.tensor(g["col"]))
+        out = m(torch.tensor(fx["x"]), adj)
+        torch.nn.functional.mse_loss(out.float(), torch.tensor(g["truth05"]).float()).backward()
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    return m
+
+
 @pytest.mark.parametrize("name", ["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2"])
 def test_model_matches_reference_fixture(name):
+    """Forward/backward of a reference model class (models.py) on chr19 1 mb, same weights.
+
+    The reference's torch.cdist uses the mm formula for N > 25: its distances
+    carry O(1e-4) absolute error, its MSE is off by ~5e-6 relative and its gradients carry noise
+    (dense3.bias, exactly 0 by translation invariance, comes out O(1e-6)).  The HIP path computes
+    distances exactly, so: coordinates are checked against the fixture at 1e-5; D, loss and
+    gradients against the oracle with exact distances (tight) and the fixture's loss loosely."""
     import hicgat
     fx = load_golden(f"model_{name}.npz")
     g = load_golden("graph_chr19_1mb.npz")
@@ -288,43 +312,64 @@ def test_model_matches_reference_fixture(name):
     y.fill_diagonal_(0)
     adj = hicgat.Adj.from_dense_device(y)
     x = torch.tensor(fx["x"], device=DEV)
-    out = model(x, adj)
-    # D: our cdist is exact; the reference used the mm formula -> absolute check
-    np.testing.assert_allclose(out.detach().cpu().numpy(), fx["out"], rtol=1e-5, atol=2e-5)
     coords = model.get_model(x, adj)
     np.testing.assert_allclose(coords.detach().cpu().numpy(), fx["coords"], rtol=1e-5, atol=1e-6)
+    out = model(x, adj)
+    c64 = torch.tensor(fx["coords"]).double()
+    d_exact = torch.cdist(c64, c64, compute_mode="donot_use_mm_for_euclid_dist")
+    np.testing.assert_allclose(out.detach().cpu().numpy(), d_exact.numpy(), rtol=1e-5, atol=1e-6)
     tr = hicgat.Truth.from_contacts(y, 0.5)
     loss, stats, _ = model.loss(x, adj, tr, "combined")
-    assert abs(stats[6].item() - float(fx["mse"])) <= 1e-5 * float(fx["mse"])
+    t = torch.tensor(g["truth05"])
+    mse_exact = float(torch.nn.functional.mse_loss(d_exact, t))
+    assert abs(stats[6].item() - mse_exact) <= 1e-5 * mse_exact
+    assert abs(stats[6].item() - float(fx["mse"])) <= 3e-5 * float(fx["mse"])
     assert abs(stats[7].item() - float(fx["pearson"])) < 1e-5
-    assert abs(loss.item() - float(fx["total"])) < 1e-5 * float(fx["total"])
+    assert abs(loss.item() - float(fx["total"])) < 3e-5 * float(fx["total"])
+    ref = _oracle_exact(name, fx, g)
     model.zero_grad()
     lm, _, _ = model.loss(x, adj, tr, "mse")
     lm.backward()
-    for k, p in model.named_parameters():
-        ref = fx[f"grad::{k}"]
-        assert _rel(p.grad.cpu(), ref) < 2e-4, k
+    for (k, p), pr in zip(model.named_parameters(), ref.parameters()):
+        scale = pr.grad.abs().max().item()
+        if k == "dense3.bias" or (k == "dense2.bias" and name.endswith("v2")):
+            assert p.grad.abs().max().item() < 1e-5 * max(scale, 1e-3), k   # exactly 0 in exact arithmetic
+            continue
+        assert _rel(p.grad.cpu(), pr.grad) < 2e-4, k
 
 
-def test_train_loop_tracks_reference_fixture():
-    """HiC-GNN_main.py loop, fixed K = 25: loss curve vs the reference run.  The first steps agree
-    to fp32 rounding; Adam's sign sensitivity makes later steps drift, so the
-    bound widens with the step index."""
+def test_train_loop_tracks_oracle():
+    """HiC-GNN_main.py loop, fixed K = 25 on chr19 1 mb, vs the oracle loop (exact distances,
+    deterministic): step 1 to fp32 rounding; later steps drift slowly (Adam turns rounding-level
+    gradient differences into lr-sized steps of either sign)."""
     import hicgat
+    from oracle import gat as og
+    from oracle import loop as ol
     fx = load_golden("train_GATNetSelectiveResidualsUpdated.npz")
     mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz")
     g = load_golden("graph_chr19_1mb.npz")
+    K = int(fx["steps"])
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        torch.manual_seed(0)
+        ref = og.GATNetSelectiveResidualsUpdated()
+        radj = (torch.tensor(g["rowptr"]), torch.tensor(g["col"]))
+        ref_hist = np.array(ol.train(ref, torch.tensor(mfx["x"]), radj, torch.tensor(g["truth05"]), steps=K))
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
     y = torch.tensor(g["matrix"], device=DEV)
     y.fill_diagonal_(0)
     data = hicgat.Data(x=torch.tensor(mfx["x"], device=DEV), edge_index=hicgat.Adj.from_dense_device(y), y=y)
     tr = hicgat.Truth.from_contacts(y, 0.5)
-    _, hist = hicgat.train.train(model, data, tr, steps=int(fx["steps"]))
-    ref = fx["loss"]
-    rel = np.abs(np.array(hist) - ref) / ref
-    assert rel[0] < 1e-5 and rel[1] < 1e-5 and rel[2] < 1e-4
-    assert np.all(rel < 0.05)
+    _, hist = hicgat.train.train(model, data, tr, steps=K)
+    rel = np.abs(np.array(hist) - ref_hist) / ref_hist
+    assert rel[0] < 1e-5, rel[:3]
+    assert np.all(rel[:5] < 1e-3), rel[:5]
+    assert np.all(rel < 5e-2), rel
+    # and the reference's own run (mm-formula cdist) stays within the same band
+    assert np.all(np.abs(np.array(hist) - fx["loss"]) / fx["loss"] < 5e-2)
 
 
 def test_dscc_matches_scipy():
@@ -337,9 +382,10 @@ def test_dscc_matches_scipy():
     t = torch.tensor(g["truth05"], device=DEV)
     rho = hicgat.metrics.dscc(c, t)
     iu = np.triu_indices(n, 1)
+    d_gpu = hicgat.ops.pairwise_dist(c).cpu().numpy()
+    assert abs(rho - spearmanr(g["truth05"][iu], d_gpu[iu])[0]) < 1e-12      # ranking logic, ties
     d = torch.cdist(c.cpu(), c.cpu(), compute_mode="donot_use_mm_for_euclid_dist").numpy()
-    ref = spearmanr(g["truth05"][iu], d[iu])[0]
-    assert abs(rho - ref) < 1e-9
+    assert abs(rho - spearmanr(g["truth05"][iu], d[iu])[0]) < 1e-6           # 1-ulp sqrt ties
 
 
 # ---------------------------------------------------------------- full-size properties
@@ -364,25 +410,24 @@ def test_full_size_synth20000_properties():
         hv = h.view(n, 2, 256)
         a_s = (hv * conv.att_l.double()).sum(-1)
         a_d = (hv * conv.att_r.double()).sum(-1)
-    rp = adj.rowptr32.cpu().numpy()
-    cl = adj.col32.cpu().numpy()
-    for r in np.random.default_rng(1).choice(n, 24, replace=False):
-        nb = torch.tensor(cl[rp[r]:rp[r + 1]].astype(np.int64), device=DEV)
-        e = torch.nn.functional.leaky_relu(a_s[nb] + a_d[r], 0.2)
-        al = torch.softmax(e, 0)
-        ref = (al.unsqueeze(-1) * hv[nb]).sum(0).reshape(-1) + conv.bias.double()
-        assert _rel(out[r].cpu(), ref.cpu()) < 1e-5
+        rp = adj.rowptr32.cpu().numpy()
+        cl = adj.col32.cpu().numpy()
+        for r in np.random.default_rng(1).choice(n, 24, replace=False):
+            nb = torch.tensor(cl[rp[r]:rp[r + 1]].astype(np.int64), device=DEV)
+            e = torch.nn.functional.leaky_relu(a_s[nb] + a_d[r], 0.2)
+            al = torch.softmax(e, 0)
+            ref = (al.unsqueeze(-1) * hv[nb]).sum(0).reshape(-1) + conv.bias.double()
+            assert _rel(out[r].cpu(), ref.cpu()) < 1e-5
     lib = _lib.lib()
     hconst = torch.full((n, 512), 0.75, device=DEV)
     a_s = torch.randn(n, 2, device=DEV)
     a_d = torch.randn(n, 2, device=DEV)
     bias = torch.randn(512, device=DEV)
     o = torch.empty(n, 512, device=DEV)
-    rm = torch.empty(n, 2, device=DEV)
-    rs = torch.empty(n, 2, device=DEV)
-    _lib.check(lib.hicgat_gat_agg_fwd(_lib.ptr(adj.rowptr32), _lib.ptr(adj.col32), n, nnz, 2, 256,
+    rs = torch.empty(n, 8, device=DEV)
+    _lib.check(lib.hicgat_gat_agg_fwd(_lib.ptr(adj.rowptr32), _lib.ptr(adj.col32), n, nnz, 2, 256, 0, n,
                                       _lib.ptr(hconst), _lib.ptr(a_s), _lib.ptr(a_d), _lib.ptr(bias), 0.2,
-                                      _lib.ptr(o), _lib.ptr(rm), _lib.ptr(rs), _lib.stream()), "agg")
+                                      _lib.ptr(o), _lib.ptr(rs), _lib.stream()), "agg")
     assert torch.allclose(o, 0.75 + bias.expand_as(o), rtol=0, atol=2e-6)
     tr = hicgat.Truth.from_contacts(A, 0.5)
     cc = torch.randn(n, 3, device=DEV).requires_grad_(True)
