@@ -138,7 +138,7 @@ def main():
         step = runner.step
     else:
         opt = hicgat.FlatAdam(model.parameters(), lr=1e-3)
-        stats = torch.empty(10, dtype=torch.float64, device=dev)
+        stats = torch.empty(12, dtype=torch.float64, device=dev)
 
         def step():
             return hicgat.train.train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss, stats)

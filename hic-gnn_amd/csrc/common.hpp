@@ -33,15 +33,16 @@ __device__ __forceinline__ float half_wave_sum(float v) {
   return v;
 }
 
-// Correctly rounded square roots.  v_sqrt_f32 / the default f64 lowering are within 1 ulp but
-// not IEEE-exact; torch's CPU sqrt (and pow(x, 0.5)) is.  Given y within 1 ulp of sqrt(x), the
-// neighbour y-1ulp is the answer iff x <= (y-1ulp)*y, and y+1ulp iff x > (y+1ulp)*y (the exact
-// products sit inside the rounding midpoints by far less than one ulp of x).
+// Correctly rounded square roots.  v_sqrt_f32 and the default f64 lowering are not IEEE-exact;
+// torch's CPU sqrt (and pow(x, 0.5)) is.  One Newton step brings the estimate y within 1 ulp;
+// then y-1ulp is the answer iff x <= (y-1ulp)*y, y+1ulp iff x > (y+1ulp)*y (the exact products
+// differ from the rounding midpoints' squares by far less than one ulp of x).
 __device__ __forceinline__ float sqrt_rn_f32(float x) {
   if (!(x > 0.f) || x == INFINITY) return __builtin_sqrtf(x);
   const bool tiny = x < 0x1.0p-96f;
   const float xs = tiny ? x * 0x1.0p+32f : x;
   float y = __builtin_amdgcn_sqrtf(xs);
+  y = fmaf(fmaf(-y, y, xs), 0.5f / y, y);
   const float yd = __int_as_float(__float_as_int(y) - 1), yu = __int_as_float(__float_as_int(y) + 1);
   if (fmaf(-yd, y, xs) <= 0.f) y = yd;
   else if (fmaf(-yu, y, xs) > 0.f) y = yu;
@@ -49,12 +50,16 @@ __device__ __forceinline__ float sqrt_rn_f32(float x) {
 }
 __device__ __forceinline__ double sqrt_rn_f64(double x) {
   if (!(x > 0.0) || x == (double)INFINITY) return __builtin_sqrt(x);
-  double y = __builtin_sqrt(x);
+  const bool tiny = x < 0x1.0p-900;
+  const double xs = tiny ? x * 0x1.0p+256 : x;
+  double y = (double)__builtin_amdgcn_sqrtf((float)xs);   // ~24-bit start (xs is in float range)
+  if (xs > 3.0e38 || xs < 1.0e-37) y = __builtin_sqrt(xs);
+  for (int it = 0; it < 3; ++it) y = fma(fma(-y, y, xs), 0.5 / y, y);   // 24 -> 48 -> >53 bits
   const double yd = __longlong_as_double(__double_as_longlong(y) - 1);
   const double yu = __longlong_as_double(__double_as_longlong(y) + 1);
-  if (fma(-yd, y, x) <= 0.0) y = yd;
-  else if (fma(-yu, y, x) > 0.0) y = yu;
-  return y;
+  if (fma(-yd, y, xs) <= 0.0) y = yd;
+  else if (fma(-yu, y, xs) > 0.0) y = yu;
+  return tiny ? y * 0x1.0p-128 : y;
 }
 
 // torch.nn.functional.leaky_relu: x > 0 ? x : x * slope.
@@ -82,7 +87,7 @@ __device__ __forceinline__ float f4_dot(float4 a, float4 b) {
 // Cost: V-1 shuffles + 2 for the final intra-group sum (vs 6 per value for independent sums).
 template <int V>
 __device__ __forceinline__ void transpose_reduce(float (&v)[V], int lane) {
-  static_assert(V == 16 || V == 8, "transpose_reduce: V must be 8 or 16");
+  static_assert(V == 16 || V == 8 || V == 4, "transpose_reduce: V must be 4, 8 or 16");
   int mask = 32;
 #pragma unroll
   for (int n = V; n > 1; n >>= 1, mask >>= 1) {

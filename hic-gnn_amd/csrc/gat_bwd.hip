@@ -17,13 +17,25 @@
 // transpose reduce instead of 16 independent 6-step wave sums.
 #include "common.hpp"
 
+#ifndef HICGAT_BWD_U
+#define HICGAT_BWD_U 8   // neighbours gathered per inner step (2 float4 loads per lane each)
+#endif
+
 namespace hicgat {
+
+// After transpose_reduce<2U> over values [head*U + k], lane l owns head l>>5 and slot k; the
+// 64/(2U) lanes of a group hold the same sum and the first of them is the "owner".
+template <int U> struct Owner {
+  static constexpr int kShift = U == 8 ? 2 : U == 4 ? 3 : 4;
+  __device__ static int slot(int lane) { return (lane >> kShift) & (U - 1); }
+  __device__ static bool owner(int lane) { return (lane & ((1 << kShift) - 1)) == 0; }
+};
 
 __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ dout, float ns, float *__restrict__ row_stats) {
-  constexpr int U = 8;
+  constexpr int U = HICGAT_BWD_U;
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (i >= row_end) return;
@@ -31,16 +43,27 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
   const float4 d0 = g4[(size_t)i * 128 + lane], d1 = g4[(size_t)i * 128 + 64 + lane];
-  // after transpose_reduce<16> with values [head*8 + k], lane owns (head hh, neighbour slot kk)
-  const int hh = lane >> 5, kk = (lane >> 2) & 7;
-  const bool owner = (lane & 3) == 0;
-  const float adh = a_dst[2 * (size_t)i + hh];
-  const float mh = row_stats[8 * (size_t)i + hh];
-  const float denh = row_stats[8 * (size_t)i + 2 + hh] + 1e-16f;
+  const int hh = lane >> 5, kk = Owner<U>::slot(lane);
+  const bool owner = Owner<U>::owner(lane);
+  const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
+  const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];  // max0 max1 sum0 sum1
+  const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
   float S1 = 0.f, S2 = 0.f, S3 = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
-    const int j = e < end ? col[e] : i;
+    int j = i;
+    // per-edge softmax weight and leaky-relu slope of this chunk, one edge per lane (the only
+    // scattered loads of the row), later broadcast to the lane that owns each reduced dot product
+    float al0 = 0.f, al1 = 0.f, alp0 = 0.f, alp1 = 0.f;
+    if (e < end) {
+      j = col[e];
+      const float2 s = as2[j];
+      const float e0 = s.x + ad.x, e1 = s.y + ad.y;
+      al0 = expf(lrelu(e0, ns) - ms.x) / (ms.z + 1e-16f);
+      al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
+      alp0 = al0 * (e0 > 0.f ? 1.f : ns);
+      alp1 = al1 * (e1 > 0.f ? 1.f : ns);
+    }
     const int cnt = min(64, end - base);
     for (int k = 0; k < cnt; k += U) {
       float4 v0[U], v1[U];
@@ -57,14 +80,14 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
         v[U + u] = f4_dot(d1, v1[u]);
       }
       transpose_reduce<2 * U>(v, lane);
-      const int jn = __shfl(j, k + kk);
-      const float eh = a_src[2 * (size_t)jn + hh] + adh;
-      const float lp = eh > 0.f ? 1.f : ns;
-      const float al = expf(lrelu(eh, ns) - mh) / denh;
-      if (owner && k + kk < cnt) {
+      const int src = k + kk;
+      const float a0 = __shfl(al0, src), a1 = __shfl(al1, src);
+      const float p0 = __shfl(alp0, src), p1 = __shfl(alp1, src);
+      const float al = hh ? a1 : a0, alp = hh ? p1 : p0;
+      if (owner && src < cnt) {
         S1 = fmaf(al, v[0], S1);
-        S2 = fmaf(al * lp, v[0], S2);
-        S3 = fmaf(al, lp, S3);
+        S2 = fmaf(alp, v[0], S2);
+        S3 += alp;
       }
     }
   }
@@ -82,7 +105,7 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const float *__restrict__ row_stats, const float *__restrict__ dout,
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
     float *__restrict__ dh, float *__restrict__ da_src) {
-  constexpr int U = 8;
+  constexpr int U = HICGAT_BWD_U;
   const int lane = lane_id();
   const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (r >= row_end) return;
@@ -93,8 +116,8 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   const float2 asr = *reinterpret_cast<const float2 *>(a_src + 2 * (size_t)r);
   const float2 *ad2 = reinterpret_cast<const float2 *>(a_dst);
   const float4 *rs4 = reinterpret_cast<const float4 *>(row_stats);
-  const int hh = lane >> 5, kk = (lane >> 2) & 7;
-  const bool owner = (lane & 3) == 0;
+  const int hh = lane >> 5, kk = Owner<U>::slot(lane);
+  const bool owner = Owner<U>::owner(lane);
   float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
   float Sda = 0.f;
   for (int base = beg; base < end; base += 64) {
@@ -160,7 +183,7 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
 // ---- GATConv parameter gradients: deterministic two-stage column reductions over N rows. ------
 // stage 1: block b sums rows [b*R, (b+1)*R) into part[b][3][D] (datt_src, datt_dst, dbias);
 // stage 2: one thread per output column sums the partials in block order.
-constexpr int kParamBlocks = 512;
+constexpr int kParamBlocks = 128;
 
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
                                                          const float *__restrict__ dout,
@@ -188,16 +211,26 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
   }
 }
 
+// block = 64 output columns x 4 groups; group g adds partials b = g, g+4, ...; groups combined
+// in order through LDS (fixed order: bitwise reproducible).
 __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict__ part, int nblk,
                                                          int D, float *__restrict__ datt_s,
                                                          float *__restrict__ datt_d,
                                                          float *__restrict__ dbias) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 3 * D) return;
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * 3 * D + c];
-  const int which = c / D, cc = c % D;
-  (which == 0 ? datt_s : which == 1 ? datt_d : dbias)[cc] = s;
+  if (c < 3 * D) {
+    for (int b = grp; b < nblk; b += 4) s += part[(size_t)b * 3 * D + c];
+  }
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < 3 * D) {
+    const float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    const int which = c / D, cc = c % D;
+    (which == 0 ? datt_s : which == 1 ? datt_d : dbias)[cc] = t;
+  }
 }
 
 }  // namespace hicgat
@@ -263,7 +296,7 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
                        da_src, row_stats, N, H, C, rpb, part);
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;

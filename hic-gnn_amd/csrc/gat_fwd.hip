@@ -11,6 +11,10 @@
 // (a rank's destination shard); every per-row array is indexed by the global row id.
 #include "common.hpp"
 
+#ifndef HICGAT_FWD_U
+#define HICGAT_FWD_U 8   // neighbours gathered per inner step
+#endif
+
 namespace hicgat {
 
 // ---- a2: a_src[n,h] = <h[n,h,:], att_src[h,:]>, a_dst likewise (one wave per row). -------------
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ bias, float ns, float *__restrict__ out,
     float *__restrict__ row_stats) {
-  constexpr int U = 8;  // neighbours in flight per lane
+  constexpr int U = HICGAT_FWD_U;  // neighbours in flight per lane
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (i >= row_end) return;

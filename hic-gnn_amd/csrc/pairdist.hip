@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
                                                             double *__restrict__ mom) {
   __shared__ float sc[2][BT][3];
   __shared__ float4 colred[4][BT];
-  __shared__ double mred[4][6];
+  __shared__ double mred[4][7];
   const int64_t t = t0 + blockIdx.x;
   int I, J;
   if (MODE == MODE_SYM) {
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     cz[q] = sc[1][lc][2];
     ax[q] = ay[q] = az[q] = 0.f;
   }
-  float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f;
+  float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f, dg = 0.f;
   float4 *prow = part + (size_t)t * 2 * BT;
 
 #pragma unroll 1
@@ -122,10 +122,15 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float dx = rx - cx[q], dy = ry - cy[q], dz = rz - cz[q];
-      const float d = sqrtf(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
+      const float d2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+      // one v_rsq for both d and 1/d (1-2 ulp; the reference's own mm-formula cdist is far
+      // coarser); d2 == 0 (coincident points, the diagonal) gives d = w = 0
+      const float inv = d2 > 0.f ? __builtin_amdgcn_rsqf(d2) : 0.f;
+      const float d = d2 * inv;
       bool valid = gi < N && gj[q] < N;
       float w;
       if (MODE == MODE_SYM) {
+        if (valid && gi == gj[q]) dg = fmaf(tv[q], tv[q], dg);   // (D_ii - T_ii)^2 = T_ii^2
         valid = valid && (I != J || gi < gj[q]);
         const float tt = tv[q], r = d - tt;
         if (valid) {
@@ -136,10 +141,10 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
           st += tt;
           stt = fmaf(tt, tt, stt);
         }
-        w = (valid && d > 0.f) ? r / d : 0.f;
+        w = valid ? r * inv : 0.f;
       } else {
         valid = valid && gi != gj[q];
-        w = (valid && d > 0.f) ? tv[q] / d : 0.f;
+        w = valid ? tv[q] * inv : 0.f;
       }
       px = fmaf(w, dx, px);
       py = fmaf(w, dy, py);
@@ -168,14 +173,14 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     for (int q = 0; q < 8; ++q) colred[wv][tx * 4 + (q & 3) + (q >> 2) * 64] = make_float4(ax[q], ay[q], az[q], 0.f);
   }
   if (MODE == MODE_SYM) {
-    double m[6] = {L, sd, sdd, sdt, st, stt};
+    double m[7] = {L, sd, sdd, sdt, st, stt, dg};
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
+    for (int c = 0; c < 7; ++c) {
       for (int o = 32; o > 0; o >>= 1) m[c] += shfl_xor_d(m[c], o);
     }
     if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < 6; ++c) mred[wv][c] = m[c];
+      for (int c = 0; c < 7; ++c) mred[wv][c] = m[c];
     }
   }
   __syncthreads();
@@ -190,79 +195,87 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     }
     prow[BT + tid] = s;
   }
-  if (MODE == MODE_SYM && tid < 6) {
+  if (MODE == MODE_SYM && tid < 7) {
     mom[(size_t)t * 8 + tid] = ((mred[0][tid] + mred[1][tid]) + mred[2][tid]) + mred[3][tid];
   }
 }
 
 // dcoords[i] = scale * (sum of the row partials of tiles (R, *) + column partials of (*, R)).
+// Block = 64 rows x 4 groups; group g adds the tiles J = g, g+4, ... of its row, then the 4 group
+// sums are combined in group order (fixed order: bitwise reproducible).
 __global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__restrict__ part,
                                                               int N, int nb, int mode, int64_t t0,
                                                               int64_t t1, float scale,
                                                               float *__restrict__ dcoords) {
-  const int gi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= N) return;
-  const int R = gi / BT, lr = gi % BT;
+  __shared__ float4 red[4][64];
+  const int lr64 = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int gi = blockIdx.x * 64 + lr64;
   float sx = 0.f, sy = 0.f, sz = 0.f;
-  for (int J = 0; J < nb; ++J) {
-    int64_t trow, tcol;
-    if (mode == MODE_SYM) {
-      trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
-      tcol = J <= R ? tri_start(J, nb) + (R - J) : -1;
-    } else {
-      trow = (int64_t)R * nb + J;
-      tcol = (int64_t)J * nb + R;
-    }
-    if (trow >= t0 && trow < t1) {
-      const float4 p = part[(size_t)trow * 2 * BT + lr];
-      sx += p.x; sy += p.y; sz += p.z;
-    }
-    if (tcol >= t0 && tcol < t1) {
-      const float4 p = part[(size_t)tcol * 2 * BT + BT + lr];
-      sx += p.x; sy += p.y; sz += p.z;
+  if (gi < N) {
+    const int R = gi / BT, lr = gi % BT;
+    for (int J = grp; J < nb; J += 4) {
+      int64_t trow, tcol;
+      if (mode == MODE_SYM) {
+        trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
+        tcol = J <= R ? tri_start(J, nb) + (R - J) : -1;
+      } else {
+        trow = (int64_t)R * nb + J;
+        tcol = (int64_t)J * nb + R;
+      }
+      if (trow >= t0 && trow < t1) {
+        const float4 p = part[(size_t)trow * 2 * BT + lr];
+        sx += p.x; sy += p.y; sz += p.z;
+      }
+      if (tcol >= t0 && tcol < t1) {
+        const float4 p = part[(size_t)tcol * 2 * BT + BT + lr];
+        sx += p.x; sy += p.y; sz += p.z;
+      }
     }
   }
-  dcoords[3 * (size_t)gi] = sx * scale;
-  dcoords[3 * (size_t)gi + 1] = sy * scale;
-  dcoords[3 * (size_t)gi + 2] = sz * scale;
+  red[grp][lr64] = make_float4(sx, sy, sz, 0.f);
+  __syncthreads();
+  if (grp == 0 && gi < N) {
+    float4 s0 = red[0][lr64];
+#pragma unroll
+    for (int g = 1; g < 4; ++g) {
+      const float4 o = red[g][lr64];
+      s0.x += o.x; s0.y += o.y; s0.z += o.z;
+    }
+    dcoords[3 * (size_t)gi] = s0.x * scale;
+    dcoords[3 * (size_t)gi + 1] = s0.y * scale;
+    dcoords[3 * (size_t)gi + 2] = s0.z * scale;
+  }
 }
 
-// stats[0..5] = sum over tiles [t0,t1) of the tile moments (fixed order, fp64).
+// stats[0..6] = sum over tiles [t0,t1) of the tile moments (fixed order, fp64).
 __global__ __launch_bounds__(256) void moments_reduce_kernel(const double *__restrict__ mom,
                                                              int64_t t0, int64_t t1,
                                                              double *__restrict__ stats) {
-  __shared__ double red[256][6];
-  double s[6] = {0, 0, 0, 0, 0, 0};
+  __shared__ double red[256][7];
+  double s[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) {
 #pragma unroll
-    for (int c = 0; c < 6; ++c) s[c] += mom[(size_t)t * 8 + c];
+    for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
   }
 #pragma unroll
-  for (int c = 0; c < 6; ++c) red[threadIdx.x][c] = s[c];
+  for (int c = 0; c < 7; ++c) red[threadIdx.x][c] = s[c];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
 #pragma unroll
-      for (int c = 0; c < 6; ++c) red[threadIdx.x][c] += red[threadIdx.x + o][c];
+      for (int c = 0; c < 7; ++c) red[threadIdx.x][c] += red[threadIdx.x + o][c];
     }
     __syncthreads();
   }
-  if (threadIdx.x < 6) stats[threadIdx.x] = red[0][threadIdx.x];
+  if (threadIdx.x < 7) stats[threadIdx.x] = red[0][threadIdx.x];
 }
 
-// stats[6..9] and loss from stats[0..5] (+ the truth diagonal): mse, pearson r, alpha, total.
-__global__ __launch_bounds__(64) void finalize_kernel(const float *__restrict__ T, int N, int64_t ldt,
-                                                      int loss_kind, double *__restrict__ stats,
+// stats[7..10] and loss from the all-reduced moments stats[0..6]: mse, pearson r, alpha, total.
+__global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, double *__restrict__ stats,
                                                       float *__restrict__ loss) {
-  double dg = 0.0;
-  for (int i = threadIdx.x; i < N; i += 64) {
-    const double v = T[(size_t)i * ldt + i];
-    dg += v * v;
-  }
-  for (int o = 32; o > 0; o >>= 1) dg += shfl_xor_d(dg, o);
   if (threadIdx.x != 0) return;
   const double n2 = (double)N * (double)N;
-  const double mse = (2.0 * stats[0] + dg) / n2;
+  const double mse = (2.0 * stats[0] + stats[6]) / n2;
   const double M = 0.5 * (double)N * (double)(N - 1);
   const double sd = stats[1], sdd = stats[2], sdt = stats[3], st = stats[4], stt = stats[5];
   const double cov = sdt - sd * st / M, vd = sdd - sd * sd / M, vt = stt - st * st / M;
@@ -272,11 +285,11 @@ __global__ __launch_bounds__(64) void finalize_kernel(const float *__restrict__ 
   const float msef = (float)mse;
   const double alpha = fmin(1.0, 0.1 + 1.0 / ((double)msef + 1e-6));
   const float totalf = msef + (float)(alpha * (1.0 - r));
-  const double total = (double)totalf;
-  stats[6] = mse;
-  stats[7] = r;
-  stats[8] = alpha;
-  stats[9] = total;
+  stats[7] = mse;
+  stats[8] = r;
+  stats[9] = alpha;
+  stats[10] = (double)totalf;
+  stats[11] = 0.0;
   if (loss) loss[0] = loss_kind == 1 ? totalf : msef;
 }
 
@@ -348,7 +361,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false>), dim3(tiles), dim3(256), 0,
                        (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, part, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
                      dcoords);
   HICGAT_CHECK_LAUNCH();
@@ -386,7 +399,7 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
   }
   if (dcoords) {
     const float scale = (float)(4.0 / ((double)N * (double)N));
-    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0,
+    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0,
                        (hipStream_t)stream, part, N, nb, (int)MODE_SYM, tile_begin, tile_end,
                        scale, dcoords);
     HICGAT_CHECK_LAUNCH();
@@ -394,17 +407,17 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
   hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, mom,
                      tile_begin, tile_end, stats);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, T, N, ldt,
-                     loss_kind, stats, loss);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
+                     stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
-extern "C" int hicgat_pairdist_finalize(const float *T, int N, int64_t ldt, int loss_kind,
-                                        double *stats, float *loss, hicgat_stream_t stream) {
-  if (N <= 0 || !T || !stats || ldt < N) return HICGAT_EINVAL;
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, T, N, ldt,
-                     loss_kind, stats, loss);
+extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss,
+                                        hicgat_stream_t stream) {
+  if (N <= 0 || !stats || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
+                     stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhicgat.so")
+# HICGAT_LIB lets tools/kbench.py A/B an alternative build of the same ABI in one process
+LIB_PATH = os.environ.get("HICGAT_LIB", os.path.join(_HERE, "libhicgat.so"))
 
 c_int, c_i64, c_f, c_d, c_sz, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double,
                                      ctypes.c_size_t, ctypes.c_void_p)
@@ -37,7 +38,7 @@ SIGNATURES = {
     "hicgat_pairdist_bwd": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_mse_fused": (c_int, [c_p, c_p, c_int, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_p,
                                           c_p, c_sz, c_p]),
-    "hicgat_pairdist_finalize": (c_int, [c_p, c_int, c_i64, c_int, c_p, c_p, c_p]),
+    "hicgat_pairdist_finalize": (c_int, [c_int, c_int, c_p, c_p, c_p]),
     "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
     "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),

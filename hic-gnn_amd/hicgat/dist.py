@@ -78,7 +78,7 @@ class ShardedTrainer:
         self.c_in = torch.zeros((R, 3), **f32)
         self.coords = torch.zeros((P * R, 3), **f32)
         self.dcoords = torch.zeros((N, 3), **f32)
-        self.stats = torch.zeros(10, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros(12, dtype=torch.float64, device=dev)
         self.loss = torch.zeros((), **f32)
         T = kern.num_tiles(N)
         self.t0 = T * self.rank // P
@@ -103,9 +103,9 @@ class ShardedTrainer:
         _all_gather(self.coords, self.c_in, g)
         coords = self.coords[:N]
         K.fused_loss(coords, self.truth.buf, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords)
-        dist.all_reduce(self.stats[:6], group=g)
+        dist.all_reduce(self.stats[:7], group=g)
         dist.all_reduce(self.dcoords, group=g)
-        K.loss_finalize(self.truth.buf, N, self.kind, self.stats, self.loss)
+        K.loss_finalize(N, self.kind, self.stats, self.loss)
         # ---- backward -----------------------------------------------------------------------
         coords_loc.backward(self.dcoords[r0:r1])
         self.dout_in[:n_loc].copy_(o.grad)

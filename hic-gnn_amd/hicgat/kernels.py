@@ -114,9 +114,9 @@ class HipKernels:
                                                           ws.numel(), _lib.stream(coords.device)),
                        "hicgat_pairdist_mse_fused")
 
-    def loss_finalize(self, tbuf, n, kind, stats, loss):
-        _lib.check(self.lib.hicgat_pairdist_finalize(P(tbuf), n, tbuf.shape[1], int(kind), P(stats), P(loss),
-                                                     _lib.stream(tbuf.device)), "hicgat_pairdist_finalize")
+    def loss_finalize(self, n, kind, stats, loss):
+        _lib.check(self.lib.hicgat_pairdist_finalize(n, int(kind), P(stats), P(loss), _lib.stream(stats.device)),
+                   "hicgat_pairdist_finalize")
 
     def pairdist_fwd(self, coords):
         n = coords.shape[0]

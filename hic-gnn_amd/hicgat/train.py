@@ -36,7 +36,7 @@ def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_
     """Returns (optimizer, per-step loss list).  ``truth`` is a ``graph.Truth``."""
     opt = FlatAdam(model.parameters(), lr=lr)
     old, diff, hist = 1.0, 1.0, []
-    stats = torch.empty(10, dtype=torch.float64, device=data.x.device)
+    stats = torch.empty(12, dtype=torch.float64, device=data.x.device)
     while (diff > thresh if steps is None else len(hist) < steps) and len(hist) < max_steps:
         model.train()
         opt.zero_grad()

@@ -126,19 +126,18 @@ int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg,
  * pearsonr / alpha / total (HiC_GAT_generalize_directly.py:210-225).  T is the SYMMETRIC truth
  * (leading dim ldt); only upper-triangle tiles [tile_begin, tile_end) of the 128x128 tiling are
  * read (pass 0, -1 for all).  Outputs:
- *   stats[10] (float64): 0 sum_{i<j}(d-t)^2, 1 sum d, 2 sum d^2, 3 sum dt, 4 sum t, 5 sum t^2
- *     (all over i<j of the tile range), 6 mse = (2*[0] + sum_i T_ii^2)/N^2, 7 pearson r,
- *     8 alpha = min(1, 0.1 + 1/(mse + 1e-6)), 9 total = mse + alpha*(1 - r);
+ *   stats[12] (float64): 0 sum_{i<j}(d-t)^2, 1 sum d, 2 sum d^2, 3 sum dt, 4 sum t, 5 sum t^2,
+ *     6 sum_i T_ii^2 (moments 0..6 over the tile range; a multi-GPU caller all-reduces them and
+ *     calls hicgat_pairdist_finalize), 7 mse = (2*[0] + [6])/N^2, 8 pearson r over i<j,
+ *     9 alpha = min(1, 0.1 + 1/(mse + 1e-6)), 10 total = mse + alpha*(1 - r), 11 reserved;
  *   loss[1] (float32): mse (loss_kind 0) or total (loss_kind 1);
  *   dcoords [N,3] = d(mse)/dcoords restricted to the tile range (sum over ranks = full gradient).
- * stats 6..9 are only meaningful when the range covers every tile (or after an all-reduce of
- * 0..5 followed by hicgat_pairdist_finalize). workspace: hicgat_pairdist_workspace_bytes(N, 1). */
+ * workspace: hicgat_pairdist_workspace_bytes(N, 1). */
 int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
                               int64_t tile_begin, int64_t tile_end, int loss_kind, double *stats,
                               float *loss, float *dcoords, void *workspace, size_t workspace_bytes,
                               hicgat_stream_t stream);
-int hicgat_pairdist_finalize(const float *T, int N, int64_t ldt, int loss_kind, double *stats,
-                             float *loss, hicgat_stream_t stream);
+int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, hicgat_stream_t stream);
 int64_t hicgat_pairdist_num_tiles(int N, int mode);
 size_t hicgat_pairdist_workspace_bytes(int N, int mode);
 

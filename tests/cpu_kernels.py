@@ -126,17 +126,20 @@ class CpuKernels:
         stats[3] = (d * t).sum()
         stats[4] = t.sum()
         stats[5] = (t * t).sum()
+        dii = torch.arange(n)
+        dtile = _tri(dii // BT, dii // BT, nb)
+        dkeep = (dtile >= t0) & (dtile < t1)
+        stats[6] = (T[dii[dkeep], dii[dkeep]] ** 2).sum()
         w = torch.where(d > 0, r / d, torch.zeros_like(d)) * (4.0 / (n * n))
         g = torch.zeros((n, 3), dtype=torch.float64)
         g.index_add_(0, ii, w.unsqueeze(1) * diff)
         g.index_add_(0, jj, -w.unsqueeze(1) * diff)
         dcoords.copy_(g.float())
-        self.loss_finalize(tbuf, n, kind, stats, loss)
+        self.loss_finalize(n, kind, stats, loss)
 
-    def loss_finalize(self, tbuf, n, kind, stats, loss):
+    def loss_finalize(self, n, kind, stats, loss):
         s = stats.double()
-        dg = float((torch.diagonal(tbuf[:, :n]).double() ** 2).sum())
-        mse = (2 * float(s[0]) + dg) / (n * n)
+        mse = (2 * float(s[0]) + float(s[6])) / (n * n)
         M = n * (n - 1) / 2
         cov = float(s[3]) - float(s[1]) * float(s[4]) / M
         vd = float(s[2]) - float(s[1]) ** 2 / M
@@ -145,7 +148,7 @@ class CpuKernels:
         msef = float(np.float32(mse))
         alpha = min(1.0, 0.1 + 1.0 / (msef + 1e-6))
         total = float(np.float32(msef) + np.float32(alpha * (1 - r)))
-        stats[6], stats[7], stats[8], stats[9] = mse, r, alpha, total
+        stats[7], stats[8], stats[9], stats[10] = mse, r, alpha, total
         loss.fill_(total if kind == 1 else msef)
 
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):

@@ -88,7 +88,7 @@ def test_sharded_step_equals_single_rank(tmp_path, kind):
     one = _run(1, 300, kind, tmp_path)
     two = _run(2, 300, kind, tmp_path)
     assert abs(two["losses"][0] - one["losses"][0]) <= 1e-6 * abs(one["losses"][0])
-    assert torch.allclose(two["stats"][:8], one["stats"][:8], rtol=1e-9)
+    assert torch.allclose(two["stats"][:9], one["stats"][:9], rtol=1e-9)
     g1, g2 = one["grad1"], two["grad1"]
     assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
     np.testing.assert_allclose(two["losses"], one["losses"], rtol=1e-3)
