@@ -1,0 +1,232 @@
+// fp32 MFMA GEMM family for the MLP tail (a6 / a6') and the GAT weight gradient (a10).
+//
+// Reference: torch.nn.Linear forward/backward inside models.py:637-659 and the lin_l weight
+// gradient of PyG GATConv, run by ATen/MKL sgemm on the CPU.  On MI355X these shapes are skinny
+// (M = N_nodes = 20000 rows against 3..512 features, and the weight gradients reduce over K = 20000
+// rows); a library GEMM picks tiles for square problems, so the tail gets its own kernels:
+//
+//   C[M,N] = op(A)[M,K] * op(B)[K,N] (+ bias[N]),  op(A) = A (row-major [M,K]) or A^T (A is [K,M]),
+//                                                 op(B) = B^T (B is [N,K]) or B (B is [K,N])
+//   Linear forward   Y  = X W^T + b : A = X [M,K],  B = W [N,K]           (A_KM = 0, B_KM = 0)
+//   input gradient   dX = dY W      : A = dY [M,K], B = W [K,N]           (A_KM = 0, B_KM = 1)
+//   weight gradient  dW = dY^T X    : A = dY [K,M], B = X [K,N], K = rows  (A_KM = 1, B_KM = 1)
+//
+// v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate), 4 waves in 2x2, LDS tiles stored
+// K-major (As[k][m], Bs[k][n]) so every MFMA operand read is 32 consecutive floats; the next
+// K-step is prefetched into registers under the current step's MFMAs.  K can be split over
+// gridDim.z: each split writes an fp32 partial slab and a second kernel adds the slabs in split
+// order (deterministic, no float atomics).
+#include "common.hpp"
+
+namespace hicgat {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GK = 16;  // K-step
+
+template <int BM, int BN, bool A_KM, bool B_KM>
+__global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, int64_t lda,
+                                                   const float *__restrict__ B, int64_t ldb,
+                                                   float *__restrict__ C, int64_t ldc, int M, int N,
+                                                   int K, int kchunk, const float *__restrict__ bias,
+                                                   float *__restrict__ slab, int accumulate) {
+  constexpr int WM = BM / 2, WN = BN / 2;        // wave tile
+  constexpr int TM = WM / 32, TN = WN / 32;      // 32x32 MFMA tiles per wave
+  constexpr int AE = BM * GK / 256, BE = BN * GK / 256;  // staged elements per thread
+  __shared__ float As[GK][BM + 4];
+  __shared__ float Bs[GK][BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+
+  float ra[AE], rb[BE];
+  // element e of thread t: K-major operands walk the contiguous m (n) dim first, the others the
+  // contiguous k dim first, so consecutive threads read consecutive addresses either way.
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < AE; ++e) {
+      const int idx = e * 256 + tid;
+      int m, k;
+      if (A_KM) { m = idx % BM; k = idx / BM; } else { k = idx % GK; m = idx / GK; }
+      const int gm = m0 + m, gk = k0 + k;
+      ra[e] = (gm < M && gk < ke) ? (A_KM ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < BE; ++e) {
+      const int idx = e * 256 + tid;
+      int n, k;
+      if (B_KM) { n = idx % BN; k = idx / BN; } else { k = idx % GK; n = idx / GK; }
+      const int gn = n0 + n, gk = k0 + k;
+      rb[e] = (gn < N && gk < ke) ? (B_KM ? B[(size_t)gk * ldb + gn] : B[(size_t)gn * ldb + gk]) : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < AE; ++e) {
+      const int idx = e * 256 + tid;
+      if (A_KM) As[idx / BM][idx % BM] = ra[e];
+      else As[idx % GK][idx / GK] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < BE; ++e) {
+      const int idx = e * 256 + tid;
+      if (B_KM) Bs[idx / BN][idx % BN] = rb[e];
+      else Bs[idx % GK][idx / GK] = rb[e];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int li = lane & 31, lk = lane >> 5;
+  if (kb < ke) load(kb);
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (k0 + GK < ke) load(k0 + GK);
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 2) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) av[a] = As[kk + lk][wm * WM + a * 32 + li];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bv[b] = Bs[kk + lk][wn * WN + b * 32 + li];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  // C/D map of a 32x32 f32 tile: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  float *out = slab ? slab + (size_t)blockIdx.z * M * N : C;
+  const int64_t ldo = slab ? N : ldc;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int gn = n0 + wn * WN + b * 32 + li;
+      const float bb = (bias && !slab && gn < N) ? bias[gn] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (gm < M && gn < N) {
+          float *o = out + (size_t)gm * ldo + gn;
+          *o = acc[a][b][r] + bb + ((accumulate && !slab) ? *o : 0.f);
+        }
+      }
+    }
+  }
+}
+
+// C[m][n] = sum_z slab[z][m][n] (+ bias[n]), splits added in order.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ slab, int splits,
+                                                            int M, int N, float *__restrict__ C,
+                                                            int64_t ldc, const float *__restrict__ bias,
+                                                            int accumulate) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * total + i];
+    const int m = (int)(i / N), n = (int)(i % N);
+    float *o = C + (size_t)m * ldc + n;
+    *o = s + (bias ? bias[n] : 0.f) + (accumulate ? *o : 0.f);
+  }
+}
+
+// out[n] = sum_k A[k][n] over K rows (bias gradient of a Linear layer), deterministic two-stage.
+constexpr int kColBlocks = 128;
+__global__ __launch_bounds__(256) void colsum_stage1(const float *__restrict__ A, int64_t lda, int K, int N,
+                                                     int rows_per_block, float *__restrict__ part) {
+  const int k0 = blockIdx.x * rows_per_block, k1 = min(K, k0 + rows_per_block);
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float s = 0.f;
+    for (int k = k0; k < k1; ++k) s += A[(size_t)k * lda + n];
+    part[(size_t)blockIdx.x * N + n] = s;
+  }
+}
+__global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int nblk, int N,
+                                                     float *__restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * N + n];
+  out[n] = s;
+}
+
+template <int BM, int BN, bool AK, bool BK_>
+static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
+                  int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
+  const int kchunk = ((K + splits - 1) / splits + GK - 1) / GK * GK;
+  const dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K,
+                     kchunk, bias, splits > 1 ? slab : nullptr, acc);
+  HICGAT_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, splits, M, N, C, ldc, bias, acc);
+    HICGAT_CHECK_LAUNCH();
+  }
+  return HICGAT_OK;
+}
+
+}  // namespace hicgat
+
+using namespace hicgat;
+
+extern "C" size_t hicgat_gemm_workspace_bytes(int M, int N, int splits) {
+  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+extern "C" int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A, int64_t lda,
+                           const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
+                           int splits, void *workspace, size_t workspace_bytes, hicgat_stream_t stream) {
+  if (M < 0 || N < 0 || K < 0 || splits < 1) return HICGAT_EINVAL;
+  if (M == 0 || N == 0) return HICGAT_OK;
+  if (!A || !B || !C) return HICGAT_EINVAL;
+  if (splits > 1 && (!workspace || workspace_bytes < hicgat_gemm_workspace_bytes(M, N, splits)))
+    return HICGAT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  float *slab = static_cast<float *>(workspace);
+  const bool big = M >= 128 && N >= 128;
+  const int code = (a_kmajor ? 2 : 0) | (b_kmajor ? 1 : 0);
+  switch (code | (big ? 4 : 0)) {
+    case 0: return launch<64, 64, false, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 1: return launch<64, 64, false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 2: return launch<64, 64, true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 3: return launch<64, 64, true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 4: return launch<128, 128, false, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 5: return launch<128, 128, false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    case 6: return launch<128, 128, true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+    default: return launch<128, 128, true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+  }
+}
+
+extern "C" size_t hicgat_colsum_workspace_bytes(int N) { return (size_t)kColBlocks * N * sizeof(float); }
+
+extern "C" int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, void *workspace,
+                             size_t workspace_bytes, hicgat_stream_t stream) {
+  if (K < 0 || N < 0) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!A || !out || !workspace || workspace_bytes < hicgat_colsum_workspace_bytes(N)) return HICGAT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int rpb = K > 0 ? (K + kColBlocks - 1) / kColBlocks : 1;
+  const int nblk = K > 0 ? (K + rpb - 1) / rpb : 0;
+  float *part = static_cast<float *>(workspace);
+  if (nblk > 0) {
+    hipLaunchKernelGGL(colsum_stage1, dim3(nblk), dim3(256), 0, s, A, lda, K, N, rpb, part);
+    HICGAT_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(colsum_stage2, dim3((N + 255) / 256), dim3(256), 0, s, part, nblk, N, out);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

@@ -41,6 +41,11 @@ SIGNATURES = {
     "hicgat_pairdist_finalize": (c_int, [c_int, c_int, c_p, c_p, c_p]),
     "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
     "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),
+    "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
+                            c_int, c_p, c_sz, c_p]),
+    "hicgat_gemm_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
+    "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_sz, c_p]),
+    "hicgat_colsum_workspace_bytes": (c_sz, [c_int]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
 }
 

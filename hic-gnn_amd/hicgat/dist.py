@@ -25,6 +25,7 @@ partitioning and collectives are testable on CPU with gloo and a torch stand-in.
 import torch
 import torch.distributed as dist
 
+from .ops import weight_grad
 from .optim import FlatAdam
 
 
@@ -118,7 +119,8 @@ class ShardedTrainer:
         datt_l, datt_r, dbias = K.param_grad(self.h[r0:r1], self.dout[r0:r1], self.da_src[r0:r1],
                                              self.rs_full[r0:r1], self.H)
         with torch.no_grad():
-            self.W.grad.addmm_(self.dh[r0:r1].t(), self.x_loc)
+            weight_grad(K, self.dh[r0:r1], self.x_loc, out=self.W.grad, accumulate=True) if self.x_loc.is_cuda \
+                else self.W.grad.addmm_(self.dh[r0:r1].t(), self.x_loc)
             self.att_l.grad.add_(datt_l.view_as(self.att_l))
             self.att_r.grad.add_(datt_r.view_as(self.att_r))
             if self.bias is not None:

@@ -16,6 +16,11 @@ from . import ops
 from .nn import GATConv
 
 
+def _lin(layer, x):
+    """A torch.nn.Linear of the model, run on the MFMA GEMM kernels."""
+    return ops.linear(x, layer.weight, layer.bias)
+
+
 class _CoordsModel(torch.nn.Module):
     def forward(self, x, edge_index):
         return ops.pairwise_dist(self.get_model(x, edge_index))
@@ -44,12 +49,12 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
     def tail(self, x):
         """models.py:637-659 after the GATConv (relu, two residual LayerNorm blocks, 64 -> 3)."""
         x = F.relu(x)
-        res = self.align_densea(x)
-        x = F.relu(self.norm_a(self.densea(x))) + res
-        res = self.align_dense1(x)
-        x = F.relu(self.norm1(self.dense1(x))) + res
-        x = F.relu(self.norm2(self.dense2(x)))
-        return self.dense3(x)
+        res = _lin(self.align_densea, x)
+        x = F.relu(self.norm_a(_lin(self.densea, x))) + res
+        res = _lin(self.align_dense1, x)
+        x = F.relu(self.norm1(_lin(self.dense1, x))) + res
+        x = F.relu(self.norm2(_lin(self.dense2, x)))
+        return _lin(self.dense3, x)
 
     def get_model(self, x, edge_index):
         return self.tail(self.conv(x, edge_index))
@@ -65,9 +70,9 @@ class GATNetHeadsChanged3LayersLeakyReLUv2(_CoordsModel):
 
     def tail(self, x):
         x = F.leaky_relu(x)
-        x = F.leaky_relu(self.densea(x))
-        x = F.leaky_relu(self.dense1(x))
-        return self.dense2(x)
+        x = F.leaky_relu(_lin(self.densea, x))
+        x = F.leaky_relu(_lin(self.dense1, x))
+        return _lin(self.dense2, x)
 
     def get_model(self, x, edge_index):
         return self.tail(self.conv(x, edge_index))

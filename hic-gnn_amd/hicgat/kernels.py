@@ -133,6 +133,26 @@ class HipKernels:
                                                 _lib.stream(coords.device)), "hicgat_pairdist_bwd")
         return dc
 
+    # -- a6: Linear layers on the fp32 MFMA GEMM ---------------------------------------------------
+    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=1, name="gemm"):
+        dev = C.device
+        ws = None
+        if splits > 1:
+            ws = _lib.workspace(self.lib.hicgat_gemm_workspace_bytes(M, N, splits), dev)
+        with _timed(name):
+            _lib.check(self.lib.hicgat_gemm(int(a_kmajor), int(b_kmajor), M, N, K, P(A), A.stride(0), P(B),
+                                            B.stride(0), P(bias), P(C), C.stride(0), int(accumulate), int(splits),
+                                            P(ws), 0 if ws is None else ws.numel(), _lib.stream(dev)),
+                       "hicgat_gemm")
+        return C
+
+    def colsum(self, A, out):
+        K, N = A.shape
+        ws = _lib.workspace(self.lib.hicgat_colsum_workspace_bytes(N), A.device)
+        _lib.check(self.lib.hicgat_colsum(P(A), A.stride(0), K, N, P(out), P(ws), ws.numel(), _lib.stream(A.device)),
+                   "hicgat_colsum")
+        return out
+
     # -- a10 --------------------------------------------------------------------------------------
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):

@@ -51,10 +51,67 @@ class _GATConvFn(torch.autograd.Function):
         da_src = torch.empty_like(a_src)
         K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
         datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
-        dW = dh.t().mm(x) if ctx.needs_input_grad[1] else None
-        dx = dh.mm(W) if ctx.needs_input_grad[0] else None
+        dW = weight_grad(K, dh, x) if ctx.needs_input_grad[1] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
         return (dx, dW, datt_l.view(al.shape), datt_r.view(ar.shape),
                 dbias if ctx.has_bias else None, None, None, None)
+
+
+def _splits(m, n, k, target=1024):
+    """K-split for a weight-gradient GEMM whose K is the node count: enough workgroups to fill
+    the 256 CUs, each split at least 256 rows deep."""
+    bm = 128 if (m >= 128 and n >= 128) else 64
+    tiles = -(-m // bm) * -(-n // bm)
+    return max(1, min(k // 256, target // tiles))
+
+
+def weight_grad(K, dy, x, out=None, accumulate=False):
+    """dW = dy^T x (Linear / lin_l weight gradient), K = rows, split-K MFMA GEMM."""
+    rows, m = dy.shape
+    n = x.shape[1]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=dy.device)
+    return K.gemm(1, 1, m, n, rows, dy, x, out, accumulate=accumulate, splits=_splits(m, n, rows), name="gemm_dw")
+
+
+class _LinearFn(torch.autograd.Function):
+    """torch.nn.Linear (models.py:616-632 layers) forward/backward on the fp32 MFMA GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        K = kernels.default()
+        x = x.contiguous()
+        M = x.shape[0]
+        n_out, n_in = W.shape
+        y = torch.empty((M, n_out), dtype=torch.float32, device=x.device)
+        K.gemm(0, 0, M, n_out, n_in, x, W.contiguous(), y, bias=b, name="gemm_fwd")
+        ctx.save_for_backward(x, W)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        K = kernels.default()
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        M = x.shape[0]
+        n_out, n_in = W.shape
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(0, 1, M, n_in, n_out, dy, W.contiguous(), torch.empty_like(x), name="gemm_dx")
+        if ctx.needs_input_grad[1]:
+            dW = weight_grad(K, dy, x)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = K.colsum(dy, torch.empty(n_out, dtype=torch.float32, device=dy.device))
+        return dx, dW, db
+
+
+def linear(x, W, b=None):
+    """F.linear(x, W, b) on the MI355X GEMM kernels (CUDA tensors only)."""
+    _dev_check(x, W, b)
+    return _LinearFn.apply(x, W, b)
 
 
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2):

@@ -141,6 +141,21 @@ int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, h
 int64_t hicgat_pairdist_num_tiles(int N, int mode);
 size_t hicgat_pairdist_workspace_bytes(int N, int mode);
 
+/* ---- a6 / a10: fp32 MFMA GEMM for torch.nn.Linear forward/backward (models.py:637-659) -------
+ *   C[M,N] (+)= op(A) op(B) (+ bias[N]);  op(A) = A [M,K] (lda = row stride) or, with a_kmajor,
+ *   A^T of A [K,M];  op(B) = B^T of B [N,K] or, with b_kmajor, B [K,N].
+ *   Linear forward Y = X W^T + b (0,0); input grad dX = dY W (0,1); weight grad dW = dY^T X (1,1).
+ * accumulate != 0 adds into C (a parameter's .grad).  splits > 1 splits K over workgroups into fp32
+ * slabs (workspace: hicgat_gemm_workspace_bytes) added in split order: deterministic. */
+int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A, int64_t lda,
+                const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
+                int splits, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_gemm_workspace_bytes(int M, int N, int splits);
+/* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
+int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, void *workspace,
+                  size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_colsum_workspace_bytes(int N);
+
 /* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
  * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
  *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);

@@ -59,6 +59,7 @@ def _worker(rank, world, port, n, kind, out):
     try:
         hicgat, adj, truth, x = _setup(n)
         from cpu_kernels import CpuKernels
+        hicgat.gat_models._lin = lambda layer, inp: layer(inp)   # torch Linear on CPU tensors
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated()
         tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels())
@@ -120,7 +121,6 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
         ol.mse_loss(ref(x, radj), truth.dense().double()).backward()
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
-    torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated()
     off = 0
     for (name, p), pr in zip(model.named_parameters(), ref.parameters()):

@@ -173,6 +173,47 @@ def test_gat_agg_long_rows_and_softmax_extremes():
     assert torch.isfinite(out_m).all()
 
 
+# ---------------------------------------------------------------- a6: GEMM family / Linear
+@pytest.mark.parametrize("m,n,k", [(20000, 256, 512), (777, 3, 64), (130, 129, 7), (64, 512, 512), (5, 1, 1)])
+def test_gemm_layouts_match_torch(m, n, k):
+    import hicgat
+    K = hicgat.kernels.default()
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV)
+    w = torch.randn(n, k, device=DEV)
+    b = torch.randn(n, device=DEV)
+    y = K.gemm(0, 0, m, n, k, x, w, torch.empty(m, n, device=DEV), bias=b)
+    assert _rel(y.cpu(), (x.double() @ w.double().t() + b.double()).cpu()) < 5e-6
+    dy = torch.randn(m, n, device=DEV)
+    dx = K.gemm(0, 1, m, k, n, dy, w, torch.empty(m, k, device=DEV))
+    assert _rel(dx.cpu(), (dy.double() @ w.double()).cpu()) < 5e-6
+    for splits in (1, 3, 64):
+        dw = K.gemm(1, 1, n, k, m, dy, x, torch.empty(n, k, device=DEV), splits=splits)
+        assert _rel(dw.cpu(), (dy.double().t() @ x.double()).cpu()) < 5e-6
+    acc = torch.ones(n, k, device=DEV)
+    K.gemm(1, 1, n, k, m, dy, x, acc, accumulate=True, splits=3)
+    assert _rel(acc.cpu(), (dy.double().t() @ x.double() + 1).cpu()) < 5e-6
+    db = K.colsum(dy, torch.empty(n, device=DEV))
+    assert _rel(db.cpu(), dy.double().sum(0).cpu()) < 5e-6
+
+
+def test_linear_autograd_matches_torch():
+    import hicgat
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(512, 256).to(DEV)
+    x = torch.randn(3001, 512, device=DEV, requires_grad=True)
+    y = hicgat.ops.linear(x, lin.weight, lin.bias)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    gx, gw, gb = x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()
+    x.grad = None
+    lin.zero_grad()
+    (torch.nn.functional.linear(x.double(), lin.weight.double(), lin.bias.double()) * g.double()).sum().backward()
+    assert _rel(gx.cpu(), x.grad.cpu()) < 5e-6
+    assert _rel(gw.cpu(), lin.weight.grad.cpu()) < 5e-6
+    assert _rel(gb.cpu(), lin.bias.grad.cpu()) < 5e-6
+
+
 # ---------------------------------------------------------------- a7-a9: distance + loss
 @pytest.mark.parametrize("n", [1, 2, 58, 129, 300])
 def test_pairdist_fwd_bwd_matches_torch(n):

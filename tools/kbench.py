@@ -50,6 +50,10 @@ def main():
     g = torch.randn_like(flat)
     m = torch.zeros_like(flat)
     v = torch.zeros_like(flat)
+    Wa = model.densea.weight.detach()
+    ba = model.densea.bias.detach()
+    ya = torch.empty(n, 256, device=dev)
+    dxa = torch.empty(n, 512, device=dev)
     libs = [s for s in a.libs.split(",") if s] or [_lib.LIB_PATH]
     kset = []
     for path in libs:
@@ -69,6 +73,12 @@ def main():
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
         "adam": lambda K: K.adam(flat, g, m, v, flat.numel(), 1e-3, 0.9, 0.999, 1e-8, 1),
+        "gemm_dw_512x512": lambda K: hicgat.ops.weight_grad(K, dh, x),
+        "gemm_fwd_densea": lambda K: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba),
+        "gemm_dx_densea": lambda K: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa),
+        "gemm_dw_densea": lambda K: hicgat.ops.weight_grad(K, ya, out),
+        "torch_dw_densea": lambda K: ya.t().mm(out),
+        "torch_fwd_densea": lambda K: torch.nn.functional.linear(out, Wa, ba),
     }
     res = {}
     for r in range(a.rounds):
