@@ -115,6 +115,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured hipGraph (kernel timing then comes from an "
+                         "eager pass of the same length right after the timed region)")
     args = ap.parse_args()
 
     import hicgat
@@ -143,14 +146,20 @@ def main():
         def step():
             return hicgat.train.train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss, stats)
 
-    for w in range(args.warmup):
-        step()
+    eager_step = step
+    if args.graph and world == 1:
+        step = hicgat.graphs.captured_train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss,
+                                                 warmup=max(1, args.warmup))
+    else:
+        for w in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     log(f"[bench] warmup done ({args.warmup} steps)")
 
-    kernels.TIMERS = {}
+    if not args.graph:
+        kernels.TIMERS = {}
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -161,6 +170,11 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         torch.distributed.barrier()
+    if args.graph:
+        kernels.TIMERS = {}
+        for k in range(args.steps):
+            eager_step()
+        torch.cuda.synchronize()
     timers, kernels.TIMERS = kernels.TIMERS, None
     elapsed = t1 - t0
     if world > 1:
@@ -203,6 +217,7 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
+        "graph": bool(args.graph and world == 1),
         "config": {"workload": args.workload, "model": "GATNetSelectiveResidualsUpdated",
                    "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz, "d": D_FEAT, "heads": HEADS,
                    "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single"},

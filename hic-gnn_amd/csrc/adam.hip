@@ -24,7 +24,15 @@ __device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, 
 
 __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                                                    float *__restrict__ m, float *__restrict__ v,
-                                                   int64_t n, AdamConsts k) {
+                                                   int64_t n, AdamConsts k,
+                                                   const float2 *__restrict__ table,
+                                                   const int64_t *__restrict__ step_ctr, int64_t table_len) {
+  if (table) {  // graph-replayable form: per-step constants from the host-computed table
+    int64_t s = *step_ctr;
+    if (s >= table_len) s = table_len - 1;
+    k.neg_step = table[s].x;
+    k.bc2s = table[s].y;
+  }
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float4 *p4 = reinterpret_cast<float4 *>(p);
@@ -51,6 +59,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ p, const 
   }
 }
 
+__global__ void step_increment_kernel(int64_t *step_ctr) { *step_ctr += 1; }
+
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -74,7 +84,34 @@ extern "C" int hicgat_adam_step(float *param, const float *grad, float *exp_avg,
   const int64_t work = (n + 3) / 4;
   const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                     exp_avg, exp_avg_sq, n, k);
+                     exp_avg, exp_avg_sq, n, k, nullptr, nullptr, (int64_t)0);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                                      int64_t n, double beta1, double beta2, double eps, const float *table,
+                                      int64_t table_len, int64_t *step_counter, hicgat_stream_t stream) {
+  if (n < 0 || table_len < 1) return HICGAT_EINVAL;
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !table || !step_counter) return HICGAT_EINVAL;
+  const uintptr_t mis = reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+                        reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq);
+  if ((mis & 15) || (reinterpret_cast<uintptr_t>(table) & 7)) return HICGAT_EINVAL;
+  AdamConsts k;
+  k.w1 = (float)(1.0 - beta1);
+  k.b2 = (float)beta2;
+  k.c2 = (float)(1.0 - beta2);
+  k.eps = (float)eps;
+  k.bc2s = 1.f;
+  k.neg_step = 0.f;
+  if (n > 0) {
+    const int64_t work = (n + 3) / 4;
+    const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                       exp_avg_sq, n, k, reinterpret_cast<const float2 *>(table), step_counter, table_len);
+    HICGAT_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step_counter);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

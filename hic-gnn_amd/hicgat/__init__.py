@@ -10,7 +10,7 @@ Drop-in surface of the reference (beyzoskaya/HiC-GNN):
   hicgat.metrics.dscc, hicgat.io.write_pdb    ~ HiC-GNN_main.py:135-139, utils.WritePDB
 Compute runs in libhicgat.so (include/hicgat.h); there is no CPU fallback.
 """
-from . import _lib, dist, graph, io, kernels, metrics, nn, ops, optim, synth, train  # noqa: F401
+from . import _lib, dist, graph, graphs, io, kernels, metrics, nn, ops, optim, synth, train  # noqa: F401
 from .gat_models import (GATNetHeadsChanged3LayersLeakyReLUv2,  # noqa: F401
                          GATNetSelectiveResidualsUpdated, MODELS)
 from .graph import Adj, Data, Truth, cont2dist, convert_to_matrix, load_input  # noqa: F401

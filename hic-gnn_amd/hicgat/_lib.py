@@ -47,6 +47,7 @@ SIGNATURES = {
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_sz, c_p]),
     "hicgat_colsum_workspace_bytes": (c_sz, [c_int]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
+    "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
 }
 
 

@@ -154,6 +154,12 @@ class HipKernels:
         return out
 
     # -- a10 --------------------------------------------------------------------------------------
+    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):
+        with _timed("adam"):
+            _lib.check(self.lib.hicgat_adam_step_table(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
+                                                       float(eps), P(table), table.shape[0], P(step_ctr),
+                                                       _lib.stream(flat.device)), "hicgat_adam_step_table")
+
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):
             _lib.check(self.lib.hicgat_adam_step(P(flat), P(grad), P(m), P(v), int(n), float(lr), float(b1),

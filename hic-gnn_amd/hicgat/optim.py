@@ -36,6 +36,20 @@ class FlatAdam:
         self.lr, self.betas, self.eps = lr, betas, eps
         self.step_count = 0
 
+    def enable_device_step(self, max_steps=1 << 20):
+        """Keep the step count on the device so ``step()`` can be captured in a hipGraph and
+        replayed.  The per-step constants are tabulated on the host with libm pow in float64 --
+        the same arithmetic as the eager path (and as torch's Python-float bias corrections)."""
+        import numpy as np
+        lr, (b1, b2) = self.lr, self.betas
+        t = np.arange(1, max_steps + 1, dtype=np.float64)
+        tab = np.empty((max_steps, 2), dtype=np.float32)
+        tab[:, 0] = -(lr / (1.0 - np.power(b1, t)))
+        tab[:, 1] = np.power(1.0 - np.power(b2, t), 0.5)
+        self.table = torch.from_numpy(tab).to(self.flat.device)
+        self.step_ctr = torch.full((1,), self.step_count, dtype=torch.int64, device=self.flat.device)
+        return self
+
     def zero_grad(self, set_to_none=False):
         self.grad.zero_()
 
@@ -43,6 +57,10 @@ class FlatAdam:
     def step(self):
         self.step_count += 1
         kern = self.kern if self.kern is not None else kernels.default()
+        if getattr(self, "step_ctr", None) is not None:
+            kern.adam_table(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.betas[0],
+                            self.betas[1], self.eps, self.table, self.step_ctr)
+            return
         kern.adam(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.lr, self.betas[0],
                   self.betas[1], self.eps, self.step_count)
 

@@ -163,6 +163,12 @@ size_t hicgat_colsum_workspace_bytes(int N);
 int hicgat_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                      double lr, double beta1, double beta2, double eps, int64_t step,
                      hicgat_stream_t stream);
+/* Graph-replayable form: the step count lives on the device (*step_counter = steps done so far,
+ * incremented by the call), the per-step constants come from table[step] = (-lr/(1-b1^t),
+ * sqrt(1-b2^t)) for t = step+1, computed on the host exactly like hicgat_adam_step does. */
+int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                           int64_t n, double beta1, double beta2, double eps, const float *table,
+                           int64_t table_len, int64_t *step_counter, hicgat_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -419,6 +419,37 @@ def test_train_loop_tracks_oracle():
     assert np.all(np.abs(np.array(hist) - fx["loss"]) / fx["loss"] < 0.1)
 
 
+def test_graph_replay_equals_eager_steps():
+    """hipGraph-captured training steps (device-side Adam step counter) give the same bits as the
+    eager steps."""
+    import hicgat
+    from hicgat import synth
+    n = 1500
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=1)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    x = torch.tensor(synth.features(n, seed=1), device=DEV)
+    res = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+        opt = hicgat.FlatAdam(model.parameters(), lr=1e-3)
+        losses = []
+        if graphed:
+            step = hicgat.graphs.captured_train_step(model, opt, x, adj, tr, warmup=2)
+            losses += [None, None]
+            for _ in range(4):
+                losses.append(float(step()[0]))
+        else:
+            for _ in range(6):
+                losses.append(float(hicgat.train.train_step(model, opt, x, adj, tr)[0]))
+        res.append((losses, opt.flat.clone()))
+    (le, pe), (lg, pg) = res
+    assert le[2:] == lg[2:]
+    assert torch.equal(pe, pg)
+
+
 def test_dscc_matches_scipy():
     import hicgat
     from scipy.stats import spearmanr

@@ -20,6 +20,8 @@ for s in $STAGES; do
     tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
+    benchg) run bench_graph 600 python bench.py --steps ${STEPS:-20} --warmup 3 --graph --no-cpu-baseline ;;
+    benchcpu) run bench_cpu 900 python bench.py ;;
     kbench) run kbench 600 python tools/kbench.py --libs ${KLIBS:-hic-gnn_amd/hicgat/libhicgat.so} ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
