@@ -87,7 +87,7 @@ __device__ __forceinline__ float f4_dot(float4 a, float4 b) {
 // Cost: V-1 shuffles + 2 for the final intra-group sum (vs 6 per value for independent sums).
 template <int V>
 __device__ __forceinline__ void transpose_reduce(float (&v)[V], int lane) {
-  static_assert(V == 16 || V == 8 || V == 4, "transpose_reduce: V must be 4, 8 or 16");
+  static_assert(V == 16 || V == 8 || V == 4 || V == 2, "transpose_reduce: V must be 2, 4, 8 or 16");
   int mask = 32;
 #pragma unroll
   for (int n = V; n > 1; n >>= 1, mask >>= 1) {

@@ -18,7 +18,10 @@
 #include "common.hpp"
 
 #ifndef HICGAT_BWD_U
-#define HICGAT_BWD_U 8   // neighbours gathered per inner step (2 float4 loads per lane each)
+// neighbours gathered per inner step (2 float4 loads per lane each).  Measured on MI355X at
+// N = 20000 (tools/kbench.py): U = 8 -> 0.95 / 1.11 ms (dst / src pass, 118 / 142 VGPRs, 4 / 3
+// waves per SIMD); U = 4 -> 0.52 / 0.56; U = 2 -> 0.47 / 0.49.  The gather wants waves, not ILP.
+#define HICGAT_BWD_U 2
 #endif
 
 namespace hicgat {
@@ -26,7 +29,7 @@ namespace hicgat {
 // After transpose_reduce<2U> over values [head*U + k], lane l owns head l>>5 and slot k; the
 // 64/(2U) lanes of a group hold the same sum and the first of them is the "owner".
 template <int U> struct Owner {
-  static constexpr int kShift = U == 8 ? 2 : U == 4 ? 3 : 4;
+  static constexpr int kShift = U == 8 ? 2 : U == 4 ? 3 : U == 2 ? 4 : 5;
   __device__ static int slot(int lane) { return (lane >> kShift) & (U - 1); }
   __device__ static bool owner(int lane) { return (lane & ((1 << kShift) - 1)) == 0; }
 };

@@ -24,55 +24,86 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int GK = 16;  // K-step
 
-template <int BM, int BN, bool A_KM, bool B_KM>
+template <int BM, int BN, bool A_KM, bool B_KM, bool VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, int64_t lda,
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
                                                    int K, int kchunk, const float *__restrict__ bias,
                                                    float *__restrict__ slab, int accumulate) {
-  constexpr int WM = BM / 2, WN = BN / 2;        // wave tile
+  constexpr int WM = BM / 2, WN = BN / 2;        // wave tile (4 waves in 2 x 2)
   constexpr int TM = WM / 32, TN = WN / 32;      // 32x32 MFMA tiles per wave
-  constexpr int AE = BM * GK / 256, BE = BN * GK / 256;  // staged elements per thread
-  __shared__ float As[GK][BM + 4];
-  __shared__ float Bs[GK][BN + 4];
+  // staged values per thread: VEC -> float4 pieces, else scalars
+  constexpr int AE = VEC ? BM * GK / 1024 : BM * GK / 256;
+  constexpr int BE = VEC ? BN * GK / 1024 : BN * GK / 256;
+  constexpr int W = VEC ? 4 : 1;
+  __shared__ __attribute__((aligned(16))) float As[GK][BM + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[GK][BN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
 
-  float ra[AE], rb[BE];
-  // element e of thread t: K-major operands walk the contiguous m (n) dim first, the others the
-  // contiguous k dim first, so consecutive threads read consecutive addresses either way.
+  float ra[AE][W], rb[BE][W];
+  // piece p of a tile: K-major operands walk the contiguous m (n) dim first, the others the
+  // contiguous k dim first, so consecutive threads read consecutive 4 (or 16) bytes either way.
   auto load = [&](int k0) {
 #pragma unroll
     for (int e = 0; e < AE; ++e) {
       const int idx = e * 256 + tid;
       int m, k;
-      if (A_KM) { m = idx % BM; k = idx / BM; } else { k = idx % GK; m = idx / GK; }
+      if (A_KM) { m = (idx % (BM / W)) * W; k = idx / (BM / W); } else { k = (idx % (GK / W)) * W; m = idx / (GK / W); }
       const int gm = m0 + m, gk = k0 + k;
-      ra[e] = (gm < M && gk < ke) ? (A_KM ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
+      if (VEC) {
+        const bool ok = A_KM ? (gm < M && gk < ke) : (gm < M && gk < ke);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) v = *reinterpret_cast<const float4 *>(A_KM ? A + (size_t)gk * lda + gm : A + (size_t)gm * lda + gk);
+        ra[e][0] = v.x; ra[e][W > 1 ? 1 : 0] = v.y; ra[e][W > 2 ? 2 : 0] = v.z; ra[e][W > 3 ? 3 : 0] = v.w;
+      } else {
+        ra[e][0] = (gm < M && gk < ke) ? (A_KM ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
+      }
     }
 #pragma unroll
     for (int e = 0; e < BE; ++e) {
       const int idx = e * 256 + tid;
       int n, k;
-      if (B_KM) { n = idx % BN; k = idx / BN; } else { k = idx % GK; n = idx / GK; }
+      if (B_KM) { n = (idx % (BN / W)) * W; k = idx / (BN / W); } else { k = (idx % (GK / W)) * W; n = idx / (GK / W); }
       const int gn = n0 + n, gk = k0 + k;
-      rb[e] = (gn < N && gk < ke) ? (B_KM ? B[(size_t)gk * ldb + gn] : B[(size_t)gn * ldb + gk]) : 0.f;
+      if (VEC) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gn < N && gk < ke)
+          v = *reinterpret_cast<const float4 *>(B_KM ? B + (size_t)gk * ldb + gn : B + (size_t)gn * ldb + gk);
+        rb[e][0] = v.x; rb[e][W > 1 ? 1 : 0] = v.y; rb[e][W > 2 ? 2 : 0] = v.z; rb[e][W > 3 ? 3 : 0] = v.w;
+      } else {
+        rb[e][0] = (gn < N && gk < ke) ? (B_KM ? B[(size_t)gk * ldb + gn] : B[(size_t)gn * ldb + gk]) : 0.f;
+      }
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int e = 0; e < AE; ++e) {
       const int idx = e * 256 + tid;
-      if (A_KM) As[idx / BM][idx % BM] = ra[e];
-      else As[idx % GK][idx / GK] = ra[e];
+      if (A_KM) {
+        const int m = (idx % (BM / W)) * W, k = idx / (BM / W);
+        if (VEC) *reinterpret_cast<float4 *>(&As[k][m]) = make_float4(ra[e][0], ra[e][W > 1 ? 1 : 0], ra[e][W > 2 ? 2 : 0], ra[e][W > 3 ? 3 : 0]);
+        else As[k][m] = ra[e][0];
+      } else {
+        const int k = (idx % (GK / W)) * W, m = idx / (GK / W);
+#pragma unroll
+        for (int c = 0; c < W; ++c) As[k + c][m] = ra[e][c];
+      }
     }
 #pragma unroll
     for (int e = 0; e < BE; ++e) {
       const int idx = e * 256 + tid;
-      if (B_KM) Bs[idx / BN][idx % BN] = rb[e];
-      else Bs[idx % GK][idx / GK] = rb[e];
+      if (B_KM) {
+        const int n = (idx % (BN / W)) * W, k = idx / (BN / W);
+        if (VEC) *reinterpret_cast<float4 *>(&Bs[k][n]) = make_float4(rb[e][0], rb[e][W > 1 ? 1 : 0], rb[e][W > 2 ? 2 : 0], rb[e][W > 3 ? 3 : 0]);
+        else Bs[k][n] = rb[e][0];
+      } else {
+        const int k = (idx % (GK / W)) * W, n = idx / (GK / W);
+#pragma unroll
+        for (int c = 0; c < W; ++c) Bs[k + c][n] = rb[e][c];
+      }
     }
   };
 
@@ -167,8 +198,16 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
                   int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
   const int kchunk = ((K + splits - 1) / splits + GK - 1) / GK * GK;
   const dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K,
-                     kchunk, bias, splits > 1 ? slab : nullptr, acc);
+  // float4 staging needs every float4 inside its operand row and 16-B aligned rows
+  const bool a_ok = AK ? (M % 4 == 0 && lda % 4 == 0) : (K % 4 == 0 && lda % 4 == 0);
+  const bool b_ok = BK_ ? (N % 4 == 0 && ldb % 4 == 0) : (K % 4 == 0 && ldb % 4 == 0);
+  const bool al = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
+  if (a_ok && b_ok && al)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
+                       K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M,
+                       N, K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
   HICGAT_CHECK_LAUNCH();
   if (splits > 1) {
     const int64_t total = (int64_t)M * N;
@@ -177,6 +216,17 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
     HICGAT_CHECK_LAUNCH();
   }
   return HICGAT_OK;
+}
+
+template <bool AK, bool BK_>
+static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
+                    int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
+  // tall row-major problems (M = node rows): 64 x 128 tiles keep >= 2 blocks per CU in flight;
+  // square-ish weight gradients (M, N = features, K = rows split): 128 x 128
+  if (M >= 128 && N >= 128 && M <= 1024)
+    return launch<128, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
+  if (N >= 128) return launch<64, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
+  return launch<64, 64, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
 }
 
 }  // namespace hicgat
@@ -197,18 +247,10 @@ extern "C" int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, cons
     return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   float *slab = static_cast<float *>(workspace);
-  const bool big = M >= 128 && N >= 128;
-  const int code = (a_kmajor ? 2 : 0) | (b_kmajor ? 1 : 0);
-  switch (code | (big ? 4 : 0)) {
-    case 0: return launch<64, 64, false, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 1: return launch<64, 64, false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 2: return launch<64, 64, true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 3: return launch<64, 64, true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 4: return launch<128, 128, false, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 5: return launch<128, 128, false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    case 6: return launch<128, 128, true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-    default: return launch<128, 128, true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
-  }
+  if (!a_kmajor && !b_kmajor) return dispatch<false, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+  if (!a_kmajor && b_kmajor) return dispatch<false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+  if (a_kmajor && !b_kmajor) return dispatch<true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
+  return dispatch<true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
 }
 
 extern "C" size_t hicgat_colsum_workspace_bytes(int N) { return (size_t)kColBlocks * N * sizeof(float); }

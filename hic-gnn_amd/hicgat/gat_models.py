@@ -47,13 +47,15 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
         self.dense3 = Linear(64, 3)
 
     def tail(self, x):
-        """models.py:637-659 after the GATConv (relu, two residual LayerNorm blocks, 64 -> 3)."""
+        """models.py:637-659 after the GATConv: relu; [densea | align_densea] as one GEMM,
+        relu(norm_a(.)) + residual in one pass; the same for dense1 / align_dense1 / norm1;
+        relu(norm2(dense2(.))); dense3."""
         x = F.relu(x)
-        res = _lin(self.align_densea, x)
-        x = F.relu(self.norm_a(_lin(self.densea, x))) + res
-        res = _lin(self.align_dense1, x)
-        x = F.relu(self.norm1(_lin(self.dense1, x))) + res
-        x = F.relu(self.norm2(_lin(self.dense2, x)))
+        y, res = ops.dual_linear(x, self.densea, self.align_densea)
+        x = ops.ln_relu_res(y, self.norm_a, res)
+        y, res = ops.dual_linear(x, self.dense1, self.align_dense1)
+        x = ops.ln_relu_res(y, self.norm1, res)
+        x = ops.ln_relu_res(_lin(self.dense2, x), self.norm2)
         return _lin(self.dense3, x)
 
     def get_model(self, x, edge_index):

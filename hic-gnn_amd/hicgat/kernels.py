@@ -153,6 +153,19 @@ class HipKernels:
                    "hicgat_colsum")
         return out
 
+    def ln_relu_res_fwd(self, y, gamma, beta, eps, res, z, row_stats):
+        M, W = z.shape
+        _lib.check(self.lib.hicgat_ln_relu_res_fwd(P(y), y.stride(0), M, W, P(gamma), P(beta), float(eps), P(res),
+                                                   0 if res is None else res.stride(0), P(z), P(row_stats),
+                                                   _lib.stream(z.device)), "hicgat_ln_relu_res_fwd")
+
+    def ln_relu_res_bwd(self, dz, y, row_stats, gamma, beta, dy, dgamma, dbeta, accumulate=False):
+        M, W = dz.shape
+        ws = _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), dz.device)
+        _lib.check(self.lib.hicgat_ln_relu_res_bwd(P(dz), P(y), y.stride(0), M, W, P(row_stats), P(gamma), P(beta),
+                                                   P(dy), dy.stride(0), P(dgamma), P(dbeta), int(accumulate), P(ws),
+                                                   ws.numel(), _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
+
     # -- a10 --------------------------------------------------------------------------------------
     def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):
         with _timed("adam"):

@@ -114,6 +114,83 @@ def linear(x, W, b=None):
     return _LinearFn.apply(x, W, b)
 
 
+class _DualLinearFn(torch.autograd.Function):
+    """Two Linear layers on the same input (models.py:638-639 / 646-647: dense* and align_dense*)
+    as ONE GEMM over [W1; W2]: the input is read once; the backward adds both input gradients
+    inside the GEMM (accumulate) instead of a separate add."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        K = kernels.default()
+        x = x.contiguous()
+        M = x.shape[0]
+        n1, n2 = W1.shape[0], W2.shape[0]
+        Wc = torch.cat([W1, W2]).contiguous()
+        bc = torch.cat([b1, b2]).contiguous()
+        Y = torch.empty((M, n1 + n2), dtype=torch.float32, device=x.device)
+        K.gemm(0, 0, M, n1 + n2, x.shape[1], x, Wc, Y, bias=bc, name="gemm_fwd")
+        ctx.save_for_backward(x, W1, W2)
+        return Y[:, :n1], Y[:, n1:]
+
+    @staticmethod
+    def backward(ctx, dy1, dy2):
+        K = kernels.default()
+        x, W1, W2 = ctx.saved_tensors
+        M, n_in = x.shape
+        dy1 = dy1.contiguous()
+        dy2 = dy2.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(0, 1, M, n_in, W1.shape[0], dy1, W1, torch.empty_like(x), name="gemm_dx")
+            K.gemm(0, 1, M, n_in, W2.shape[0], dy2, W2, dx, accumulate=True, name="gemm_dx")
+        dW1 = weight_grad(K, dy1, x)
+        dW2 = weight_grad(K, dy2, x)
+        db1 = K.colsum(dy1, torch.empty(W1.shape[0], dtype=torch.float32, device=x.device))
+        db2 = K.colsum(dy2, torch.empty(W2.shape[0], dtype=torch.float32, device=x.device))
+        return dx, dW1, db1, dW2, db2
+
+
+def dual_linear(x, lin1, lin2):
+    _dev_check(x)
+    return _DualLinearFn.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+
+
+class _LnReluResFn(torch.autograd.Function):
+    """relu(LayerNorm(y)) + res in one pass (models.py:641-655)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, res, eps):
+        K = kernels.default()
+        M, W = y.shape
+        z = torch.empty((M, W), dtype=torch.float32, device=y.device)
+        stats = torch.empty((M, 2), dtype=torch.float32, device=y.device)
+        K.ln_relu_res_fwd(y, gamma, beta, eps, res, z, stats)
+        ctx.save_for_backward(y, stats, gamma, beta)
+        ctx.has_res = res is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        K = kernels.default()
+        y, stats, gamma, beta = ctx.saved_tensors
+        dz = dz.contiguous()
+        dy = torch.empty(y.shape, dtype=torch.float32, device=y.device)
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(beta)
+        K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, dgamma, dbeta)
+        return dy, dgamma, dbeta, (dz if ctx.has_res else None), None
+
+
+def ln_relu_res(y, norm, res=None):
+    """F.relu(norm(y)) + res for a torch.nn.LayerNorm ``norm`` (elementwise affine)."""
+    _dev_check(y)
+    if y.stride(1) != 1:
+        y = y.contiguous()
+    if res is not None and res.stride(1) != 1:
+        res = res.contiguous()
+    return _LnReluResFn.apply(y, norm.weight, norm.bias, res, norm.eps)
+
+
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2):
     if adj.rowptr32 is None or adj.rowptr32.device != x.device:
         adj.to(x.device)

@@ -156,6 +156,20 @@ int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, void *w
                   size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_colsum_workspace_bytes(int N);
 
+/* ---- a6: LayerNorm + ReLU (+ residual) of the flagship tail (models.py:641-655) --------------
+ * z = relu(LayerNorm(y) * gamma + beta) + res (res may be NULL), W in {64, 128, 256}, eps as in
+ * torch.nn.LayerNorm (biased variance); row_stats [M, 2] = (mean, rstd) saved for the backward.
+ * Backward: dy (ld lddy), dgamma/dbeta (accumulate != 0 adds into them); dres = dz is the
+ * caller's (no copy).  workspace: hicgat_ln_relu_res_workspace_bytes(W). */
+int hicgat_ln_relu_res_fwd(const float *y, int64_t ldy, int M, int W, const float *gamma, const float *beta,
+                           float eps, const float *res, int64_t ldr, float *z, float *row_stats,
+                           hicgat_stream_t stream);
+int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, int W, const float *row_stats,
+                           const float *gamma, const float *beta, float *dy, int64_t lddy, float *dgamma,
+                           float *dbeta, int accumulate, void *workspace, size_t workspace_bytes,
+                           hicgat_stream_t stream);
+size_t hicgat_ln_relu_res_workspace_bytes(int W);
+
 /* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
  * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
  *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);

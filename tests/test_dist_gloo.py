@@ -51,6 +51,22 @@ def _setup(n):
     return hicgat, adj, truth, torch.tensor(x)
 
 
+def _torch_tail(hicgat):
+    """The flagship tail (models.py:637-659) in plain torch for CPU tensors (the product tail runs
+    on the HIP GEMM / LayerNorm kernels)."""
+    import torch.nn.functional as F
+
+    def tail(self, x):
+        x = F.relu(x)
+        res = self.align_densea(x)
+        x = F.relu(self.norm_a(self.densea(x))) + res
+        res = self.align_dense1(x)
+        x = F.relu(self.norm1(self.dense1(x))) + res
+        x = F.relu(self.norm2(self.dense2(x)))
+        return self.dense3(x)
+    hicgat.GATNetSelectiveResidualsUpdated.tail = tail
+
+
 def _worker(rank, world, port, n, kind, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -59,7 +75,7 @@ def _worker(rank, world, port, n, kind, out):
     try:
         hicgat, adj, truth, x = _setup(n)
         from cpu_kernels import CpuKernels
-        hicgat.gat_models._lin = lambda layer, inp: layer(inp)   # torch Linear on CPU tensors
+        _torch_tail(hicgat)
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated()
         tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels())

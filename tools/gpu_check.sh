@@ -22,6 +22,7 @@ for s in $STAGES; do
     bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
     benchg) run bench_graph 600 python bench.py --steps ${STEPS:-20} --warmup 3 --graph --no-cpu-baseline ;;
     benchcpu) run bench_cpu 900 python bench.py ;;
+    c2d) run debug_c2d 300 python tools/debug_c2d.py ;;
     kbench) run kbench 600 python tools/kbench.py --libs ${KLIBS:-hic-gnn_amd/hicgat/libhicgat.so} ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
