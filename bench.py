@@ -50,6 +50,37 @@ def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
     raise KeyError(kind)
 
 
+# timer name (kernels.py) -> HIP kernels launched inside that timed region
+PMC_KERNELS = {
+    "gat_agg_fwd": ["agg_fwd_h2c256_kernel"],
+    "gat_agg_bwd_dst": ["agg_bwd_dst_h2c256_kernel"],
+    "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel"],
+    "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_reduce_kernel", "moments_reduce_kernel"],
+}
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary for ``workload``
+    (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py from two rocprofv3 --pmc passes
+    of this bench: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if not collected."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload:
+            best = d
+    if best is None:
+        return None
+    tot, seen = 0.0, False
+    for pat in PMC_KERNELS[kernel]:
+        for name, v in best["kernels"].items():
+            if pat in name:
+                tot += v["bytes"]
+                seen = True
+    return tot if seen else None
+
+
 def build_workload(name, seed, device):
     import hicgat
     from hicgat import synth
@@ -213,7 +244,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
@@ -223,7 +254,8 @@ def main():
                    "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single"},
         "final_loss": loss_v,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic(dom, args.workload) if world == 1 else None,
                      "alg_bytes_per_launch": alg, "avg_launch_ms": kern[dom]["avg_ms"]},
         "kernels": kern,
     }

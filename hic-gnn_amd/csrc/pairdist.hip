@@ -56,6 +56,8 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
                                                             int64_t ldt, int nb, int64_t t0,
                                                             float4 *__restrict__ part,
                                                             double *__restrict__ mom) {
+  // one dynamic LDS array: [T tile 128x128 fp32 (VEC only)] -- 64 KiB, 16-B aligned
+  extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ float sc[2][BT][3];
   __shared__ float4 colred[4][BT];
   __shared__ double mred[4][7];
@@ -68,6 +70,18 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     J = (int)(t % nb);
   }
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, lane = tid & 63, wv = tid >> 6;
+  if (VEC) {
+    // LDS-DMA the whole T tile (global_load_lds_dwordx4: each wave instruction moves 1 KiB = two
+    // 512-B tile rows, wave-uniform LDS base + lane*16).  Rows past N are clamped to a valid row
+    // (their values are masked below); columns past N lie inside the padded leading dimension.
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = wv * 32 + q * 2 + (lane >> 5);
+      const int gi = min(I * BT + row, N - 1);
+      const float *src = T + (size_t)gi * ldt + (size_t)J * BT + (lane & 31) * 4;
+      __builtin_amdgcn_global_load_lds(src, &tile[(wv * 32 + q * 2) * BT], 16, 0, 0);
+    }
+  }
   for (int k = tid; k < 2 * BT; k += 256) {
     const int which = k / BT, li = k % BT;
     const int g = (which ? J : I) * BT + li;
@@ -81,6 +95,7 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     sc[which][li][1] = y;
     sc[which][li][2] = z;
   }
+  if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   float cx[8], cy[8], cz[8], ax[8], ay[8], az[8];
@@ -103,17 +118,15 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     const int gi = I * BT + lr;
     const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
     float tv[8];
-    if (gi < N) {
+    if (VEC) {  // from the LDS image of the tile (conflict-free ds_read_b128: 16 lanes = one row)
+      const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
+      const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
+      tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
+      tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
+    } else if (gi < N) {
       const float *trow = T + (size_t)gi * ldt + (size_t)J * BT;
-      if (VEC) {
-        const float4 a = *reinterpret_cast<const float4 *>(trow + tx * 4);
-        const float4 b = *reinterpret_cast<const float4 *>(trow + 64 + tx * 4);
-        tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
-        tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
-      } else {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
-      }
+      for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) tv[q] = 0.f;
@@ -311,6 +324,8 @@ __global__ __launch_bounds__(256) void pairdist_fwd_kernel(const float *__restri
 
 using namespace hicgat;
 
+constexpr size_t kTileLds = (size_t)BT * BT * sizeof(float);  // LDS image of one T tile
+
 extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
   if (N <= 0) return 0;
   const int64_t nb = pd_nb(N);
@@ -355,7 +370,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   const bool vec = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) &&
                    ldg >= (int64_t)nb * BT;
   if (vec)
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true>), dim3(tiles), dim3(256), 0,
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true>), dim3(tiles), dim3(256), kTileLds,
                        (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
   else
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false>), dim3(tiles), dim3(256), 0,
@@ -390,7 +405,7 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
                    ldt >= (int64_t)nb * BT;
   if (nt > 0) {
     if (vec)
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, true>), dim3(nt), dim3(256), 0,
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, true>), dim3(nt), dim3(256), kTileLds,
                          (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom);
     else
       hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false>), dim3(nt), dim3(256), 0,

@@ -1,7 +1,8 @@
-"""The in-scope GAT-HiC models on the HIP path, with the reference's forward()/get_model() surface.
+"""The in-scope HiC-GNN models on the HIP path, with the reference's forward()/get_model() surface.
 
 * ``GATNetSelectiveResidualsUpdated``       -- models.py:614-691 (flagship, 601 475 parameters).
 * ``GATNetHeadsChanged3LayersLeakyReLUv2``  -- models.py:1010-1047 (411 651 parameters).
+* ``Net``                                   -- models.py:14-55, the SAGEConv baseline (697 475).
 
 Submodules are registered in the reference's order (so the same seed gives the same initial
 weights and the same state_dict keys).  ``forward`` returns the N x N distance matrix like the
@@ -13,7 +14,7 @@ import torch.nn.functional as F
 from torch.nn import LayerNorm, Linear
 
 from . import ops
-from .nn import GATConv
+from .nn import GATConv, SAGEConv
 
 
 def _lin(layer, x):
@@ -80,7 +81,27 @@ class GATNetHeadsChanged3LayersLeakyReLUv2(_CoordsModel):
         return self.tail(self.conv(x, edge_index))
 
 
+class Net(_CoordsModel):
+    """models.py:14-55: SAGEConv(512, 512) -> relu -> 512-256-128-64-3 with relu between."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = SAGEConv(512, 512)
+        self.densea = Linear(512, 256)
+        self.dense1 = Linear(256, 128)
+        self.dense2 = Linear(128, 64)
+        self.dense3 = Linear(64, 3)
+
+    def get_model(self, x, edge_index):
+        x = F.relu(self.conv(x, edge_index))
+        x = F.relu(_lin(self.densea, x))
+        x = F.relu(_lin(self.dense1, x))
+        x = F.relu(_lin(self.dense2, x))
+        return _lin(self.dense3, x)
+
+
 MODELS = {
     "GATNetSelectiveResidualsUpdated": GATNetSelectiveResidualsUpdated,
     "GATNetHeadsChanged3LayersLeakyReLUv2": GATNetHeadsChanged3LayersLeakyReLUv2,
+    "Net": Net,
 }

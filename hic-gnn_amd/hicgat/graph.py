@@ -86,6 +86,8 @@ class Adj:
         self.storage = _Storage(rowptr, colv, val)
         self.rowptr32 = None
         self.col32 = None
+        self.value32 = None   # SAGEConv edge weight per device CSR entry (0 on the self loops)
+        self.inv_deg = None   # 1 / sum_j w_ij (SAGEConv.adjust_weights, layers.py:41-53)
 
     def sparse_sizes(self):
         return (self.n, self.n)
@@ -107,12 +109,23 @@ class Adj:
         r = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
         keep = r != c
         r, c = r[keep], c[keep]
+        v = self.storage.value()
         r = torch.cat([r, torch.arange(n)])
         c = torch.cat([c, torch.arange(n)])
-        key = torch.sort(r * n + c).values
+        key, perm = torch.sort(r * n + c)
         self.rowptr32 = torch.zeros(n + 1, dtype=torch.int32)
         self.rowptr32[1:] = torch.cumsum(torch.bincount(key // n, minlength=n), 0).to(torch.int32)
         self.col32 = (key % n).to(torch.int32)
+        if v is not None:
+            # the device weights of the self loops are 0; the degree sums run over each row in
+            # ascending column order, in float32 (adj_t.sum(dim=0) of a symmetric matrix)
+            w = torch.cat([v[keep].float(), torch.zeros(n)])[perm].numpy()
+            s = np.zeros(n, dtype=np.float32)
+            np.add.at(s, (key // n).numpy(), w)
+            with np.errstate(divide="ignore"):
+                inv = np.float32(1.0) / s
+            self.value32 = torch.tensor(w).to(device)
+            self.inv_deg = torch.tensor(inv).to(device)
         self.rowptr32 = self.rowptr32.to(device)
         self.col32 = self.col32.to(device)
         return self
@@ -123,7 +136,8 @@ class Adj:
 
     @classmethod
     def from_dense_device(cls, A, keep_host=True):
-        """a13 + a3 on the GPU: CSR of (A != 0 | A.T != 0), i != j, plus self loops.
+        """a13 + a3 on the GPU: CSR of (A != 0 | A.T != 0), i != j, plus self loops, and the
+        networkx edge weights (``value32``) with the SAGEConv normaliser (``inv_deg``).
 
         ``A`` is a float64 [N, N] device tensor.  The host ``storage`` view (without self loops)
         is derived from the device CSR when ``keep_host`` is set."""
@@ -142,6 +156,10 @@ class Adj:
         obj = cls.__new__(cls)
         obj.n = n
         obj.rowptr32, obj.col32 = rowptr, col
+        obj.value32 = torch.empty(nnz, dtype=torch.float32, device=dev)
+        obj.inv_deg = torch.empty(n, dtype=torch.float32, device=dev)
+        _lib.check(lib.hicgat_sage_weights(_lib.ptr(A), n, n, _lib.ptr(rowptr), _lib.ptr(col), _lib.ptr(obj.value32),
+                                           _lib.ptr(obj.inv_deg), s), "hicgat_sage_weights")
         if keep_host:
             rp = rowptr.cpu().long()
             c = col.cpu().long()
@@ -149,7 +167,7 @@ class Adj:
             keep = r != c
             hrp = torch.zeros(n + 1, dtype=torch.long)
             hrp[1:] = torch.cumsum(torch.bincount(r[keep], minlength=n), 0)
-            obj.storage = _Storage(hrp, c[keep], None)
+            obj.storage = _Storage(hrp, c[keep], obj.value32.cpu()[keep])
         else:
             obj.storage = None
         return obj

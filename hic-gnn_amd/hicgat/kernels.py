@@ -102,6 +102,23 @@ class HipKernels:
                    "hicgat_gat_param_grad")
         return datt_l, datt_r, dbias
 
+    # -- f1: SAGEConv (layers.py:41-79) --------------------------------------------------------------
+    def sage_weights(self, A, rowptr, col):
+        n = A.shape[0]
+        w = torch.empty(col.numel(), dtype=torch.float32, device=A.device)
+        inv = torch.empty(n, dtype=torch.float32, device=A.device)
+        _lib.check(self.lib.hicgat_sage_weights(P(A), n, A.stride(0), P(rowptr), P(col), P(w), P(inv),
+                                                _lib.stream(A.device)), "hicgat_sage_weights")
+        return w, inv
+
+    def sage_agg(self, rowptr, col, w, inv, r0, r1, x, z, transpose=False, write_trunc=False):
+        N, F = x.shape
+        with _timed("sage_agg"):
+            _lib.check(self.lib.hicgat_sage_agg(P(rowptr), P(col), P(w), P(inv), N, F, r0, r1, P(x), int(transpose),
+                                                int(write_trunc), P(z), z.stride(0), _lib.stream(x.device)),
+                       "hicgat_sage_agg")
+        return z
+
     # -- a7..a9 -----------------------------------------------------------------------------------
     def num_tiles(self, n):
         return int(self.lib.hicgat_pairdist_num_tiles(n, 0))

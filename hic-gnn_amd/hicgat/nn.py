@@ -63,3 +63,37 @@ class GATConv(torch.nn.Module):
 
     def __repr__(self):
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"
+
+
+class SAGEConv(torch.nn.Module):
+    """Drop-in for the reference's own ``layers.SAGEConv`` (layers.py:12-79).
+
+    Same parameters and state_dict keys (``lin_l.weight``, ``lin_l.bias``, ``lin_r.weight``) and
+    the same init (torch.nn.Linear's, in construction order: the reference never calls its
+    ``reset_parameters``, layers.py:33).  ``forward`` keeps the degree normalisation
+    ``diag(1/colsum) @ adj`` and the ``x.long()`` truncation of the root branch (layers.py:64)."""
+
+    def __init__(self, in_channels, out_channels, normalize=False, root_weight=True, bias=True, **kwargs):
+        super().__init__()
+        if not isinstance(in_channels, int):
+            raise NotImplementedError("bipartite (tuple) in_channels is out of scope")
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.normalize, self.root_weight = normalize, root_weight
+        self.lin_l = Linear(in_channels, out_channels, bias=bias)
+        if root_weight:
+            self.lin_r = Linear(in_channels, out_channels, bias=False)
+
+    def reset_parameters(self):
+        self.lin_l.reset_parameters()
+        if self.root_weight:
+            self.lin_r.reset_parameters()
+
+    def forward(self, x, edge_index):
+        out = ops.sage_conv(x, self.lin_l.weight, self.lin_l.bias,
+                            self.lin_r.weight if self.root_weight else None, edge_index)
+        if self.normalize:
+            out = torch.nn.functional.normalize(out, p=2.0, dim=-1)
+        return out
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"

@@ -249,3 +249,52 @@ def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
     kind_i = {"mse": 0, "combined": 1}[kind]
     loss = _FusedLossFn.apply(coords, truth.buf, truth.n, kind_i, int(tile_range[0]), int(tile_range[1]), stats)
     return loss, stats
+
+
+class _SageConvFn(torch.autograd.Function):
+    """SAGEConv.forward (layers.py:55-77) on the HIP path: one wave-per-row pass writes
+    z = [N_adj x | trunc(x)] and lin_l + lin_r run as ONE GEMM over [W_l | W_r] (K = 2F).  The
+    x.long() branch carries no gradient (as in the reference); d x = N_adj^T (d out W_l)."""
+
+    @staticmethod
+    def forward(ctx, x, W_l, b_l, W_r, rowptr, col, w, inv_deg):
+        K = kernels.default()
+        x = x.contiguous().float()
+        N, F = x.shape
+        root = W_r is not None
+        z = torch.empty((N, 2 * F if root else F), dtype=torch.float32, device=x.device)
+        K.sage_agg(rowptr, col, w, inv_deg, 0, N, x, z, transpose=False, write_trunc=root)
+        Wc = torch.cat([W_l, W_r], dim=1).contiguous() if root else W_l.contiguous()
+        out = torch.empty((N, W_l.shape[0]), dtype=torch.float32, device=x.device)
+        K.gemm(0, 0, N, W_l.shape[0], z.shape[1], z, Wc, out, bias=b_l, name="gemm_fwd")
+        ctx.save_for_backward(z, W_l, rowptr, col, w, inv_deg)
+        ctx.dims = (N, F, root, b_l is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        K = kernels.default()
+        z, W_l, rowptr, col, w, inv_deg = ctx.saved_tensors
+        N, F, root, has_b = ctx.dims
+        dout = dout.contiguous()
+        dx = dWl = db = dWr = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            dWc = weight_grad(K, dout, z)
+            dWl = dWc[:, :F].contiguous()
+            dWr = dWc[:, F:].contiguous() if root else None
+        if has_b and ctx.needs_input_grad[2]:
+            db = K.colsum(dout, torch.empty(dout.shape[1], dtype=torch.float32, device=dout.device))
+        if ctx.needs_input_grad[0]:
+            dagg = K.gemm(0, 1, N, F, dout.shape[1], dout, W_l.contiguous(),
+                          torch.empty((N, F), dtype=torch.float32, device=dout.device), name="gemm_dx")
+            dx = K.sage_agg(rowptr, col, w, inv_deg, 0, N, dagg, torch.empty_like(dagg), transpose=True)
+        return dx, dWl, db, dWr, None, None, None, None
+
+
+def sage_conv(x, W_l, b_l, W_r, adj):
+    """SAGEConv (layers.py:12-79) over a ``hicgat.Adj`` that carries ``value32``/``inv_deg``."""
+    _dev_check(x, W_l, b_l, W_r)
+    if adj.value32 is None or adj.inv_deg is None:
+        raise ValueError("SAGEConv needs the edge weights: build the Adj with values (load_input / "
+                         "Adj.from_dense_device / Adj(row, col, value).to(device))")
+    return _SageConvFn.apply(x, W_l, b_l, W_r, adj.rowptr32, adj.col32, adj.value32, adj.inv_deg)

@@ -170,6 +170,20 @@ int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, 
                            hicgat_stream_t stream);
 size_t hicgat_ln_relu_res_workspace_bytes(int W);
 
+/* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
+ * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --
+ * the networkx weight utils.load_input assigns (utils.py:37-52): A[max(i,j), min(i,j)] when
+ * non-zero, else A[min, max]; 0 on the self loops -- and inv_deg[i] = 1 / sum_j w_ij, the
+ * SAGEConv.adjust_weights normaliser (layers.py:41-53; sum in ascending column order).
+ * hicgat_sage_agg: z[i, 0:F] = sum_{j != i} (inv_deg[i] * w_ij) x[j]  (matmul(norm_mat, x), :74-77)
+ * over rows [row_begin, row_end); transpose != 0 weights by inv_deg[j] instead (the adjoint,
+ * d agg -> d x); write_trunc != 0 also writes z[i, F:2F] = trunc(x[i]) (x.long().float(), :64). */
+int hicgat_sage_weights(const double *A, int N, int64_t lda, const int32_t *rowptr, const int32_t *col,
+                        float *weights, float *inv_deg, hicgat_stream_t stream);
+int hicgat_sage_agg(const int32_t *rowptr, const int32_t *col, const float *weights, const float *inv_deg,
+                    int N, int F, int row_begin, int row_end, const float *x, int transpose, int write_trunc,
+                    float *z, int64_t ldz, hicgat_stream_t stream);
+
 /* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
  * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
  *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);

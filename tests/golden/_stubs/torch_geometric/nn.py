@@ -15,6 +15,10 @@ class MessagePassing(torch.nn.Module):
         super().__init__()
         self.aggr = aggr
 
+    def propagate(self, edge_index, size=None, **kwargs):
+        """PyG 1.7.2 fused path for a SparseTensor adjacency: message_and_aggregate(adj_t, ...)."""
+        return self.message_and_aggregate(edge_index, **kwargs)
+
 
 class GCNConv(torch.nn.Module):
     def __init__(self, *a, **k):

@@ -1,4 +1,5 @@
-"""Stub of ``torch_sparse.SparseTensor``: COO -> sorted/coalesced CSR, ``to_symmetric`` (sum)."""
+"""Stub of ``torch_sparse`` 0.6.11: ``SparseTensor`` (COO -> sorted/coalesced CSR,
+``to_symmetric`` (sum), ``sum(dim=0)``) and ``matmul`` (sparse x diag-sparse, sparse x dense sum)."""
 import numpy as np
 import torch
 
@@ -41,6 +42,13 @@ class SparseTensor:
         self.storage = _Storage(rowptr, c, vsum)
         self._row = r
 
+    def sum(self, dim):
+        """torch_sparse.reduce.sum: dim 0 -> scatter_add of the values by column (CSR order)."""
+        if dim != 0:
+            raise NotImplementedError
+        v = self.storage.value()
+        return torch.zeros(self.n, dtype=v.dtype).scatter_add_(0, self.storage.col(), v)
+
     def to_symmetric(self):
         r, c = self._row, self.storage.col()
         v = self.storage.value()
@@ -48,5 +56,31 @@ class SparseTensor:
         return SparseTensor(torch.cat([r, c]), torch.cat([c, r]), vv, (self.n, self.n))
 
 
-def matmul(*a, **k):
-    raise NotImplementedError("torch_sparse.matmul is out of scope for the GAT fixtures")
+def matmul(src, other, reduce="sum"):
+    """torch_sparse.matmul for the two uses in layers.py: diag-sparse @ sparse (spspmm; each
+    output entry is a single product) and sparse @ dense with reduce sum/add (spmm_sum: every row
+    accumulated sequentially in CSR order, multiply then add)."""
+    rp, c, v = src.storage.rowptr(), src.storage.col(), src.storage.value()
+    if isinstance(other, SparseTensor):
+        orp, oc, ov = other.storage.rowptr(), other.storage.col(), other.storage.value()
+        rows, cols, vals = [], [], []
+        for i in range(src.n):
+            for e in range(int(rp[i]), int(rp[i + 1])):
+                k = int(c[e])
+                if k >= other.n:
+                    continue
+                for f in range(int(orp[k]), int(orp[k + 1])):
+                    rows.append(i)
+                    cols.append(int(oc[f]))
+                    vals.append(v[e] * ov[f])
+        val = torch.stack(vals) if vals else torch.zeros(0, dtype=ov.dtype)
+        return SparseTensor(torch.tensor(rows), torch.tensor(cols), val, (other.n, other.n))
+    if reduce not in ("sum", "add"):
+        raise NotImplementedError(reduce)
+    out = []
+    for i in range(src.n):
+        acc = torch.zeros(other.shape[1], dtype=other.dtype)
+        for e in range(int(rp[i]), int(rp[i + 1])):
+            acc = acc + v[e] * other[int(c[e])]
+        out.append(acc)
+    return torch.stack(out)

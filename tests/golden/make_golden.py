@@ -15,6 +15,9 @@ It imports the reference ``utils.py`` / ``models.py`` (``/root/reference``) with
   under ``torch.manual_seed(0)`` on chr19 1mb with 0.1*N(0,1) features: initial state_dict,
   forward distance matrix, coordinates, MSE vs cont2dist(y, 0.5), every parameter gradient, and the
   combined-loss value of ``HiC_GAT_generalize_directly.py:206-225``.
+* ``model_Net.npz``    -- the baseline SAGE model (models.py:14-55 over layers.py:12-79) on chr19
+  1mb: init state, SAGE aggregate, distances, coordinates, MSE, gradients; plus the key/shape
+  layout of the shipped ``Outputs/GM12878_1mb_chr19_list_weights.pt`` (safe loader).
 * ``train_<name>.npz``  -- the ``HiC-GNN_main.py:117-132`` loop run for a fixed K on the same input
   (deterministic algorithms), loss history and final coordinates.
 
@@ -101,6 +104,37 @@ def model_case(ref_utils, ref_models, cls_name, data, seed=0):
     return model
 
 
+def net_case(ref_utils, ref_models, ref, mat, seed=0):
+    """The baseline ``Net`` (models.py:14-55, SAGEConv of layers.py:12-79) on chr19 1mb.
+
+    Features are 1.5*N(0,1) so that ``x.long()`` (layers.py:64) keeps non-zero integers.  The
+    key/shape layout of the shipped trained state_dict (``Outputs/*_weights.pt``, read with
+    ``weights_only=True``) is recorded too."""
+    rng = np.random.default_rng(5)
+    feats = (1.5 * rng.standard_normal((mat.shape[0], 512))).astype(np.float32)
+    data = ref_utils.load_input(mat.copy(), feats)
+    torch.manual_seed(seed)
+    model = ref_models.Net()
+    x = data.x.float()
+    truth = ref_utils.cont2dist(data.y.clone(), 0.5)
+    state = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    out = model(x, data.edge_index)
+    coords = model.get_model(x, data.edge_index)
+    agg = model.conv.message_and_aggregate(data.edge_index, (x, x))
+    mse = torch.nn.MSELoss()(out.float(), truth.float())
+    mse.backward()
+    grads = {f"grad::{k}": p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
+    trained = torch.load(os.path.join(ref, "Outputs", "GM12878_1mb_chr19_list_weights.pt"), weights_only=True,
+                         map_location="cpu")
+    np.savez_compressed(
+        os.path.join(HERE, "model_Net.npz"),
+        x=x.numpy(), agg=agg.detach().numpy(), out=out.detach().numpy(), coords=coords.detach().numpy(),
+        mse=np.float64(mse.item()), trained_keys=np.array(list(trained.keys())),
+        trained_shapes=np.array([list(v.shape) + [0] * (2 - v.dim()) for v in trained.values()]),
+        **{f"state::{k}": v for k, v in state.items()}, **grads)
+    print(f"model_Net: mse={mse.item():.8g}; trained keys {list(trained.keys())}")
+
+
 def train_case(ref_utils, ref_models, cls_name, data, steps=25, seed=0):
     torch.use_deterministic_algorithms(True)
     torch.manual_seed(seed)
@@ -138,6 +172,7 @@ def main(ref):
     for cls in ("GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2"):
         model_case(ref_utils, ref_models, cls, data1)
     train_case(ref_utils, ref_models, "GATNetSelectiveResidualsUpdated", data1)
+    net_case(ref_utils, ref_models, ref, ref_utils.convert_to_matrix(l1))
 
 
 if __name__ == "__main__":

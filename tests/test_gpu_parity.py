@@ -1,7 +1,8 @@
 """GPU parity: every HIP kernel (through libhicgat.so's C ABI) against the CPU oracle / fixtures.
 
 Tolerances (north star: coordinates and loss within 1e-5 relative fp32):
-  * graph build (a3, a13) and cont2dist (a12): bit-exact;
+  * graph build (a3, a13): bit-exact; cont2dist (a12): bit-exact with IEEE sqrt, <= 1 ulp of the
+    reference fixture at factor 0.5 (torch CPU float64 sqrt is MKL VML, not correctly rounded);
   * Adam (a10): bit-exact against the torch-CPU restatement;
   * GATConv forward output, coordinates, loss: rtol 1e-5 (plus a tiny atol for values near 0);
   * gradients: rtol 1e-4 relative to the tensor's max magnitude (fp32 reassociation over up to
@@ -71,15 +72,37 @@ def test_csr_from_dense_asymmetric_and_isolated():
     assert adj.rowptr32[8].item() - adj.rowptr32[7].item() == 1                # self loop only
 
 
+def _cont2dist_ieee(y, f):
+    """utils.py:75-80 with IEEE-correctly-rounded float64 sqrt (numpy)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = 1.0 / y
+        d = np.sqrt(d) if f == 0.5 else d ** f
+    np.fill_diagonal(d, 0)
+    m = np.max(np.nan_to_num(d, posinf=0))
+    return np.nan_to_num(d, posinf=m) / m
+
+
 @pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth256"])
 @pytest.mark.parametrize("factor,key", [(0.5, "truth05"), (1, "truth1")])
 def test_cont2dist_bit_exact(case, factor, key):
+    """factor 1: bit-exact with the reference fixture.  factor 0.5: bit-exact with IEEE sqrt, and
+    within 1 float64 ulp of the fixture -- the reference's torch CPU sqrt on float64 goes through
+    MKL VML (tensors above ~128 elements), which returns the correctly rounded value minus 1 ulp
+    for ~0.7 % of inputs ('Oracle and parity')."""
     import hicgat
     g, y, _ = _golden_graph(case)
-    t = hicgat.cont2dist(y, factor)
-    assert np.array_equal(t.cpu().numpy(), g[key])
+    t = hicgat.cont2dist(y, factor).cpu().numpy()
+    ieee = _cont2dist_ieee(y.cpu().numpy(), factor)
+    assert np.array_equal(t, ieee)
+    ulps = np.abs(t.view(np.int64) - g[key].view(np.int64))
+    if factor == 1:
+        assert ulps.max() == 0
+    else:
+        assert ulps.max() <= 1 and (ulps > 0).mean() < 0.02
     tr = hicgat.Truth.from_contacts(y, factor)
-    assert np.array_equal(tr.dense().cpu().numpy(), g[key].astype(np.float32))
+    d32 = tr.dense().cpu().numpy()
+    assert np.array_equal(d32, ieee.astype(np.float32))
+    assert np.abs(d32.view(np.int32) - g[key].astype(np.float32).view(np.int32)).max() <= 1
     assert tr.ld % 128 == 0
     # convert_to_matrix's triu + tril(T, 1) is asymmetric when the list has lower-triangle entries
     assert tr.symmetric == bool(np.array_equal(g[key], g[key].T))
@@ -410,10 +433,13 @@ def test_model_matches_reference_fixture(name):
     model.zero_grad()
     lm, _, _ = model.loss(x, adj, tr, "mse")
     lm.backward()
+    gscale = max(pr.grad.abs().max().item() for pr in ref.parameters())
     for (k, p), pr in zip(model.named_parameters(), ref.parameters()):
-        scale = pr.grad.abs().max().item()
-        if k == "dense3.bias" or (k == "dense2.bias" and name.endswith("v2")):
-            assert p.grad.abs().max().item() < 1e-5 * max(scale, 1e-3), k   # exactly 0 in exact arithmetic
+        if pr.grad.abs().max().item() < 1e-3 * gscale:
+            # zero in exact arithmetic: the last bias by translation invariance, and (v2 at these
+            # 0.1-scale inputs) every bias whose units keep one activation sign over all nodes,
+            # which makes sum_i g_i = 0 propagate up the tail; both sides are fp32 noise
+            assert p.grad.abs().max().item() < 1e-3 * gscale, k
             continue
         assert _rel(p.grad.cpu(), pr.grad) < 2e-4, k
 
@@ -548,3 +574,121 @@ def test_full_size_synth20000_properties():
     gsum = cc.grad.double().sum(0).abs().max().item()
     assert gsum < 1e-4 * cc.grad.abs().max().item() * np.sqrt(n)
     assert np.isfinite(stats.cpu().numpy()[:9]).all()
+
+
+# ---------------------------------------------------------------- f1: SAGEConv / Net baseline
+@pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth256"])
+def test_sage_weights_bit_exact(case):
+    """Device edge weights (networkx semantics) and 1/degree == the host derivation and oracle."""
+    import hicgat
+    from oracle import sage
+    g, y, adj = _golden_graph(case)
+    n = y.shape[0]
+    assert np.array_equal(adj.storage.value().numpy(), g["value"])
+    rp, c, v = (torch.tensor(g[k]) for k in ("rowptr", "col", "value"))
+    r = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    host = hicgat.Adj(r, c, v, (n, n)).to("cpu")
+    assert torch.equal(adj.value32.cpu(), host.value32)
+    assert np.array_equal(adj.inv_deg.cpu().numpy(), sage.degree_inverse(g["rowptr"], g["col"], g["value"], n))
+
+
+@pytest.mark.parametrize("n,p,F", [(58, 1.0, 512), (257, 0.05, 512), (1000, 0.1, 512), (130, 0.3, 100)])
+def test_sage_agg_matches_oracle(n, p, F):
+    import hicgat
+    from oracle import graph as ogr
+    from oracle import sage
+    rng = np.random.default_rng(n)
+    a = np.triu(np.where(rng.random((n, n)) < p, rng.integers(1, 1000, (n, n)).astype(np.float64), 0.0), 1)
+    if n == 257:
+        a[5, :] = 0
+        a[:, 5] = 0                        # isolated node: inv_deg = inf, its row aggregates nothing
+    a = a + a.T
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    rp, c, v = ogr.csr_from_matrix(a)
+    x = torch.tensor((1.5 * rng.standard_normal((n, F))).astype(np.float32))
+    ref = sage.sage_aggregate(x, rp, c, v)
+    K = hicgat.kernels.default()
+    xd = x.to(DEV)
+    z = torch.full((n, 2 * F), np.nan, device=DEV)
+    K.sage_agg(adj.rowptr32, adj.col32, adj.value32, adj.inv_deg, 0, n, xd, z, write_trunc=True)
+    np.testing.assert_allclose(z[:, :F].cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6 * ref.abs().max().item())
+    assert torch.equal(z[:, F:].cpu(), x.long().float())
+    # adjoint (d agg -> d x) against the oracle's autograd
+    xr = x.clone().double().requires_grad_(True)
+    gout = torch.tensor(rng.standard_normal((n, F)))
+    (sage._SageAggFn.apply(xr, torch.tensor(rp), torch.tensor(c), torch.tensor(v)) * gout).sum().backward()
+    dx = K.sage_agg(adj.rowptr32, adj.col32, adj.value32, adj.inv_deg, 0, n, gout.float().to(DEV),
+                    torch.empty((n, F), device=DEV), transpose=True)
+    assert _rel(dx.cpu(), xr.grad) < 1e-5
+    # a row range writes only its rows
+    z2 = torch.zeros((n, F), device=DEV)
+    K.sage_agg(adj.rowptr32, adj.col32, adj.value32, adj.inv_deg, 3, n // 2, xd, z2)
+    assert torch.equal(z2[3:n // 2], z[3:n // 2, :F]) and z2[:3].abs().sum() == 0 and z2[n // 2:].abs().sum() == 0
+
+
+def test_net_matches_reference_fixture():
+    """The baseline Net (models.py:14-55, layers.py SAGEConv) on chr19 1 mb vs the fixture
+    recorded from the reference's code: coordinates 1e-5; D / MSE vs exact distances; gradients
+    vs the oracle with exact distances."""
+    import hicgat
+    from oracle import gat as og
+    from oracle import sage
+    fx = load_golden("model_Net.npz")
+    g, y, adj = _golden_graph("chr19_1mb")
+    state = {k[len("state::"):]: torch.tensor(v) for k, v in fx.items() if k.startswith("state::")}
+    model = hicgat.Net().to(DEV)
+    model.load_state_dict(state)
+    x = torch.tensor(fx["x"], device=DEV)
+    coords = model.get_model(x, adj)
+    np.testing.assert_allclose(coords.detach().cpu().numpy(), fx["coords"], rtol=1e-5,
+                               atol=1e-5 * np.abs(fx["coords"]).max())
+    out = model(x, adj)
+    c64 = torch.tensor(fx["coords"]).double()
+    d_exact = torch.cdist(c64, c64, compute_mode="donot_use_mm_for_euclid_dist")
+    np.testing.assert_allclose(out.detach().cpu().numpy(), d_exact.numpy(), rtol=1e-5, atol=1e-5 * d_exact.max().item())
+    tr = hicgat.Truth.from_contacts(y, 0.5)
+    loss, stats, _ = model.loss(x, adj, tr, "mse")
+    mse_exact = float(torch.nn.functional.mse_loss(d_exact, torch.tensor(g["truth05"])))
+    assert abs(stats[7].item() - mse_exact) <= 2e-5 * mse_exact
+    ref = sage.Net()
+    ref.load_state_dict(state)
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        radj = (torch.tensor(g["rowptr"]), torch.tensor(g["col"]), torch.tensor(g["value"]))
+        torch.nn.functional.mse_loss(ref(torch.tensor(fx["x"]), radj).float(),
+                                     torch.tensor(g["truth05"]).float()).backward()
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    model.zero_grad()
+    loss.backward()
+    gscale = max(p.grad.abs().max().item() for p in ref.parameters())
+    for (k, p), pr in zip(model.named_parameters(), ref.parameters()):
+        if pr.grad.abs().max().item() < 1e-3 * gscale:
+            assert p.grad.abs().max().item() < 1e-3 * gscale, k
+            continue
+        assert _rel(p.grad.cpu(), pr.grad) < 2e-4, k
+
+
+def test_net_train_loop_tracks_oracle():
+    """HiC-GNN_main.py loop with the baseline Net (fixed K = 10) vs the oracle loop."""
+    import hicgat
+    from oracle import gat as og
+    from oracle import loop as ol
+    from oracle import sage
+    fx = load_golden("model_Net.npz")
+    g, y, adj = _golden_graph("chr19_1mb")
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        torch.manual_seed(0)
+        ref = sage.Net()
+        radj = (torch.tensor(g["rowptr"]), torch.tensor(g["col"]), torch.tensor(g["value"]))
+        ref_hist = np.array(ol.train(ref, torch.tensor(fx["x"]), radj, torch.tensor(g["truth05"]), steps=10))
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    torch.manual_seed(0)
+    model = hicgat.Net().to(DEV)
+    data = hicgat.Data(x=torch.tensor(fx["x"], device=DEV), edge_index=adj, y=y)
+    _, hist = hicgat.train.train(model, data, hicgat.Truth.from_contacts(y, 0.5), steps=10)
+    rel = np.abs(np.array(hist) - ref_hist) / ref_hist
+    assert rel[0] < 1e-5 and rel[1] < 1e-4, rel[:3]
+    assert np.all(rel < 0.05), rel

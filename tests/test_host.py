@@ -86,3 +86,23 @@ def test_synthetic_generator_density_and_determinism():
     assert np.all(i < j) and np.all(c >= 1)
     i, j, c = synth.contact_pairs(200, density=None, seed=0)
     assert len(i) == 200 * 199 // 2
+
+
+def test_adj_host_sage_weights_match_oracle():
+    """Adj(row, col, value).to(device) derives the SAGEConv weights of the set_diag'd CSR and the
+    1/degree normaliser on the host (no GPU needed for device='cpu')."""
+    import hicgat
+    from conftest import load_golden
+    from oracle import sage
+    g = load_golden("graph_chr19_500kb.npz")
+    rp, c, v = (torch.tensor(g[k]) for k in ("rowptr", "col", "value"))
+    n = rp.numel() - 1
+    r = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    adj = hicgat.Adj(r, c, v, (n, n)).to("cpu")
+    rp2 = adj.rowptr32.long()
+    c2 = adj.col32.long()
+    r2 = torch.repeat_interleave(torch.arange(n), rp2[1:] - rp2[:-1])
+    diag = r2 == c2
+    assert diag.sum().item() == n and torch.all(adj.value32[diag] == 0)
+    assert torch.equal(adj.value32[~diag], v.float())
+    assert np.array_equal(adj.inv_deg.numpy(), sage.degree_inverse(g["rowptr"], g["col"], g["value"], n))

@@ -126,3 +126,66 @@ def test_adam_restatement_matches_torch():
         opt.step()
         p, m, v = loop.adam_reference_step(p, g, m, v, step)
         assert np.array_equal(p, tp.detach().numpy())
+
+
+# ---------------------------------------------------------------- f1: SAGEConv / Net baseline
+def _net_adj(g):
+    return (torch.tensor(g["rowptr"]), torch.tensor(g["col"]), torch.tensor(g["value"]))
+
+
+def test_net_init_and_state_layout_match_reference(golden):
+    """models.py:14-55 init under seed 0, and the key/shape layout of the shipped trained
+    state_dict (Outputs/GM12878_1mb_chr19_list_weights.pt)."""
+    import hicgat
+    from oracle import sage
+    fx = golden("model_Net.npz")
+    for cls in (sage.Net, hicgat.Net):
+        torch.manual_seed(0)
+        sd = cls().state_dict()
+        assert list(sd) == [k[len("state::"):] for k in fx if k.startswith("state::")]
+        for k, v in sd.items():
+            assert np.array_equal(v.numpy(), fx["state::" + k]), k
+        assert list(sd) == list(fx["trained_keys"])
+        for v, shp in zip(sd.values(), fx["trained_shapes"]):
+            assert list(v.shape) == [s for s in shp if s], shp
+
+
+def test_net_forward_backward_matches_reference(golden):
+    """Oracle SAGEConv + Net against the reference's layers.py / models.py (fixture): the
+    aggregate, coordinates and distances bit-exact, gradients to 1e-6 relative."""
+    from oracle import sage
+    torch.set_num_threads(1)
+    fx = golden("model_Net.npz")
+    g = golden("graph_chr19_1mb.npz")
+    m = sage.Net()
+    m.load_state_dict({k[len("state::"):]: torch.tensor(v) for k, v in fx.items() if k.startswith("state::")})
+    x = torch.tensor(fx["x"])
+    adj = _net_adj(g)
+    agg = sage.sage_aggregate(x, *adj)
+    assert np.array_equal(agg.numpy(), fx["agg"])
+    assert np.abs(np.trunc(fx["x"])).max() >= 1          # the x.long() branch is exercised
+    coords = m.get_model(x, adj)
+    np.testing.assert_array_equal(coords.detach().numpy(), fx["coords"])
+    out = m(x, adj)
+    np.testing.assert_array_equal(out.detach().numpy(), fx["out"])
+    mse = torch.nn.functional.mse_loss(out.float(), torch.tensor(g["truth05"]).float())
+    assert mse.item() == float(fx["mse"])
+    mse.backward()
+    for k, p in m.named_parameters():
+        ref = fx["grad::" + k]
+        assert np.max(np.abs(p.grad.numpy() - ref)) <= 1e-6 * max(np.abs(ref).max(), 1e-12), k
+
+
+def test_sage_adjoint_is_transpose():
+    """The oracle's d x = N^T g equals the transpose of the dense normalised adjacency."""
+    from oracle import sage
+    rng = np.random.default_rng(0)
+    a = np.triu(np.where(rng.random((40, 40)) < 0.3, rng.random((40, 40)), 0.0), 1)
+    a = a + a.T
+    rp, c, v = graph.csr_from_matrix(a)
+    x = torch.tensor(rng.standard_normal((40, 8)), dtype=torch.float64, requires_grad=True)
+    gout = torch.tensor(rng.standard_normal((40, 8)))
+    (sage._SageAggFn.apply(x, torch.tensor(rp), torch.tensor(c), torch.tensor(v)) * gout).sum().backward()
+    inv = sage.degree_inverse(rp, c, v, 40)
+    dense = (np.asarray(a, np.float32) * inv[:, None]).astype(np.float64)   # fp32 weights, as N
+    np.testing.assert_allclose(x.grad.numpy(), dense.T @ gout.numpy(), rtol=1e-6)

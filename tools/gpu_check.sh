@@ -26,5 +26,9 @@ for s in $STAGES; do
     kbench) run kbench 600 python tools/kbench.py --libs ${KLIBS:-hic-gnn_amd/hicgat/libhicgat.so} ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
+               python bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+           run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
+               python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
 done
