@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
 __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict__ part, int nblk,
                                                          int D, float *__restrict__ datt_s,
                                                          float *__restrict__ datt_d,
-                                                         float *__restrict__ dbias) {
+                                                         float *__restrict__ dbias, int accumulate) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -232,7 +232,8 @@ __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict
   if (grp == 0 && c < 3 * D) {
     const float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
     const int which = c / D, cc = c % D;
-    (which == 0 ? datt_s : which == 1 ? datt_d : dbias)[cc] = t;
+    float *o = (which == 0 ? datt_s : which == 1 ? datt_d : dbias) + cc;
+    *o = t + (accumulate ? *o : 0.f);
   }
 }
 
@@ -284,7 +285,7 @@ extern "C" size_t hicgat_gat_param_grad_workspace_bytes(int N, int D) {
 
 extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
                                      const float *row_stats, int N, int H, int C, float *datt_src,
-                                     float *datt_dst, float *dbias, void *workspace,
+                                     float *datt_dst, float *dbias, int accumulate, void *workspace,
                                      size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || H <= 0 || C <= 0 || (C % 4) != 0) return HICGAT_EINVAL;
   const int D = H * C;
@@ -300,7 +301,7 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
     HICGAT_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 63) / 64), dim3(256), 0,
-                     (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias);
+                     (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias, accumulate);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -15,8 +15,8 @@
 // K-major (As[k][m], Bs[k][n]) so every MFMA operand read is 32 consecutive floats; the next
 // K-step is prefetched into registers under the current step's MFMAs.  K can be split over
 // gridDim.z: each split writes an fp32 partial slab and a second kernel adds the slabs in split
-// order (deterministic, no float atomics).
-#include "common.hpp"
+// order (deterministic, no float atomics; reduce.hip).
+#include "reduce.hpp"
 
 namespace hicgat {
 
@@ -158,39 +158,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, 
   }
 }
 
-// C[m][n] = sum_z slab[z][m][n] (+ bias[n]), splits added in order.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ slab, int splits,
-                                                            int M, int N, float *__restrict__ C,
-                                                            int64_t ldc, const float *__restrict__ bias,
-                                                            int accumulate) {
-  const int64_t total = (int64_t)M * N;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * total + i];
-    const int m = (int)(i / N), n = (int)(i % N);
-    float *o = C + (size_t)m * ldc + n;
-    *o = s + (bias ? bias[n] : 0.f) + (accumulate ? *o : 0.f);
-  }
-}
-
-// out[n] = sum_k A[k][n] over K rows (bias gradient of a Linear layer), deterministic two-stage.
-constexpr int kColBlocks = 128;
-__global__ __launch_bounds__(256) void colsum_stage1(const float *__restrict__ A, int64_t lda, int K, int N,
-                                                     int rows_per_block, float *__restrict__ part) {
-  const int k0 = blockIdx.x * rows_per_block, k1 = min(K, k0 + rows_per_block);
-  for (int n = threadIdx.x; n < N; n += 256) {
-    float s = 0.f;
-    for (int k = k0; k < k1; ++k) s += A[(size_t)k * lda + n];
-    part[(size_t)blockIdx.x * N + n] = s;
-  }
-}
-__global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int nblk, int N,
-                                                     float *__restrict__ out) {
+__global__ void colsum_zero_kernel(float *out, int N, int accumulate) {
   const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * N + n];
-  out[n] = s;
+  if (n < N && !accumulate) out[n] = 0.f;
 }
 
 template <int BM, int BN, bool AK, bool BK_>
@@ -210,10 +180,9 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
                        N, K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
   HICGAT_CHECK_LAUNCH();
   if (splits > 1) {
-    const int64_t total = (int64_t)M * N;
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, splits, M, N, C, ldc, bias, acc);
-    HICGAT_CHECK_LAUNCH();
+    // C[m][n] = sum_z slab[z][m][n] (+ bias[n]) (+ C), splits added in order
+    const ColOut o{C, ldc, N, nullptr, bias, acc};
+    return colsum_wide_launch(slab, (int64_t)M * N, splits, (int64_t)M * N, o, s);
   }
   return HICGAT_OK;
 }
@@ -253,22 +222,21 @@ extern "C" int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, cons
   return dispatch<true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, s);
 }
 
-extern "C" size_t hicgat_colsum_workspace_bytes(int N) { return (size_t)kColBlocks * N * sizeof(float); }
+extern "C" size_t hicgat_colsum_workspace_bytes(int K, int N) { return colsum_workspace_bytes(K, N); }
 
-extern "C" int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, void *workspace,
+extern "C" int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                              size_t workspace_bytes, hicgat_stream_t stream) {
   if (K < 0 || N < 0) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
-  if (!A || !out || !workspace || workspace_bytes < hicgat_colsum_workspace_bytes(N)) return HICGAT_EINVAL;
+  if (!out || (K > 0 && !A)) return HICGAT_EINVAL;
+  const size_t need = colsum_workspace_bytes(K, N);
+  if (need > 0 && (!workspace || workspace_bytes < need)) return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const int rpb = K > 0 ? (K + kColBlocks - 1) / kColBlocks : 1;
-  const int nblk = K > 0 ? (K + rpb - 1) / rpb : 0;
-  float *part = static_cast<float *>(workspace);
-  if (nblk > 0) {
-    hipLaunchKernelGGL(colsum_stage1, dim3(nblk), dim3(256), 0, s, A, lda, K, N, rpb, part);
+  const ColOut o{out, 0, N, nullptr, nullptr, accumulate};
+  if (K == 0) {  // empty sum
+    hipLaunchKernelGGL(colsum_zero_kernel, dim3((N + 255) / 256), dim3(256), 0, s, out, N, accumulate);
     HICGAT_CHECK_LAUNCH();
+    return HICGAT_OK;
   }
-  hipLaunchKernelGGL(colsum_stage2, dim3((N + 255) / 256), dim3(256), 0, s, part, nblk, N, out);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  return colsum_launch(A, lda, K, N, o, static_cast<float *>(workspace), s);
 }

@@ -7,9 +7,9 @@
 //             (biased variance, torch.nn.LayerNorm semantics), saves (mean, rstd) per row;
 //   backward: g = dz * [pre > 0];  dgamma += g * yhat;  dbeta += g;  dyhat = g * gamma;
 //             dy = rstd * (dyhat - mean(dyhat) - yhat * mean(dyhat * yhat));  dres = dz.
-// dgamma/dbeta: per-wave register partials over a grid-stride row loop, then a fixed-order
-// reduction over waves (deterministic).  Width W in {64, 128, 256} (W/64 values per lane).
-#include "common.hpp"
+// dgamma/dbeta: per-wave register partials over a grid-stride row loop, then the fixed-order
+// column reduction of reduce.hip over the waves (deterministic).  Width W in {64, 128, 256} (W/64 values per lane).
+#include "reduce.hpp"
 
 namespace hicgat {
 
@@ -94,28 +94,6 @@ __global__ __launch_bounds__(256) void ln_relu_res_bwd_kernel(const float *__res
   }
 }
 
-// block = 64 output columns x 4 groups; group g adds the partials of waves g, g+4, ...; the four
-// group sums are combined in order (deterministic).
-__global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float *__restrict__ part, int nw, int W,
-                                                              float *__restrict__ dgamma,
-                                                              float *__restrict__ dbeta, int accumulate) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int which = c / W, cc = c % W;
-  float s = 0.f;
-  if (c < 2 * W) {
-    for (int w = grp; w < nw; w += 4) s += part[((size_t)w * 2 + which) * W + cc];
-  }
-  red[grp][cl] = s;
-  __syncthreads();
-  if (grp == 0 && c < 2 * W) {
-    const float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
-    float *o = which == 0 ? dgamma : dbeta;
-    o[cc] = t + (accumulate ? o[cc] : 0.f);
-  }
-}
-
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -139,7 +117,9 @@ extern "C" int hicgat_ln_relu_res_fwd(const float *y, int64_t ldy, int M, int W,
   return HICGAT_OK;
 }
 
-extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W) { return (size_t)kLnWaves * 2 * W * sizeof(float); }
+extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W) {
+  return (size_t)kLnWaves * 2 * W * sizeof(float) + colsum_workspace_bytes(kLnWaves, 2 * W);
+}
 
 extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, int W,
                                       const float *row_stats, const float *gamma, const float *beta, float *dy,
@@ -159,8 +139,7 @@ extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t l
   else
     hipLaunchKernelGGL(ln_relu_res_bwd_kernel<256>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, part);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((2 * W + 63) / 64), dim3(256), 0, s, part, kLnWaves, W, dgamma,
-                     dbeta, accumulate);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  // dgamma / dbeta = column sums of the per-wave partials [kLnWaves, 2W] (fixed order)
+  const ColOut o{dgamma, 0, W, dbeta, nullptr, accumulate};
+  return colsum_launch(part, 2 * W, kLnWaves, 2 * W, o, part + (size_t)kLnWaves * 2 * W, s);
 }

@@ -11,6 +11,8 @@
 // w*(c_i - c_j) into row partials (reduced over the 16 tx lanes) and column partials (reduced over
 // ty through LDS).  Partials go to a [tile][2][128] float4 slab and a second kernel adds, per row,
 // the slabs of every tile touching it in a fixed order: bitwise reproducible, no float atomics.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace hicgat {
@@ -32,11 +34,18 @@ __device__ inline void tri_decode(int64_t t, int nb, int &I, int &J) {
   J = (int)(Ii + (t - tri_start(Ii, nb)));
 }
 
-__device__ __forceinline__ float sum16(float v) {  // over the 16 lanes sharing lane>>4
-  v += __shfl_xor(v, 8);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 1);
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 16 lanes of a DPP row (the 16 tx lanes sharing ty): row rotations by 8 and 4, then
+// quad permutes (xor 2, xor 1); VALU-only, every lane ends with the row sum.
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp<0x128>(v);   // row_ror:8
+  v += dpp<0x124>(v);   // row_ror:4
+  v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
   return v;
 }
 
@@ -48,9 +57,101 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return *reinterpret_cast<double *>(&q);
 }
 
+// Per-thread accumulators of one tile: the moments and the column partials of its 8 columns.
+struct TileAcc {
+  float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f, dg = 0.f;
+  float ax[8], ay[8], az[8];
+};
+
+// The 8 rows x 8 columns of one thread.  MASK: the diagonal and the edge tiles (row / column
+// bounds, i < j on the diagonal, the diagonal moment); interior tiles take MASK = false and do
+// no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
+// w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
+template <int MODE, bool VEC, bool PEARSON, bool MASK>
+__device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int N, int I, int J,
+                                          const float *tile, const float (*sc)[BT][3], int tx, int ty,
+                                          const float *cx, const float *cy, const float *cz, const int *gj,
+                                          float4 *__restrict__ prow, TileAcc &A) {
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
+    const int gi = I * BT + lr;
+    const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
+    float tv[8];
+    if (VEC) {  // from the LDS image of the tile (conflict-free ds_read_b128: 16 lanes = one row)
+      const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
+      const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
+      tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
+      tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
+    } else if (gi < N) {
+      const float *trow = T + (size_t)gi * ldt + (size_t)J * BT;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tv[q] = 0.f;
+    }
+    float px = 0.f, py = 0.f, pz = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float dx = rx - cx[q], dy = ry - cy[q], dz = rz - cz[q];
+      const float d2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+      // one v_rsq for both d and 1/d (1-2 ulp; the reference's own mm-formula cdist is far
+      // coarser)
+      const float inv = fminf(__builtin_amdgcn_rsqf(d2), 1e30f);
+      const float d = d2 * inv;
+      const float tt = tv[q];
+      float w;
+      if (MODE == MODE_SYM) {
+        const float r = d - tt;
+        if (MASK) {
+          bool valid = gi < N && gj[q] < N;
+          if (valid && gi == gj[q]) A.dg = fmaf(tt, tt, A.dg);   // (D_ii - T_ii)^2 = T_ii^2
+          valid = valid && (I != J || gi < gj[q]);
+          if (valid) {
+            A.L = fmaf(r, r, A.L);
+            if (PEARSON) {
+              A.sd += d;
+              A.sdd = fmaf(d, d, A.sdd);
+              A.sdt = fmaf(d, tt, A.sdt);
+              A.st += tt;
+              A.stt = fmaf(tt, tt, A.stt);
+            }
+          }
+          w = valid ? r * inv : 0.f;
+        } else {
+          A.L = fmaf(r, r, A.L);
+          if (PEARSON) {
+            A.sd += d;
+            A.sdd = fmaf(d, d, A.sdd);
+            A.sdt = fmaf(d, tt, A.sdt);
+            A.st += tt;
+            A.stt = fmaf(tt, tt, A.stt);
+          }
+          w = r * inv;
+        }
+      } else {
+        w = tt * inv;
+        if (MASK) w = (gi < N && gj[q] < N && gi != gj[q]) ? w : 0.f;
+      }
+      px = fmaf(w, dx, px);
+      py = fmaf(w, dy, py);
+      pz = fmaf(w, dz, pz);
+      A.ax[q] = fmaf(-w, dx, A.ax[q]);
+      A.ay[q] = fmaf(-w, dy, A.ay[q]);
+      A.az[q] = fmaf(-w, dz, A.az[q]);
+    }
+    px = sum16(px);
+    py = sum16(py);
+    pz = sum16(pz);
+    if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
+  }
+}
+
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
-template <int MODE, bool VEC>
+// PEARSON: also the d / t moments of the Pearson term (combined loss only).
+template <int MODE, bool VEC, bool PEARSON>
 __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
                                                             int64_t ldt, int nb, int64_t t0,
@@ -98,8 +199,9 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  float cx[8], cy[8], cz[8], ax[8], ay[8], az[8];
+  float cx[8], cy[8], cz[8];
   int gj[8];
+  TileAcc A;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int lc = tx * 4 + (q & 3) + (q >> 2) * 64;
@@ -107,88 +209,35 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     cx[q] = sc[1][lc][0];
     cy[q] = sc[1][lc][1];
     cz[q] = sc[1][lc][2];
-    ax[q] = ay[q] = az[q] = 0.f;
+    A.ax[q] = A.ay[q] = A.az[q] = 0.f;
   }
-  float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f, dg = 0.f;
   float4 *prow = part + (size_t)t * 2 * BT;
+  const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
+  if (interior)
+    tile_rows<MODE, VEC, PEARSON, false>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  else
+    tile_rows<MODE, VEC, PEARSON, true>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
 
-#pragma unroll 1
-  for (int k = 0; k < 8; ++k) {
-    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
-    const int gi = I * BT + lr;
-    const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
-    float tv[8];
-    if (VEC) {  // from the LDS image of the tile (conflict-free ds_read_b128: 16 lanes = one row)
-      const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
-      const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
-      tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
-      tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
-    } else if (gi < N) {
-      const float *trow = T + (size_t)gi * ldt + (size_t)J * BT;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) tv[q] = 0.f;
-    }
-    float px = 0.f, py = 0.f, pz = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float dx = rx - cx[q], dy = ry - cy[q], dz = rz - cz[q];
-      const float d2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-      // one v_rsq for both d and 1/d (1-2 ulp; the reference's own mm-formula cdist is far
-      // coarser); d2 == 0 (coincident points, the diagonal) gives d = w = 0
-      const float inv = d2 > 0.f ? __builtin_amdgcn_rsqf(d2) : 0.f;
-      const float d = d2 * inv;
-      bool valid = gi < N && gj[q] < N;
-      float w;
-      if (MODE == MODE_SYM) {
-        if (valid && gi == gj[q]) dg = fmaf(tv[q], tv[q], dg);   // (D_ii - T_ii)^2 = T_ii^2
-        valid = valid && (I != J || gi < gj[q]);
-        const float tt = tv[q], r = d - tt;
-        if (valid) {
-          L = fmaf(r, r, L);
-          sd += d;
-          sdd = fmaf(d, d, sdd);
-          sdt = fmaf(d, tt, sdt);
-          st += tt;
-          stt = fmaf(tt, tt, stt);
-        }
-        w = valid ? r * inv : 0.f;
-      } else {
-        valid = valid && gi != gj[q];
-        w = valid ? tv[q] * inv : 0.f;
-      }
-      px = fmaf(w, dx, px);
-      py = fmaf(w, dy, py);
-      pz = fmaf(w, dz, pz);
-      ax[q] = fmaf(-w, dx, ax[q]);
-      ay[q] = fmaf(-w, dy, ay[q]);
-      az[q] = fmaf(-w, dz, az[q]);
-    }
-    px = sum16(px);
-    py = sum16(py);
-    pz = sum16(pz);
-    if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
-  }
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    ax[q] += __shfl_xor(ax[q], 16);
-    ax[q] += __shfl_xor(ax[q], 32);
-    ay[q] += __shfl_xor(ay[q], 16);
-    ay[q] += __shfl_xor(ay[q], 32);
-    az[q] += __shfl_xor(az[q], 16);
-    az[q] += __shfl_xor(az[q], 32);
+    A.ax[q] += __shfl_xor(A.ax[q], 16);
+    A.ax[q] += __shfl_xor(A.ax[q], 32);
+    A.ay[q] += __shfl_xor(A.ay[q], 16);
+    A.ay[q] += __shfl_xor(A.ay[q], 32);
+    A.az[q] += __shfl_xor(A.az[q], 16);
+    A.az[q] += __shfl_xor(A.az[q], 32);
   }
   if (lane < 16) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) colred[wv][tx * 4 + (q & 3) + (q >> 2) * 64] = make_float4(ax[q], ay[q], az[q], 0.f);
+    for (int q = 0; q < 8; ++q)
+      colred[wv][tx * 4 + (q & 3) + (q >> 2) * 64] = make_float4(A.ax[q], A.ay[q], A.az[q], 0.f);
   }
   if (MODE == MODE_SYM) {
-    double m[7] = {L, sd, sdd, sdt, st, stt, dg};
+    double m[7] = {A.L, A.sd, A.sdd, A.sdt, A.st, A.stt, A.dg};
 #pragma unroll
     for (int c = 0; c < 7; ++c) {
+      if (!PEARSON && c >= 1 && c <= 5) continue;
       for (int o = 32; o > 0; o >>= 1) m[c] += shfl_xor_d(m[c], o);
     }
     if (lane == 0) {
@@ -216,17 +265,20 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
 // dcoords[i] = scale * (sum of the row partials of tiles (R, *) + column partials of (*, R)).
 // Block = 64 rows x 4 groups; group g adds the tiles J = g, g+4, ... of its row, then the 4 group
 // sums are combined in group order (fixed order: bitwise reproducible).
-__global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__restrict__ part,
-                                                              int N, int nb, int mode, int64_t t0,
-                                                              int64_t t1, float scale,
-                                                              float *__restrict__ dcoords) {
-  __shared__ float4 red[4][64];
+constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-thread blocks)
+
+__global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part,
+                                                               int N, int nb, int mode, int64_t t0,
+                                                               int64_t t1, float scale,
+                                                               float *__restrict__ dcoords) {
+  __shared__ float4 red[kRedGroups][64];
   const int lr64 = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int gi = blockIdx.x * 64 + lr64;
   float sx = 0.f, sy = 0.f, sz = 0.f;
   if (gi < N) {
     const int R = gi / BT, lr = gi % BT;
-    for (int J = grp; J < nb; J += 4) {
+#pragma unroll 2
+    for (int J = grp; J < nb; J += kRedGroups) {
       int64_t trow, tcol;
       if (mode == MODE_SYM) {
         trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
@@ -235,14 +287,11 @@ __global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__re
         trow = (int64_t)R * nb + J;
         tcol = (int64_t)J * nb + R;
       }
-      if (trow >= t0 && trow < t1) {
-        const float4 p = part[(size_t)trow * 2 * BT + lr];
-        sx += p.x; sy += p.y; sz += p.z;
-      }
-      if (tcol >= t0 && tcol < t1) {
-        const float4 p = part[(size_t)tcol * 2 * BT + BT + lr];
-        sx += p.x; sy += p.y; sz += p.z;
-      }
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (trow >= t0 && trow < t1) a = part[(size_t)trow * 2 * BT + lr];
+      if (tcol >= t0 && tcol < t1) b = part[(size_t)tcol * 2 * BT + BT + lr];
+      sx += a.x; sy += a.y; sz += a.z;
+      sx += b.x; sy += b.y; sz += b.z;
     }
   }
   red[grp][lr64] = make_float4(sx, sy, sz, 0.f);
@@ -250,7 +299,7 @@ __global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__re
   if (grp == 0 && gi < N) {
     float4 s0 = red[0][lr64];
 #pragma unroll
-    for (int g = 1; g < 4; ++g) {
+    for (int g = 1; g < kRedGroups; ++g) {
       const float4 o = red[g][lr64];
       s0.x += o.x; s0.y += o.y; s0.z += o.z;
     }
@@ -261,26 +310,27 @@ __global__ __launch_bounds__(256) void pairdist_reduce_kernel(const float4 *__re
 }
 
 // stats[0..6] = sum over tiles [t0,t1) of the tile moments (fixed order, fp64).
-__global__ __launch_bounds__(256) void moments_reduce_kernel(const double *__restrict__ mom,
-                                                             int64_t t0, int64_t t1,
-                                                             double *__restrict__ stats) {
-  __shared__ double red[256][7];
+__global__ __launch_bounds__(1024) void moments_reduce_kernel(const double *__restrict__ mom,
+                                                              int64_t t0, int64_t t1,
+                                                              double *__restrict__ stats) {
+  __shared__ double red[7][1024];
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) {
+#pragma unroll 4
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += 1024) {
 #pragma unroll
     for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
   }
 #pragma unroll
-  for (int c = 0; c < 7; ++c) red[threadIdx.x][c] = s[c];
+  for (int c = 0; c < 7; ++c) red[c][threadIdx.x] = s[c];
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = 512; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
 #pragma unroll
-      for (int c = 0; c < 7; ++c) red[threadIdx.x][c] += red[threadIdx.x + o][c];
+      for (int c = 0; c < 7; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + o];
     }
     __syncthreads();
   }
-  if (threadIdx.x < 7) stats[threadIdx.x] = red[0][threadIdx.x];
+  if (threadIdx.x < 7) stats[threadIdx.x] = red[threadIdx.x][0];
 }
 
 // stats[7..10] and loss from the all-reduced moments stats[0..6]: mse, pearson r, alpha, total.
@@ -370,13 +420,13 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   const bool vec = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) &&
                    ldg >= (int64_t)nb * BT;
   if (vec)
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true>), dim3(tiles), dim3(256), kTileLds,
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true, false>), dim3(tiles), dim3(256), kTileLds,
                        (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
   else
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false>), dim3(tiles), dim3(256), 0,
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false, false>), dim3(tiles), dim3(256), 0,
                        (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
                      dcoords);
   HICGAT_CHECK_LAUNCH();
@@ -401,25 +451,31 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
   double *mom;
   carve(workspace, tiles, &part, &mom);
   const int64_t nt = tile_end - tile_begin;
-  const bool vec = (ldt % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+  // HICGAT_PD_NOLDS=1 (A/B measurement only): read T straight into registers instead of the
+  // LDS-DMA tile image
+  static const bool nolds = getenv("HICGAT_PD_NOLDS") && atoi(getenv("HICGAT_PD_NOLDS")) != 0;
+  const bool vec = !nolds && (ldt % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                    ldt >= (int64_t)nb * BT;
   if (nt > 0) {
-    if (vec)
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, true>), dim3(nt), dim3(256), kTileLds,
-                         (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom);
-    else
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false>), dim3(nt), dim3(256), 0,
-                         (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom);
+    // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only
+#define HICGAT_PD_SYM(V, P)                                                                          \
+  hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, P>), dim3(nt), dim3(256), V ? kTileLds : 0, \
+                     (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom)
+    if (vec && loss_kind == 1) HICGAT_PD_SYM(true, true);
+    else if (vec) HICGAT_PD_SYM(true, false);
+    else if (loss_kind == 1) HICGAT_PD_SYM(false, true);
+    else HICGAT_PD_SYM(false, false);
+#undef HICGAT_PD_SYM
     HICGAT_CHECK_LAUNCH();
   }
   if (dcoords) {
     const float scale = (float)(4.0 / ((double)N * (double)N));
-    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(256), 0,
+    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                        (hipStream_t)stream, part, N, nb, (int)MODE_SYM, tile_begin, tile_end,
                        scale, dcoords);
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, mom,
+  hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mom,
                      tile_begin, tile_end, stats);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,

@@ -31,7 +31,7 @@ SIGNATURES = {
                                        c_f, c_p, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
-    "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+    "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_pairdist_fwd": (c_int, [c_p, c_int, c_p, c_i64, c_p]),
@@ -44,8 +44,8 @@ SIGNATURES = {
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),
     "hicgat_gemm_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
-    "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_sz, c_p]),
-    "hicgat_colsum_workspace_bytes": (c_sz, [c_int]),
+    "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
+    "hicgat_colsum_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_ln_relu_res_fwd": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_p]),
     "hicgat_ln_relu_res_bwd": (c_int, [c_p, c_p, c_i64, c_int, c_int, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_int,
                                        c_p, c_sz, c_p]),

@@ -116,15 +116,12 @@ class ShardedTrainer:
         _all_gather(self.rs_full, self.rs_in, g)
         K.agg_bwd_src(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.rs_full, self.dout,
                       self.att_l.detach(), self.att_r.detach(), self.ns, self.dh, self.da_src)
-        datt_l, datt_r, dbias = K.param_grad(self.h[r0:r1], self.dout[r0:r1], self.da_src[r0:r1],
-                                             self.rs_full[r0:r1], self.H)
+        dbias = self.bias.grad if self.bias is not None else torch.empty(self.h.shape[1], device=self.h.device)
+        K.param_grad(self.h[r0:r1], self.dout[r0:r1], self.da_src[r0:r1], self.rs_full[r0:r1], self.H,
+                     out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)
         with torch.no_grad():
             weight_grad(K, self.dh[r0:r1], self.x_loc, out=self.W.grad, accumulate=True) if self.x_loc.is_cuda \
                 else self.W.grad.addmm_(self.dh[r0:r1].t(), self.x_loc)
-            self.att_l.grad.add_(datt_l.view_as(self.att_l))
-            self.att_r.grad.add_(datt_r.view_as(self.att_r))
-            if self.bias is not None:
-                self.bias.grad.add_(dbias)
         dist.all_reduce(self.opt.grad, group=g)
         self.opt.step()
         return self.loss, self.stats, coords

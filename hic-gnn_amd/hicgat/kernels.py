@@ -88,18 +88,20 @@ class HipKernels:
                                                        float(ns), P(dh), P(da_src), _lib.stream(h.device)),
                        "hicgat_gat_agg_bwd_src")
 
-    def param_grad(self, h, dout, da_src, row_stats, H):
-        """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D])."""
+    def param_grad(self, h, dout, da_src, row_stats, H, out=None, accumulate=False):
+        """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D]); ``out`` =
+        three destination tensors (e.g. the parameters' own .grad views) to write or add into."""
         N, D = h.shape
         C = D // H
         dev = h.device
-        datt_l = torch.empty(D, dtype=torch.float32, device=dev)
-        datt_r = torch.empty_like(datt_l)
-        dbias = torch.empty_like(datt_l)
+        if out is None:
+            out = tuple(torch.empty(D, dtype=torch.float32, device=dev) for _ in range(3))
+        datt_l, datt_r, dbias = out
         ws = _lib.workspace(self.lib.hicgat_gat_param_grad_workspace_bytes(N, D), dev)
-        _lib.check(self.lib.hicgat_gat_param_grad(P(h), P(dout), P(da_src), P(row_stats), N, H, C, P(datt_l),
-                                                  P(datt_r), P(dbias), P(ws), ws.numel(), _lib.stream(dev)),
-                   "hicgat_gat_param_grad")
+        with _timed("param_grad"):
+            _lib.check(self.lib.hicgat_gat_param_grad(P(h), P(dout), P(da_src), P(row_stats), N, H, C, P(datt_l),
+                                                      P(datt_r), P(dbias), int(accumulate), P(ws), ws.numel(),
+                                                      _lib.stream(dev)), "hicgat_gat_param_grad")
         return datt_l, datt_r, dbias
 
     # -- f1: SAGEConv (layers.py:41-79) --------------------------------------------------------------
@@ -163,11 +165,12 @@ class HipKernels:
                        "hicgat_gemm")
         return C
 
-    def colsum(self, A, out):
+    def colsum(self, A, out, accumulate=False):
         K, N = A.shape
-        ws = _lib.workspace(self.lib.hicgat_colsum_workspace_bytes(N), A.device)
-        _lib.check(self.lib.hicgat_colsum(P(A), A.stride(0), K, N, P(out), P(ws), ws.numel(), _lib.stream(A.device)),
-                   "hicgat_colsum")
+        ws = _lib.workspace(self.lib.hicgat_colsum_workspace_bytes(K, N), A.device)
+        with _timed("colsum"):
+            _lib.check(self.lib.hicgat_colsum(P(A), A.stride(0), K, N, P(out), int(accumulate), P(ws), ws.numel(),
+                                              _lib.stream(A.device)), "hicgat_colsum")
         return out
 
     def ln_relu_res_fwd(self, y, gamma, beta, eps, res, z, row_stats):

@@ -10,6 +10,16 @@ import torch
 from . import _lib, kernels
 
 
+def _sink(p):
+    """The parameter's own ``.grad`` when it is a view into ``FlatAdam``'s flat gradient buffer
+    (marked ``_hicgat_grad_sink``): the backward kernels then ADD the gradient into it in place
+    (accumulate epilogue) and return ``None`` to autograd, which saves one add kernel and one
+    temporary per parameter.  Otherwise ``None`` (ordinary autograd accumulation)."""
+    if p is not None and getattr(p, "_hicgat_grad_sink", False) and p.grad is not None:
+        return p.grad
+    return None
+
+
 def _dev_check(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -37,6 +47,7 @@ class _GATConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col)
         ctx.has_bias = bias is not None
         ctx.ns = float(negative_slope)
+        ctx.params = (W, att_l, att_r, bias)
         return out
 
     @staticmethod
@@ -50,13 +61,25 @@ class _GATConvFn(torch.autograd.Function):
         dh = torch.empty_like(h)
         da_src = torch.empty_like(a_src)
         K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
-        datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
-        dW = weight_grad(K, dh, x) if ctx.needs_input_grad[1] else None
+        pW, pl, pr, pb = ctx.params
+        sinks = (_sink(pl), _sink(pr), _sink(pb) if ctx.has_bias else None)
+        if all(t is not None for t in sinks):
+            K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
+                         accumulate=True)
+            datt_l = datt_r = dbias = None
+        else:
+            datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
+            datt_l, datt_r = datt_l.view(al.shape), datt_r.view(ar.shape)
+            dbias = dbias if ctx.has_bias else None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            gW = _sink(pW)
+            dW = weight_grad(K, dh, x, out=gW, accumulate=gW is not None)
+            dW = None if gW is not None else dW
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
-        return (dx, dW, datt_l.view(al.shape), datt_r.view(ar.shape),
-                dbias if ctx.has_bias else None, None, None, None)
+        return (dx, dW, datt_l, datt_r, dbias, None, None, None)
 
 
 def _splits(m, n, k, target=1024):
@@ -76,6 +99,22 @@ def weight_grad(K, dy, x, out=None, accumulate=False):
     return K.gemm(1, 1, m, n, rows, dy, x, out, accumulate=accumulate, splits=_splits(m, n, rows), name="gemm_dw")
 
 
+def _weight_grad_to(K, p, dy, x):
+    """dW = dy^T x into the parameter's sink (returns None) or a new tensor (returned)."""
+    g = _sink(p)
+    dW = weight_grad(K, dy, x, out=g, accumulate=g is not None)
+    return None if g is not None else dW
+
+
+def _bias_grad_to(K, p, dy):
+    """db = column sums of dy into the parameter's sink (returns None) or a new tensor."""
+    g = _sink(p)
+    if g is not None:
+        K.colsum(dy, g, accumulate=True)
+        return None
+    return K.colsum(dy, torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device))
+
+
 class _LinearFn(torch.autograd.Function):
     """torch.nn.Linear (models.py:616-632 layers) forward/backward on the fp32 MFMA GEMM."""
 
@@ -89,6 +128,7 @@ class _LinearFn(torch.autograd.Function):
         K.gemm(0, 0, M, n_out, n_in, x, W.contiguous(), y, bias=b, name="gemm_fwd")
         ctx.save_for_backward(x, W)
         ctx.has_bias = b is not None
+        ctx.params = (W, b)
         return y
 
     @staticmethod
@@ -102,9 +142,9 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, M, n_in, n_out, dy, W.contiguous(), torch.empty_like(x), name="gemm_dx")
         if ctx.needs_input_grad[1]:
-            dW = weight_grad(K, dy, x)
+            dW = _weight_grad_to(K, ctx.params[0], dy, x)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = K.colsum(dy, torch.empty(n_out, dtype=torch.float32, device=dy.device))
+            db = _bias_grad_to(K, ctx.params[1], dy)
         return dx, dW, db
 
 
@@ -130,6 +170,7 @@ class _DualLinearFn(torch.autograd.Function):
         Y = torch.empty((M, n1 + n2), dtype=torch.float32, device=x.device)
         K.gemm(0, 0, M, n1 + n2, x.shape[1], x, Wc, Y, bias=bc, name="gemm_fwd")
         ctx.save_for_backward(x, W1, W2)
+        ctx.params = (W1, b1, W2, b2)
         return Y[:, :n1], Y[:, n1:]
 
     @staticmethod
@@ -143,10 +184,11 @@ class _DualLinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, M, n_in, W1.shape[0], dy1, W1, torch.empty_like(x), name="gemm_dx")
             K.gemm(0, 1, M, n_in, W2.shape[0], dy2, W2, dx, accumulate=True, name="gemm_dx")
-        dW1 = weight_grad(K, dy1, x)
-        dW2 = weight_grad(K, dy2, x)
-        db1 = K.colsum(dy1, torch.empty(W1.shape[0], dtype=torch.float32, device=x.device))
-        db2 = K.colsum(dy2, torch.empty(W2.shape[0], dtype=torch.float32, device=x.device))
+        pW1, pb1, pW2, pb2 = ctx.params
+        dW1 = _weight_grad_to(K, pW1, dy1, x)
+        dW2 = _weight_grad_to(K, pW2, dy2, x)
+        db1 = _bias_grad_to(K, pb1, dy1)
+        db2 = _bias_grad_to(K, pb2, dy2)
         return dx, dW1, db1, dW2, db2
 
 
@@ -167,6 +209,7 @@ class _LnReluResFn(torch.autograd.Function):
         K.ln_relu_res_fwd(y, gamma, beta, eps, res, z, stats)
         ctx.save_for_backward(y, stats, gamma, beta)
         ctx.has_res = res is not None
+        ctx.params = (gamma, beta)
         return z
 
     @staticmethod
@@ -175,9 +218,14 @@ class _LnReluResFn(torch.autograd.Function):
         y, stats, gamma, beta = ctx.saved_tensors
         dz = dz.contiguous()
         dy = torch.empty(y.shape, dtype=torch.float32, device=y.device)
-        dgamma = torch.empty_like(gamma)
-        dbeta = torch.empty_like(beta)
-        K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, dgamma, dbeta)
+        sg, sb = _sink(ctx.params[0]), _sink(ctx.params[1])
+        if sg is not None and sb is not None:
+            K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, sg, sb, accumulate=True)
+            dgamma = dbeta = None
+        else:
+            dgamma = torch.empty_like(gamma)
+            dbeta = torch.empty_like(beta)
+            K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, dgamma, dbeta)
         return dy, dgamma, dbeta, (dz if ctx.has_res else None), None
 
 
@@ -269,6 +317,7 @@ class _SageConvFn(torch.autograd.Function):
         K.gemm(0, 0, N, W_l.shape[0], z.shape[1], z, Wc, out, bias=b_l, name="gemm_fwd")
         ctx.save_for_backward(z, W_l, rowptr, col, w, inv_deg)
         ctx.dims = (N, F, root, b_l is not None)
+        ctx.params = (W_l, b_l, W_r)
         return out
 
     @staticmethod
@@ -278,12 +327,13 @@ class _SageConvFn(torch.autograd.Function):
         N, F, root, has_b = ctx.dims
         dout = dout.contiguous()
         dx = dWl = db = dWr = None
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
-            dWc = weight_grad(K, dout, z)
-            dWl = dWc[:, :F].contiguous()
-            dWr = dWc[:, F:].contiguous() if root else None
+        pWl, pbl, pWr = ctx.params
+        if ctx.needs_input_grad[1]:
+            dWl = _weight_grad_to(K, pWl, dout, z[:, :F])
+        if root and ctx.needs_input_grad[3]:
+            dWr = _weight_grad_to(K, pWr, dout, z[:, F:])
         if has_b and ctx.needs_input_grad[2]:
-            db = K.colsum(dout, torch.empty(dout.shape[1], dtype=torch.float32, device=dout.device))
+            db = _bias_grad_to(K, pbl, dout)
         if ctx.needs_input_grad[0]:
             dagg = K.gemm(0, 1, N, F, dout.shape[1], dout, W_l.contiguous(),
                           torch.empty((N, F), dtype=torch.float32, device=dout.device), name="gemm_dx")

@@ -32,6 +32,8 @@ class FlatAdam:
                 view.copy_(p.data)
                 p.data = view
                 p.grad = self.grad[off:off + p.numel()].view_as(p)
+                p._hicgat_grad_sink = True   # hicgat ops add their gradient straight into p.grad
+        self.offsets = offs
         self.n_params = n
         self.lr, self.betas, self.eps = lr, betas, eps
         self.step_count = 0
@@ -51,10 +53,26 @@ class FlatAdam:
         return self
 
     def zero_grad(self, set_to_none=False):
+        """Zero the flat gradient buffer (``set_to_none`` is ignored: the ``.grad`` views stay)."""
         self.grad.zero_()
+        self._reattach()
+
+    def _reattach(self):
+        """Restore every ``p.grad`` as its flat-buffer view if something replaced it (e.g. a torch
+        ``model.zero_grad()`` setting it to None), folding a foreign gradient tensor back in."""
+        for p, off in zip(self.params, self.offsets):
+            g = p.grad
+            view = self.grad[off:off + p.numel()]
+            if g is None or g.data_ptr() != view.data_ptr():
+                if g is not None:
+                    view.copy_(g.reshape(-1))
+                else:
+                    view.zero_()
+                p.grad = view.view_as(p)
 
     @torch.no_grad()
     def step(self):
+        self._reattach()
         self.step_count += 1
         kern = self.kern if self.kern is not None else kernels.default()
         if getattr(self, "step_ctr", None) is not None:

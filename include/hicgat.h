@@ -109,8 +109,8 @@ int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int
  *   dbias[c] = sum_n dout[n,c].  workspace: hicgat_gat_param_grad_workspace_bytes(N, H*C). */
 int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
                           const float *row_stats, int N, int H, int C, float *datt_src,
-                          float *datt_dst, float *dbias, void *workspace, size_t workspace_bytes,
-                          hicgat_stream_t stream);
+                          float *datt_dst, float *dbias, int accumulate, void *workspace,
+                          size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_gat_param_grad_workspace_bytes(int N, int D);
 
 /* ---- a7: torch.cdist(c, c, p=2) (models.py:661) and its backward -----------------------------
@@ -152,9 +152,9 @@ int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A,
                 int splits, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_gemm_workspace_bytes(int M, int N, int splits);
 /* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
-int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, void *workspace,
+int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                   size_t workspace_bytes, hicgat_stream_t stream);
-size_t hicgat_colsum_workspace_bytes(int N);
+size_t hicgat_colsum_workspace_bytes(int K, int N);
 
 /* ---- a6: LayerNorm + ReLU (+ residual) of the flagship tail (models.py:641-655) --------------
  * z = relu(LayerNorm(y) * gamma + beta) + res (res may be NULL), W in {64, 128, 256}, eps as in

@@ -95,13 +95,21 @@ class CpuKernels:
         dh[r0:r1] = acc.view(n, H * C).float()
         da_src[r0:r1] = dsrc.float()
 
-    def param_grad(self, h, dout, da_src, row_stats, H):
+    def param_grad(self, h, dout, da_src, row_stats, H, out=None, accumulate=False):
         n, D = h.shape
         C = D // H
         hv = h.view(n, H, C).double()
         datt_l = (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
         datt_r = (row_stats[:, 3 * H:4 * H].double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
-        return datt_l, datt_r, dout.double().sum(0).float()
+        res = (datt_l, datt_r, dout.double().sum(0).float())
+        if out is None:
+            return res
+        for o, r in zip(out, res):
+            if accumulate:
+                o.add_(r)
+            else:
+                o.copy_(r)
+        return out
 
     def num_tiles(self, n):
         nb = (n + BT - 1) // BT

@@ -86,7 +86,7 @@ def _cont2dist_ieee(y, f):
 @pytest.mark.parametrize("factor,key", [(0.5, "truth05"), (1, "truth1")])
 def test_cont2dist_bit_exact(case, factor, key):
     """factor 1: bit-exact with the reference fixture.  factor 0.5: bit-exact with IEEE sqrt, and
-    within 1 float64 ulp of the fixture -- the reference's torch CPU sqrt on float64 goes through
+    within 2 float64 ulps of the fixture -- the reference's torch CPU sqrt on float64 goes through
     MKL VML (tensors above ~128 elements), which returns the correctly rounded value minus 1 ulp
     for ~0.7 % of inputs ('Oracle and parity')."""
     import hicgat
@@ -97,8 +97,8 @@ def test_cont2dist_bit_exact(case, factor, key):
     ulps = np.abs(t.view(np.int64) - g[key].view(np.int64))
     if factor == 1:
         assert ulps.max() == 0
-    else:
-        assert ulps.max() <= 1 and (ulps > 0).mean() < 0.02
+    else:   # 1 ulp from the entry's sqrt, 1 more from the max it is divided by
+        assert ulps.max() <= 2 and (ulps > 0).mean() < 0.02
     tr = hicgat.Truth.from_contacts(y, factor)
     d32 = tr.dense().cpu().numpy()
     assert np.array_equal(d32, ieee.astype(np.float32))
@@ -210,7 +210,7 @@ def test_gemm_layouts_match_torch(m, n, k):
     dy = torch.randn(m, n, device=DEV)
     dx = K.gemm(0, 1, m, k, n, dy, w, torch.empty(m, k, device=DEV))
     assert _rel(dx.cpu(), (dy.double() @ w.double()).cpu()) < 5e-6
-    for splits in (1, 3, 64):
+    for splits in (1, 3, 64, 100):
         dw = K.gemm(1, 1, n, k, m, dy, x, torch.empty(n, k, device=DEV), splits=splits)
         # one fp32 fma chain of m/splits terms per element: error grows like sqrt(m/splits)
         tol = 5e-6 * max(1.0, (m / splits / 512) ** 0.5)
@@ -692,3 +692,58 @@ def test_net_train_loop_tracks_oracle():
     rel = np.abs(np.array(hist) - ref_hist) / ref_hist
     assert rel[0] < 1e-5 and rel[1] < 1e-4, rel[:3]
     assert np.all(rel < 0.05), rel
+
+
+@pytest.mark.parametrize("K,N", [(0, 5), (1, 3), (64, 64), (65, 100), (5000, 3), (20000, 512), (1024, 512),
+                                 (40, 300000)])
+def test_colsum_deterministic_column_sums(K, N):
+    """The fixed-order column reduction (bias / LayerNorm / split-K sums): tall multi-pass, wide
+    one-pass, empty, accumulate; bitwise repeatable."""
+    import hicgat
+    K_ = hicgat.kernels.default()
+    torch.manual_seed(K + N)
+    A = torch.randn(K, N, device=DEV)
+    out = K_.colsum(A, torch.full((N,), np.nan, device=DEV))
+    ref = A.double().sum(0)
+    assert _rel(out.cpu(), ref.cpu()) < 1e-5 if K else torch.all(out == 0)
+    again = K_.colsum(A, torch.empty(N, device=DEV))
+    assert torch.equal(out, again)
+    base = torch.randn(N, device=DEV)
+    acc = K_.colsum(A, base.clone(), accumulate=True)
+    assert _rel(acc.cpu(), (ref + base.double()).cpu()) < 1e-5
+    if K > 64:   # strided rows (lda > N)
+        B = torch.randn(K, N + 7, device=DEV)[:, 3:3 + N]
+        assert _rel(K_.colsum(B, torch.empty(N, device=DEV)).cpu(), B.double().sum(0).cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"])
+def test_grad_sink_equals_autograd_accumulation(name):
+    """With FlatAdam attached, the backward kernels add parameter gradients straight into the flat
+    buffer (no autograd add); the result is bitwise the ordinary autograd gradient, and a torch
+    ``model.zero_grad()`` (set_to_none) in between is folded back by FlatAdam."""
+    import hicgat
+    from hicgat import synth
+    n = 700
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=3)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    x = torch.tensor(synth.features(n, seed=3), device=DEV)
+    torch.manual_seed(0)
+    m1 = hicgat.MODELS[name]().to(DEV)
+    torch.manual_seed(0)
+    m2 = hicgat.MODELS[name]().to(DEV)
+    opt = hicgat.FlatAdam(m1.parameters(), lr=1e-3)
+    opt.zero_grad()
+    m1.loss(x, adj, tr)[0].backward()
+    m2.loss(x, adj, tr)[0].backward()
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert p1.grad.data_ptr() >= opt.grad.data_ptr(), k            # still the flat-buffer view
+        assert torch.equal(p1.grad, p2.grad), k
+    m1.zero_grad()                                                      # torch: grads -> None
+    m1.loss(x, adj, tr)[0].backward()
+    opt.step()
+    g = opt.grad.clone()
+    opt.zero_grad()
+    m1.loss(x, adj, tr)[0].backward()
+    assert g.abs().sum() > 0 and torch.all(opt.grad.abs().sum() > 0)

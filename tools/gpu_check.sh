@@ -24,6 +24,7 @@ for s in $STAGES; do
     benchcpu) run bench_cpu 900 python bench.py ;;
     c2d) run debug_c2d 300 python tools/debug_c2d.py ;;
     kbench) run kbench 600 python tools/kbench.py --libs ${KLIBS:-hic-gnn_amd/hicgat/libhicgat.so} ;;
+    kbench_nolds) HICGAT_PD_NOLDS=1 run kbench_nolds 600 python tools/kbench.py ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc)   run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \

@@ -54,6 +54,10 @@ def main():
     ba = model.densea.bias.detach()
     ya = torch.empty(n, 256, device=dev)
     dxa = torch.empty(n, 512, device=dev)
+    cs = torch.empty(512, device=dev)
+    lns = torch.rand(n, 2, device=dev)
+    g256, g256b, g256c = torch.randn(256, device=dev), torch.empty(256, device=dev), torch.empty(256, device=dev)
+    ya2 = torch.empty(n, 256, device=dev)
     libs = [s for s in a.libs.split(",") if s] or [_lib.LIB_PATH]
     kset = []
     for path in libs:
@@ -72,6 +76,9 @@ def main():
                                                    0.2, dh, da),
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
+        "pairdist_combined": lambda K: K.fused_loss(coords, truth.buf, n, 1, 0, -1, stats, loss, dc),
+        "colsum_20000x512": lambda K: K.colsum(out, cs),
+        "ln_bwd_256": lambda K: K.ln_relu_res_bwd(ya, ya, lns, g256, g256, ya2, g256b, g256c),
         "adam": lambda K: K.adam(flat, g, m, v, flat.numel(), 1e-3, 0.9, 0.999, 1e-8, 1),
         "gemm_dw_512x512": lambda K: hicgat.ops.weight_grad(K, dh, x),
         "gemm_fwd_densea": lambda K: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba),
@@ -96,8 +103,9 @@ def main():
                 res.setdefault((lname, jname), []).append(e0.elapsed_time(e1) / a.reps)
     for (lname, jname), ts in res.items():
         alg = ""
-        if jname in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_src", "pairdist_mse_fused"):
-            alg = f"{bench.agg_bytes(jname, n, nnz) / (min(ts) * 1e-3) / 1e9:9.0f} GB/s alg"
+        if jname in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_src", "pairdist_mse_fused", "pairdist_combined"):
+            kb = "pairdist_mse_fused" if jname == "pairdist_combined" else jname
+            alg = f"{bench.agg_bytes(kb, n, nnz) / (min(ts) * 1e-3) / 1e9:9.0f} GB/s alg"
         print(f"{lname:28s} {jname:22s} med {np.median(ts):8.4f} ms  min {min(ts):8.4f} ms  {alg}", flush=True)
 
 
