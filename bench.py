@@ -146,10 +146,13 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as one captured hipGraph (kernel timing then comes from an "
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python each step instead of replaying the step as one "
+                         "captured hipGraph (the default at N=1; the per-kernel timing then comes from an "
                          "eager pass of the same length right after the timed region)")
+    ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
     args = ap.parse_args()
+    args.graph = not args.eager   # refined below: graph capture at N=1 only
 
     import hicgat
     from hicgat import kernels
@@ -163,6 +166,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    args.graph = args.graph and world == 1
     wl = build_workload(args.workload, args.seed, dev)
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
@@ -178,7 +182,7 @@ def main():
             return hicgat.train.train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss, stats)
 
     eager_step = step
-    if args.graph and world == 1:
+    if args.graph:
         step = hicgat.graphs.captured_train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss,
                                                  warmup=max(1, args.warmup))
     else:
@@ -248,7 +252,7 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
-        "graph": bool(args.graph and world == 1),
+        "graph": bool(args.graph),
         "config": {"workload": args.workload, "model": "GATNetSelectiveResidualsUpdated",
                    "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz, "d": D_FEAT, "heads": HEADS,
                    "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single"},

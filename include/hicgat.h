@@ -130,6 +130,8 @@ int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg,
  *     6 sum_i T_ii^2 (moments 0..6 over the tile range; a multi-GPU caller all-reduces them and
  *     calls hicgat_pairdist_finalize), 7 mse = (2*[0] + [6])/N^2, 8 pearson r over i<j,
  *     9 alpha = min(1, 0.1 + 1/(mse + 1e-6)), 10 total = mse + alpha*(1 - r), 11 reserved;
+ *   loss_kind 0 (the MSE of HiC-GNN_main.py) forms moments 0 and 6 only: 1..5 are 0, r (8) is NaN
+ *     and 9..10 are not meaningful; loss_kind 1 (combined loss) forms all of them;
  *   loss[1] (float32): mse (loss_kind 0) or total (loss_kind 1);
  *   dcoords [N,3] = d(mse)/dcoords restricted to the tile range (sum over ranks = full gradient).
  * workspace: hicgat_pairdist_workspace_bytes(N, 1). */

@@ -313,7 +313,9 @@ def test_fused_loss_matches_oracle(n, kind):
     st = stats.cpu().numpy()
     mse_ref = float(torch.nn.functional.mse_loss(out.detach(), truth))
     assert abs(st[7] - mse_ref) <= 1e-5 * mse_ref
-    if n > 2:
+    if kind == "mse":   # the Pearson moments are only formed for the combined loss
+        assert np.isnan(st[8]) and np.all(st[1:6] == 0)
+    elif n > 2:
         r_ref = ol.pearson_r(c.double(), truth)
         assert abs(st[8] - r_ref) < 1e-6
         if kind == "combined":
@@ -573,7 +575,12 @@ def test_full_size_synth20000_properties():
     loss.backward()
     gsum = cc.grad.double().sum(0).abs().max().item()
     assert gsum < 1e-4 * cc.grad.abs().max().item() * np.sqrt(n)
-    assert np.isfinite(stats.cpu().numpy()[:9]).all()
+    assert np.isfinite(stats.cpu().numpy()[:8]).all()
+    _, stats_c = hicgat.ops.fused_dist_loss(cc.detach(), tr, "combined")
+    sc = stats_c.cpu().numpy()
+    assert np.isfinite(sc[:11]).all() and -1 <= sc[8] <= 1
+    s0 = stats.cpu().numpy()[0]
+    assert abs(sc[0] - s0) <= 1e-12 * s0            # same sum (d - t)^2, Pearson on or off
 
 
 # ---------------------------------------------------------------- f1: SAGEConv / Net baseline

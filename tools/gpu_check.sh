@@ -20,16 +20,16 @@ for s in $STAGES; do
     tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
-    benchg) run bench_graph 600 python bench.py --steps ${STEPS:-20} --warmup 3 --graph --no-cpu-baseline ;;
+    benche) run bench_eager 600 python bench.py --steps ${STEPS:-20} --warmup 3 --eager --no-cpu-baseline ;;
     benchcpu) run bench_cpu 900 python bench.py ;;
     c2d) run debug_c2d 300 python tools/debug_c2d.py ;;
     kbench) run kbench 600 python tools/kbench.py --libs ${KLIBS:-hic-gnn_amd/hicgat/libhicgat.so} ;;
     kbench_nolds) HICGAT_PD_NOLDS=1 run kbench_nolds 600 python tools/kbench.py ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-               python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+               python bench.py --steps 10 --warmup 2 --no-cpu-baseline --eager ;;
     pmc)   run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
-               python bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+               python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager &&
            run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
-               python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+               python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager ;;
   esac
 done
