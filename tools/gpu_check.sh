@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
-    tests) run pytest_gpu 600 python -m pytest tests -m gpu -q -rf ;;
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
     benche) run bench_eager 600 python bench.py --steps ${STEPS:-20} --warmup 3 --eager --no-cpu-baseline ;;
@@ -30,6 +30,8 @@ for s in $STAGES; do
     pmc)   run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
                python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager &&
            run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
+               python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager ;;
+    pmcl2) run pmc_l2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- \
                python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager ;;
   esac
 done
