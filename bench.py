@@ -37,8 +37,10 @@ def log(*a):
 
 def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
     """Algorithmic HBM bytes per launch (DESIGN.md 'Roofline')."""
-    if kind == "gat_agg_fwd":      # gather h_j + col per edge, write out, rowptr, logits/stats
-        return nnz * (4 * d + 4) + n * 4 * d + (n + 1) * 4 + 2 * n * h * 4 + nnz * 4 * h
+    if kind == "gat_agg_fwd":      # gather h_j + col per edge, write out + out2 (training form), rowptr, stats
+        return nnz * (4 * d + 4) + 2 * n * 4 * d + (n + 1) * 4 + 2 * n * h * 4 + nnz * 4 * h + n * 16
+    if kind == "gat_agg_bwd_rows":  # stream g, y, out2 in and dout out; S3 in, (delta, da_dst) out
+        return 4 * n * 4 * d + 2 * n * 16
     if kind == "gat_agg_bwd_dst":  # gather h_j + col + a_src_j per edge, read dout_i
         return nnz * (4 * d + 4 + 4 * h) + n * 4 * d + (n + 1) * 4 + 5 * n * h * 4
     if kind == "gat_agg_bwd_src":  # gather dout_i + col + (a_dst, max, sum, delta)_i, read h_r, write dh_r
@@ -54,6 +56,7 @@ def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
 PMC_KERNELS = {
     "gat_agg_fwd": ["agg_fwd_h2c256_kernel"],
     "gat_agg_bwd_dst": ["agg_bwd_dst_h2c256_kernel"],
+    "gat_agg_bwd_rows": ["agg_bwd_rows_kernel"],
     "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel"],
     "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_reduce_kernel", "moments_reduce_kernel"],
 }
@@ -228,7 +231,8 @@ def main():
         n_loc = runner.local_rows
     else:
         n_loc = n
-    cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_src", "pairdist_mse_fused") if k in kern]
+    cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "pairdist_mse_fused")
+             if k in kern]
     dom = max(cands, key=lambda k: kern[k]["total_ms"])
     if dom == "pairdist_mse_fused":
         alg = agg_bytes(dom, n, nnz) / (world if world > 1 else 1)

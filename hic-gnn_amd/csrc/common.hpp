@@ -77,6 +77,11 @@ __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 acc) {
   acc.w = fmaf(a, x.w, acc.w);
   return acc;
 }
+// torch.relu: x <= 0 ? 0 : x (NaN passes through).
+__device__ __forceinline__ float relu_t(float x) { return x <= 0.f ? 0.f : x; }
+__device__ __forceinline__ float4 f4_relu(float4 a) {
+  return make_float4(relu_t(a.x), relu_t(a.y), relu_t(a.z), relu_t(a.w));
+}
 __device__ __forceinline__ float f4_dot(float4 a, float4 b) {
   return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
 }

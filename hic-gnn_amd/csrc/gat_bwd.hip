@@ -10,18 +10,24 @@
 // (the +1e-16 of the softmax denominator and the detached-max gradient change these by
 // O(1e-16) relative; both are dropped.)
 //
-// Pass 1 (dst side, row i) gathers h_j; pass 2 (src side, row r) gathers dout_i of the rows that
-// have r as a neighbour.  The graph is structurally symmetric (to_symmetric, utils.py:71), so
-// row r's own CSR list *is* that set: the transpose needs no permutation array and no atomics.
-// The per-edge dot products are reduced 8 neighbours x 2 heads at a time with one 17-shuffle
-// transpose reduce instead of 16 independent 6-step wave sums.
+// Destination side, two forms with the same outputs (delta_i, da_dst_i into row_stats[i, 4:8]):
+//  * agg_bwd_rows (the training path): no gather -- delta_i = <dout_i, out_i - bias> and
+//    da_dst_i = <dout_i, out2_i> - delta_i S3_i from the forward's TRAIN outputs (gat_fwd.hip);
+//  * agg_bwd_dst (stand-alone form, needs only h): gathers h_j and forms every g_ij; the per-edge
+//    dot products are reduced 2U neighbour-heads at a time with one transpose reduce.
+// Source side (row r) gathers dout_i of the rows that have r as a neighbour.  The graph is
+// structurally symmetric (to_symmetric, utils.py:71), so row r's own CSR list *is* that set: the
+// transpose needs no permutation array and no atomics.
 #include "common.hpp"
 
 #ifndef HICGAT_BWD_U
-// neighbours gathered per inner step (2 float4 loads per lane each).  Measured on MI355X at
-// N = 20000 (tools/kbench.py): U = 8 -> 0.95 / 1.11 ms (dst / src pass, 118 / 142 VGPRs, 4 / 3
-// waves per SIMD); U = 4 -> 0.52 / 0.56; U = 2 -> 0.47 / 0.49.  The gather wants waves, not ILP.
+// neighbours gathered per inner step of agg_bwd_dst (2 float4 loads per lane each).  Measured on
+// MI355X at N = 20000 (tools/kbench.py): U = 8 -> 0.95 ms (118 VGPRs, 4 waves per SIMD); U = 4 ->
+// 0.52; U = 2 -> 0.47.  With per-edge reductions in the loop the gather wants waves, not ILP.
 #define HICGAT_BWD_U 2
+#endif
+#ifndef HICGAT_SRC_U
+#define HICGAT_SRC_U 4   // neighbours per inner step of the (reduction-free) source pass
 #endif
 
 namespace hicgat {
@@ -102,31 +108,34 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
   if (lane == 0) reinterpret_cast<float4 *>(row_stats)[2 * (size_t)i + 1] = make_float4(dl0, dl1, dd0, dd1);
 }
 
+// Source side, algebraically regrouped so that no per-edge dot product (and no cross-lane
+// reduction) sits inside the gather loop:
+//   da_src[r] = sum_i alpha_ir s_ir (<dout_i, h_r> - delta_i)
+//             = <sum_i alpha_ir s_ir dout_i, h_r> - sum_i alpha_ir s_ir delta_i      (s = lrelu')
+// so the loop only accumulates two vectors (sum alpha dout_i, sum alpha s dout_i) and a scalar.
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ row_stats, const float *__restrict__ dout,
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
     float *__restrict__ dh, float *__restrict__ da_src) {
-  constexpr int U = HICGAT_BWD_U;
+  constexpr int U = HICGAT_SRC_U;
   const int lane = lane_id();
   const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (r >= row_end) return;
   const int beg = rowptr[r], end = rowptr[r + 1];
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
-  const float4 hr0 = h4[(size_t)r * 128 + lane], hr1 = h4[(size_t)r * 128 + 64 + lane];
   const float2 asr = *reinterpret_cast<const float2 *>(a_src + 2 * (size_t)r);
   const float2 *ad2 = reinterpret_cast<const float2 *>(a_dst);
   const float4 *rs4 = reinterpret_cast<const float4 *>(row_stats);
-  const int hh = lane >> 5, kk = Owner<U>::slot(lane);
-  const bool owner = Owner<U>::owner(lane);
-  float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
-  float Sda = 0.f;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc0 = z4, acc1 = z4, c0 = z4, c1 = z4;
+  float sb0 = 0.f, sb1 = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
     int inb = r;
-    float al0 = 0.f, al1 = 0.f, A0 = 0.f, A1 = 0.f, B0 = 0.f, B1 = 0.f;
+    float al0 = 0.f, al1 = 0.f, A0 = 0.f, A1 = 0.f;
     if (e < end) {
       inb = col[e];
       const float2 ad = ad2[inb];
@@ -137,8 +146,8 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
       al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
       A0 = al0 * (e0 > 0.f ? 1.f : ns);
       A1 = al1 * (e1 > 0.f ? 1.f : ns);
-      B0 = A0 * dl.x;
-      B1 = A1 * dl.y;
+      sb0 = fmaf(A0, dl.x, sb0);
+      sb1 = fmaf(A1, dl.y, sb1);
     }
     const int cnt = min(64, end - base);
     for (int k = 0; k < cnt; k += U) {
@@ -149,23 +158,20 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
         g0[u] = g4[ii * 128 + lane];
         g1[u] = g4[ii * 128 + 64 + lane];
       }
-      float v[2 * U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         acc0 = f4_fma(readlane_f(al0, k + u), g0[u], acc0);
         acc1 = f4_fma(readlane_f(al1, k + u), g1[u], acc1);
-        v[u] = f4_dot(g0[u], hr0);
-        v[U + u] = f4_dot(g1[u], hr1);
+        c0 = f4_fma(readlane_f(A0, k + u), g0[u], c0);
+        c1 = f4_fma(readlane_f(A1, k + u), g1[u], c1);
       }
-      transpose_reduce<2 * U>(v, lane);
-      const int src = k + kk;
-      const float a0 = __shfl(A0, src), a1 = __shfl(A1, src);
-      const float b0 = __shfl(B0, src), b1 = __shfl(B1, src);
-      if (owner && src < cnt) Sda += hh ? fmaf(a1, v[0], -b1) : fmaf(a0, v[0], -b0);
     }
   }
-  Sda = half_wave_sum(Sda);
-  const float ds0 = readlane_f(Sda, 0), ds1 = readlane_f(Sda, 32);
+  const float4 hr0 = h4[(size_t)r * 128 + lane], hr1 = h4[(size_t)r * 128 + 64 + lane];
+  float v[4] = {f4_dot(c0, hr0), f4_dot(c1, hr1), sb0, sb1};
+  transpose_reduce<4>(v, lane);   // lane 0: v0, 16: v1, 32: v2, 48: v3 (summed over the wave)
+  const float ds0 = readlane_f(v[0], 0) - readlane_f(v[0], 32);
+  const float ds1 = readlane_f(v[0], 16) - readlane_f(v[0], 48);
   const float2 dd = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)r + 6);
   const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
   const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
@@ -180,6 +186,51 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   if (lane == 0) {
     da_src[2 * (size_t)r] = ds0;
     da_src[2 * (size_t)r + 1] = ds1;
+  }
+}
+
+// Destination side without a gather (the forward's TRAIN outputs, gat_fwd.hip):
+//   dout_i = g_i * [y_i > 0] (ACT = 1: the relu after the GATConv, torch's threshold_backward on
+//   its output) or g_i (ACT = 0);  delta_i = <dout_i, y_i - bias> (y = out where the mask is on);
+//   da_dst_i = <dout_i, out2_i> - delta_i * S3_i.   One wave per row, 8 KB streamed per row.
+template <int ACT>
+__global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int row_end,
+                                                           const float *__restrict__ g,
+                                                           const float *__restrict__ y,
+                                                           const float *__restrict__ bias,
+                                                           const float *__restrict__ out2,
+                                                           float *__restrict__ dout,
+                                                           float *__restrict__ row_stats) {
+  const int lane = lane_id();
+  const int i = row_begin + blockIdx.x * 4 + wave_in_block();
+  if (i >= row_end) return;
+  const size_t o0 = (size_t)i * 128 + lane, o1 = o0 + 64;
+  const float4 *g4 = reinterpret_cast<const float4 *>(g);
+  const float4 *y4 = reinterpret_cast<const float4 *>(y);
+  const float4 *q4 = reinterpret_cast<const float4 *>(out2);
+  const float4 *b4 = reinterpret_cast<const float4 *>(bias);
+  float4 d0 = g4[o0], d1 = g4[o1];
+  const float4 y0 = y4[o0], y1 = y4[o1], q0 = q4[o0], q1 = q4[o1];
+  const float4 b0 = b4[lane], b1 = b4[64 + lane];
+  if (ACT == 1) {
+    d0 = make_float4(y0.x <= 0.f ? 0.f : d0.x, y0.y <= 0.f ? 0.f : d0.y, y0.z <= 0.f ? 0.f : d0.z,
+                     y0.w <= 0.f ? 0.f : d0.w);
+    d1 = make_float4(y1.x <= 0.f ? 0.f : d1.x, y1.y <= 0.f ? 0.f : d1.y, y1.z <= 0.f ? 0.f : d1.z,
+                     y1.w <= 0.f ? 0.f : d1.w);
+    float4 *d4 = reinterpret_cast<float4 *>(dout);
+    d4[o0] = d0;
+    d4[o1] = d1;
+  }
+  const float4 e0 = make_float4(y0.x - b0.x, y0.y - b0.y, y0.z - b0.z, y0.w - b0.w);
+  const float4 e1 = make_float4(y1.x - b1.x, y1.y - b1.y, y1.z - b1.z, y1.w - b1.w);
+  float v[4] = {f4_dot(d0, e0), f4_dot(d1, e1), f4_dot(d0, q0), f4_dot(d1, q1)};
+  transpose_reduce<4>(v, lane);
+  const float dl0 = readlane_f(v[0], 0), dl1 = readlane_f(v[0], 16);
+  const float p0 = readlane_f(v[0], 32), p1 = readlane_f(v[0], 48);
+  if (lane == 0) {
+    float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+    const float4 t = rs4[2 * (size_t)i + 1];   // (S3_0, S3_1, -, -) from the forward
+    rs4[2 * (size_t)i + 1] = make_float4(dl0, dl1, fmaf(-dl0, t.x, p0), fmaf(-dl1, t.y, p1));
   }
 }
 
@@ -274,6 +325,26 @@ extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col,
   hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
                      row_stats, dout, att_src, att_dst, neg_slope, dh, da_src);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_gat_agg_bwd_rows(int N, int H, int C, int row_begin, int row_end, int act,
+                                       const float *g, const float *y, const float *bias,
+                                       const float *out2, float *dout, float *row_stats,
+                                       hicgat_stream_t stream) {
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (act != 0 && act != 1) return HICGAT_EINVAL;
+  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!g || !y || !bias || !out2 || !row_stats || (act && !dout)) return HICGAT_EINVAL;
+  const int rows = row_end - row_begin;
+  if (act)
+    hipLaunchKernelGGL(agg_bwd_rows_kernel<1>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                       row_begin, row_end, g, y, bias, out2, dout, row_stats);
+  else
+    hipLaunchKernelGGL(agg_bwd_rows_kernel<0>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                       row_begin, row_end, g, y, bias, out2, dout, row_stats);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

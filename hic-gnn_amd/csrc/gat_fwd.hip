@@ -53,10 +53,19 @@ __global__ __launch_bounds__(256) void att_logits_kernel(const float *__restrict
 // Pass 1/2 stream only col[] and a_src[] (row max, row sum); pass 3 gathers h[j] rows with the
 // neighbour index and both alphas broadcast from lane k through SGPRs (v_readlane), so each
 // gather is one scalar base + per-lane offset global_load_dwordx4, 8 neighbours in flight.
+//
+// TRAIN also accumulates, from the same gathered rows (FMAs only, no extra loads),
+//   out2[i] = sum_j alpha_ij lrelu'(e_ij) h_j    and    S3[i] = sum_j alpha_ij lrelu'(e_ij)
+// (S3 into row_stats[i, 4:6]).  With those the destination half of the backward needs no gather:
+//   delta_i = sum_j alpha_ij <dout_i, h_j> = <dout_i, out_i - bias>,
+//   da_dst_i = sum_j alpha_ij lrelu'(e_ij) (<dout_i, h_j> - delta_i) = <dout_i, out2_i> - delta_i S3_i
+// (agg_bwd_rows_kernel, gat_bwd.hip).  ACT = 1 applies the relu that follows the GATConv in
+// GATNetSelectiveResidualsUpdated (models.py:637) in the epilogue: out = relu(acc + bias).
+template <bool TRAIN, int ACT>
 __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
-    const float *__restrict__ bias, float ns, float *__restrict__ out,
+    const float *__restrict__ bias, float ns, float *__restrict__ out, float *__restrict__ out2,
     float *__restrict__ row_stats) {
   constexpr int U = HICGAT_FWD_U;  // neighbours in flight per lane
   const int lane = lane_id();
@@ -85,16 +94,25 @@ __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
   const float den0 = s0 + 1e-16f, den1 = s1 + 1e-16f;
 
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
-  float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc0 = z4, acc1 = z4, acs0 = z4, acs1 = z4;
+  float t0 = 0.f, t1 = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
     int j = i;  // padded slots gather the (valid) own row with weight 0
-    float p0 = 0.f, p1 = 0.f;
+    float p0 = 0.f, p1 = 0.f, q0 = 0.f, q1 = 0.f;
     if (e < end) {
       j = col[e];
       const float2 s = as2[j];
-      p0 = expf(lrelu(s.x + ad.x, ns) - m0) / den0;
-      p1 = expf(lrelu(s.y + ad.y, ns) - m1) / den1;
+      const float e0 = s.x + ad.x, e1 = s.y + ad.y;
+      p0 = expf(lrelu(e0, ns) - m0) / den0;
+      p1 = expf(lrelu(e1, ns) - m1) / den1;
+      if (TRAIN) {
+        q0 = p0 * (e0 > 0.f ? 1.f : ns);
+        q1 = p1 * (e1 > 0.f ? 1.f : ns);
+        t0 += q0;
+        t1 += q1;
+      }
     }
     const int cnt = min(64, end - base);
     for (int k = 0; k < cnt; k += U) {
@@ -109,6 +127,10 @@ __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
       for (int u = 0; u < U; ++u) {
         acc0 = f4_fma(readlane_f(p0, k + u), v0[u], acc0);
         acc1 = f4_fma(readlane_f(p1, k + u), v1[u], acc1);
+        if (TRAIN) {
+          acs0 = f4_fma(readlane_f(q0, k + u), v0[u], acs0);
+          acs1 = f4_fma(readlane_f(q1, k + u), v1[u], acs1);
+        }
       }
     }
   }
@@ -117,9 +139,22 @@ __global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
   float4 b0 = b4[lane], b1 = b4[64 + lane];
   acc0.x += b0.x; acc0.y += b0.y; acc0.z += b0.z; acc0.w += b0.w;
   acc1.x += b1.x; acc1.y += b1.y; acc1.z += b1.z; acc1.w += b1.w;
+  if (ACT == 1) {
+    acc0 = f4_relu(acc0);
+    acc1 = f4_relu(acc1);
+  }
   o4[(size_t)i * 128 + lane] = acc0;
   o4[(size_t)i * 128 + 64 + lane] = acc1;
-  if (lane == 0) reinterpret_cast<float4 *>(row_stats)[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
+  float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+  if (TRAIN) {
+    float4 *q4 = reinterpret_cast<float4 *>(out2);
+    q4[(size_t)i * 128 + lane] = acs0;
+    q4[(size_t)i * 128 + 64 + lane] = acs1;
+    t0 = wave_sum(t0);
+    t1 = wave_sum(t1);
+    if (lane == 0) rs4[2 * (size_t)i + 1] = make_float4(t0, t1, 0.f, 0.f);
+  }
+  if (lane == 0) rs4[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
 }
 
 }  // namespace hicgat
@@ -138,18 +173,39 @@ extern "C" int hicgat_gat_att_logits(const float *h, const float *att_src, const
   return HICGAT_OK;
 }
 
+extern "C" int hicgat_gat_agg_fwd_act(const int32_t *rowptr, const int32_t *col, int N, int nnz,
+                                      int H, int C, int row_begin, int row_end, const float *h,
+                                      const float *a_src, const float *a_dst, const float *bias,
+                                      float neg_slope, int act, float *out, float *out2,
+                                      float *row_stats, hicgat_stream_t stream) {
+  if (N < 0 || nnz < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (act != 0 && act != 1) return HICGAT_EINVAL;
+  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !bias || !out || !row_stats) return HICGAT_EINVAL;
+  const int rows = row_end - row_begin;
+  const dim3 grid((rows + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define HICGAT_FWD_LAUNCH(TR, AC)                                                                  \
+  hipLaunchKernelGGL((agg_fwd_h2c256_kernel<TR, AC>), grid, block, 0, s, rowptr, col, row_begin,   \
+                     row_end, h, a_src, a_dst, bias, neg_slope, out, out2, row_stats)
+  if (out2) {
+    if (act) HICGAT_FWD_LAUNCH(true, 1);
+    else HICGAT_FWD_LAUNCH(true, 0);
+  } else {
+    if (act) HICGAT_FWD_LAUNCH(false, 1);
+    else HICGAT_FWD_LAUNCH(false, 0);
+  }
+#undef HICGAT_FWD_LAUNCH
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 extern "C" int hicgat_gat_agg_fwd(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H,
                                   int C, int row_begin, int row_end, const float *h,
                                   const float *a_src, const float *a_dst, const float *bias,
                                   float neg_slope, float *out, float *row_stats,
                                   hicgat_stream_t stream) {
-  if (N < 0 || nnz < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
-  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (row_end == row_begin) return HICGAT_OK;
-  if (!rowptr || !col || !h || !a_src || !a_dst || !bias || !out || !row_stats) return HICGAT_EINVAL;
-  const int rows = row_end - row_begin;
-  hipLaunchKernelGGL(agg_fwd_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     rowptr, col, row_begin, row_end, h, a_src, a_dst, bias, neg_slope, out, row_stats);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  return hicgat_gat_agg_fwd_act(rowptr, col, N, nnz, H, C, row_begin, row_end, h, a_src, a_dst, bias,
+                                neg_slope, 0, out, nullptr, row_stats, stream);
 }

@@ -27,8 +27,12 @@ SIGNATURES = {
     "hicgat_gat_att_logits": (c_int, [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p]),
     "hicgat_gat_agg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p,
                                    c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_agg_fwd_act": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p,
+                                       c_p, c_f, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_gat_agg_bwd_dst": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_f, c_p, c_p]),
+    "hicgat_gat_agg_bwd_rows": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p,
+                                        c_p, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,

@@ -8,11 +8,13 @@ section 2: no collectives anywhere), so every exchange below is new:
   in global row order: buffer row == global node id; the CSR, x and the truth are replicated).
   forward:  h_p = x_p W^T (MFMA)  -> all_gather(h)              [N, 512] fp32, 41 MB at N=20000
             a_src, a_dst for all rows from the gathered h (one cheap pass, no collective)
-            GAT aggregation for own rows -> MLP tail on own rows -> all_gather(coords) [N, 3]
+            GAT aggregation for own rows (+ the model's fused activation and the out2 / S3
+            training outputs) -> MLP tail on own rows -> all_gather(coords) [N, 3]
             fused distance/MSE over this rank's share of the upper-triangle tiles
             all_reduce(loss moments fp64) + all_reduce(dcoords) ; finalize loss
-  backward: tail backward on own rows -> dout_p -> all_gather(dout)  [N, 512]
-            GAT bwd pass 1 on own rows -> all_gather(row stats: max, sum, delta, da_dst)
+  backward: tail backward on own rows -> GAT bwd rows pass (activation backward, delta, da_dst;
+            no gather) -> all_gather(dout) [N, 512] and all_gather(row stats: max, sum, delta,
+            da_dst)
             GAT bwd pass 2 on own rows -> dh_p (complete: own rows gather dout of all neighbours)
             dW_p = dh_p^T x_p, datt/dbias partial -> all_reduce(one flat fp32 grad buffer)
             identical Adam step on every rank (weights stay replicated).
@@ -25,7 +27,7 @@ partitioning and collectives are testable on CPU with gloo and a torch stand-in.
 import torch
 import torch.distributed as dist
 
-from .ops import weight_grad
+from .ops import _ACTS, weight_grad
 from .optim import FlatAdam
 
 
@@ -69,6 +71,9 @@ class ShardedTrainer:
         self.h_in = torch.zeros((R, D), **f32)
         self.h = torch.zeros((P * R, D), **f32)
         self.out = torch.zeros((P * R, D), **f32)
+        self.out2 = torch.zeros((P * R, D), **f32)
+        self.gbuf = torch.zeros((P * R, D), **f32)
+        self.act = _ACTS[getattr(model, "conv_act", None)]
         self.dout_in = torch.zeros((R, D), **f32)
         self.dout = torch.zeros((P * R, D), **f32)
         self.dh = torch.zeros((P * R, D), **f32)
@@ -96,10 +101,10 @@ class ShardedTrainer:
         self.h_in[:n_loc].copy_(h_loc)
         _all_gather(self.h, self.h_in, g)
         a_src, a_dst = K.att_logits(self.h, self.att_l.detach(), self.att_r.detach())
-        K.agg_fwd(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.out,
-                  self.rs)
+        K.agg_fwd_act(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.act,
+                      self.out, self.out2, self.rs)
         o = self.out[r0:r1].detach().requires_grad_(True)
-        coords_loc = self.model.tail(o)
+        coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
         self.c_in[:n_loc].copy_(coords_loc.detach())
         _all_gather(self.coords, self.c_in, g)
         coords = self.coords[:N]
@@ -109,9 +114,11 @@ class ShardedTrainer:
         K.loss_finalize(N, self.kind, self.stats, self.loss)
         # ---- backward -----------------------------------------------------------------------
         coords_loc.backward(self.dcoords[r0:r1])
-        self.dout_in[:n_loc].copy_(o.grad)
+        self.gbuf[r0:r1].copy_(o.grad)
+        # act: writes dout = g * relu'(out) into self.dout's own rows; otherwise dout is g itself
+        K.agg_bwd_rows(r0, r1, self.act, self.gbuf, self.out, self.bias.detach(), self.out2, self.dout, self.rs)
+        self.dout_in[:n_loc].copy_((self.dout if self.act else self.gbuf)[r0:r1])
         _all_gather(self.dout, self.dout_in, g)
-        K.agg_bwd_dst(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.dout, self.ns, self.rs)
         self.rs_in[:n_loc].copy_(self.rs[r0:r1])
         _all_gather(self.rs_full, self.rs_in, g)
         K.agg_bwd_src(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, self.rs_full, self.dout,

@@ -47,11 +47,12 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
         self.norm2 = LayerNorm(64)
         self.dense3 = Linear(64, 3)
 
-    def tail(self, x):
-        """models.py:637-659 after the GATConv: relu; [densea | align_densea] as one GEMM,
+    conv_act = "relu"   # the relu of models.py:637 runs in the GAT aggregation's epilogue
+
+    def post_act(self, x):
+        """models.py:638-659 (after the relu): [densea | align_densea] as one GEMM,
         relu(norm_a(.)) + residual in one pass; the same for dense1 / align_dense1 / norm1;
         relu(norm2(dense2(.))); dense3."""
-        x = F.relu(x)
         y, res = ops.dual_linear(x, self.densea, self.align_densea)
         x = ops.ln_relu_res(y, self.norm_a, res)
         y, res = ops.dual_linear(x, self.dense1, self.align_dense1)
@@ -59,8 +60,12 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
         x = ops.ln_relu_res(_lin(self.dense2, x), self.norm2)
         return _lin(self.dense3, x)
 
+    def tail(self, x):
+        """models.py:637-659 after the GATConv output."""
+        return self.post_act(F.relu(x))
+
     def get_model(self, x, edge_index):
-        return self.tail(self.conv(x, edge_index))
+        return self.post_act(self.conv(x, edge_index, act=self.conv_act))
 
 
 class GATNetHeadsChanged3LayersLeakyReLUv2(_CoordsModel):
@@ -71,11 +76,15 @@ class GATNetHeadsChanged3LayersLeakyReLUv2(_CoordsModel):
         self.dense1 = Linear(256, 64)
         self.dense2 = Linear(64, 3)
 
+    conv_act = None     # leaky_relu(0.01) stays a torch op on the GATConv output
+
     def tail(self, x):
         x = F.leaky_relu(x)
         x = F.leaky_relu(_lin(self.densea, x))
         x = F.leaky_relu(_lin(self.dense1, x))
         return _lin(self.dense2, x)
+
+    post_act = tail
 
     def get_model(self, x, edge_index):
         return self.tail(self.conv(x, edge_index))

@@ -69,6 +69,26 @@ class HipKernels:
                                                    P(a_dst), P(bias), float(ns), P(out), P(row_stats),
                                                    _lib.stream(h.device)), "hicgat_gat_agg_fwd")
 
+    def agg_fwd_act(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, act, out, out2, row_stats):
+        """Training form: ``act`` 1 = relu epilogue; ``out2`` (or None) = sum alpha lrelu' h."""
+        N = h.shape[0]
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        with _timed("gat_agg_fwd"):
+            _lib.check(self.lib.hicgat_gat_agg_fwd_act(P(rowptr), P(col), N, col.numel(), H, C, r0, r1, P(h),
+                                                       P(a_src), P(a_dst), P(bias), float(ns), int(act), P(out),
+                                                       P(out2), P(row_stats), _lib.stream(h.device)),
+                       "hicgat_gat_agg_fwd_act")
+
+    def agg_bwd_rows(self, r0, r1, act, g, y, bias, out2, dout, row_stats):
+        """Destination half of the backward without a gather (after ``agg_fwd_act`` with out2)."""
+        N, D = y.shape
+        H = row_stats.shape[1] // 4
+        with _timed("gat_agg_bwd_rows"):
+            _lib.check(self.lib.hicgat_gat_agg_bwd_rows(N, H, D // H, r0, r1, int(act), P(g), P(y), P(bias), P(out2),
+                                                        P(dout), P(row_stats), _lib.stream(y.device)),
+                       "hicgat_gat_agg_bwd_rows")
+
     def agg_bwd_dst(self, rowptr, col, r0, r1, h, a_src, a_dst, dout, ns, row_stats):
         N = h.shape[0]
         H = a_src.shape[1]

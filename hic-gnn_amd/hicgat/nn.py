@@ -56,10 +56,11 @@ class GATConv(torch.nn.Module):
             with torch.no_grad():
                 self.bias.zero_()
 
-    def forward(self, x, edge_index):
-        """``edge_index`` is a ``hicgat.graph.Adj`` (the reference passes a SparseTensor)."""
+    def forward(self, x, edge_index, act=None):
+        """``edge_index`` is a ``hicgat.graph.Adj`` (the reference passes a SparseTensor).
+        ``act="relu"`` (not in PyG) returns relu(forward(x)) with the relu fused into the kernel."""
         return ops.gat_conv(x, self.lin_l.weight, self.att_l, self.att_r, self.bias, edge_index,
-                            self.negative_slope)
+                            self.negative_slope, act)
 
     def __repr__(self):
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"

@@ -26,9 +26,16 @@ def _dev_check(*ts):
             raise _lib.HicgatUnavailable("hicgat ops need CUDA (HIP) tensors; got a CPU tensor")
 
 
+_ACTS = {None: 0, "relu": 1}
+
+
 class _GATConvFn(torch.autograd.Function):
+    """PyG 1.7.2 GATConv (+ an optional fused relu epilogue, act=1).  With gradients enabled the
+    aggregation also emits out2 / S3 (include/hicgat.h), so the destination half of the backward
+    is a streaming pass (``agg_bwd_rows``) and only the source half gathers."""
+
     @staticmethod
-    def forward(ctx, x, W, att_l, att_r, bias, rowptr, col, negative_slope):
+    def forward(ctx, x, W, att_l, att_r, bias, rowptr, col, negative_slope, act):
         _lib.lib()
         _dev_check(x, W, att_l, att_r, bias, rowptr, col)
         K = kernels.default()
@@ -43,21 +50,29 @@ class _GATConvFn(torch.autograd.Function):
         b = bias if bias is not None else torch.zeros(D, dtype=torch.float32, device=x.device)
         out = torch.empty((N, D), dtype=torch.float32, device=x.device)
         row_stats = torch.empty((N, 4 * H), dtype=torch.float32, device=x.device)
-        K.agg_fwd(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, out, row_stats)
-        ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col)
+        train = any(ctx.needs_input_grad[:5])
+        out2 = torch.empty((N, D), dtype=torch.float32, device=x.device) if train else None
+        K.agg_fwd_act(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, act, out, out2, row_stats)
+        if train:
+            ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col, out, out2, b)
         ctx.has_bias = bias is not None
         ctx.ns = float(negative_slope)
+        ctx.act = act
         ctx.params = (W, att_l, att_r, bias)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         K = kernels.default()
-        x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col = ctx.saved_tensors
+        x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col, out, out2, b = ctx.saved_tensors
         dout = dout.contiguous()
         N = x.shape[0]
         H = al.shape[-2]
-        K.agg_bwd_dst(rowptr, col, 0, N, h, a_src, a_dst, dout, ctx.ns, row_stats)
+        if ctx.act:
+            g, dout = dout, torch.empty_like(dout)
+            K.agg_bwd_rows(0, N, ctx.act, g, out, b, out2, dout, row_stats)
+        else:
+            K.agg_bwd_rows(0, N, 0, dout, out, b, out2, None, row_stats)
         dh = torch.empty_like(h)
         da_src = torch.empty_like(a_src)
         K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
@@ -79,7 +94,7 @@ class _GATConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
-        return (dx, dW, datt_l, datt_r, dbias, None, None, None)
+        return (dx, dW, datt_l, datt_r, dbias, None, None, None, None)
 
 
 def _splits(m, n, k, target=1024):
@@ -239,10 +254,11 @@ def ln_relu_res(y, norm, res=None):
     return _LnReluResFn.apply(y, norm.weight, norm.bias, res, norm.eps)
 
 
-def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2):
+def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):
+    """GATConv forward; ``act="relu"`` returns relu(GATConv(x)) with the relu fused."""
     if adj.rowptr32 is None or adj.rowptr32.device != x.device:
         adj.to(x.device)
-    return _GATConvFn.apply(x, W, att_l, att_r, bias, adj.rowptr32, adj.col32, negative_slope)
+    return _GATConvFn.apply(x, W, att_l, att_r, bias, adj.rowptr32, adj.col32, negative_slope, _ACTS[act])
 
 
 class _PairDistFn(torch.autograd.Function):

@@ -84,6 +84,15 @@ int hicgat_gat_agg_fwd(const int32_t *rowptr, const int32_t *col, int N, int nnz
                        int row_begin, int row_end, const float *h, const float *a_src,
                        const float *a_dst, const float *bias, float neg_slope, float *out,
                        float *row_stats, hicgat_stream_t stream);
+/* Training form of the same aggregation.  act = 1 writes out = relu(sum + bias) (the relu that
+ * follows the GATConv at models.py:637), act = 0 the plain sum + bias.  out2 != NULL (training)
+ * also writes, from the same gathered rows, out2 [N, H*C] = sum_j alpha_ij lrelu'(e_ij) h_j and
+ * S3[i,h] = sum_j alpha_ij lrelu'(e_ij) into row_stats[i, 2H..3H) -- the inputs that let
+ * hicgat_gat_agg_bwd_rows form the destination half of the backward without a gather. */
+int hicgat_gat_agg_fwd_act(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
+                           int row_begin, int row_end, const float *h, const float *a_src,
+                           const float *a_dst, const float *bias, float neg_slope, int act,
+                           float *out, float *out2, float *row_stats, hicgat_stream_t stream);
 
 /* ---- a10 (part): backward of a4+a5 ----------------------------------------------------------
  * Pass 1 (destination side, rows of the range):  g_ij = <dout[i,h,:], h[j,h,:]>,
@@ -98,6 +107,13 @@ int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int
                            int row_begin, int row_end, const float *h, const float *a_src,
                            const float *a_dst, const float *dout, float neg_slope,
                            float *row_stats, hicgat_stream_t stream);
+/* Pass 1 without a gather, after hicgat_gat_agg_fwd_act(..., out2, ...) (same row_stats):
+ *   dout = g * [y > 0] (act = 1, written to dout; torch's relu backward on the output y) or g
+ *   (act = 0, dout unused); delta = <dout, y - bias>; da_dst = <dout, out2> - delta * S3,
+ * per row of the range and head -> row_stats[i, 2H..4H) exactly as hicgat_gat_agg_bwd_dst. */
+int hicgat_gat_agg_bwd_rows(int N, int H, int C, int row_begin, int row_end, int act, const float *g,
+                            const float *y, const float *bias, const float *out2, float *dout,
+                            float *row_stats, hicgat_stream_t stream);
 int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
                            int row_begin, int row_end, const float *h, const float *a_src,
                            const float *a_dst, const float *row_stats, const float *dout,

@@ -56,6 +56,37 @@ class CpuKernels:
         row_stats[r0:r1, 0:H] = m
         row_stats[r0:r1, H:2 * H] = s
 
+    def agg_fwd_act(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, act, out, out2, row_stats):
+        self.agg_fwd(rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats)
+        if act:
+            out[r0:r1] = torch.relu(out[r0:r1])
+        if out2 is None:
+            return
+        H = a_src.shape[1]
+        C = h.shape[1] // H
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        al, lp = self._alpha(a_src, a_dst, row_stats, row, j, ns, H)
+        n = r1 - r0
+        msg = h[j].view(-1, H, C).double() * (al * lp).unsqueeze(-1)
+        out2[r0:r1] = torch.zeros((n, H, C), dtype=torch.float64).index_add(0, row - r0, msg).view(n, H * C).float()
+        row_stats[r0:r1, 2 * H:3 * H] = torch.zeros((n, H), dtype=torch.float64).index_add(
+            0, row - r0, al * lp).float()
+
+    def agg_bwd_rows(self, r0, r1, act, g, y, bias, out2, dout, row_stats):
+        H = row_stats.shape[1] // 4
+        n, D = r1 - r0, y.shape[1]
+        d = g[r0:r1].double()
+        yy = y[r0:r1].double()
+        if act:
+            d = torch.where(yy > 0, d, torch.zeros_like(d))
+            dout[r0:r1] = d.float()
+        delta = (d * (yy - bias.double())).view(n, H, D // H).sum(-1)
+        p = (d * out2[r0:r1].double()).view(n, H, D // H).sum(-1)
+        s3 = row_stats[r0:r1, 2 * H:3 * H].double()
+        row_stats[r0:r1, 2 * H:3 * H] = delta.float()
+        row_stats[r0:r1, 3 * H:4 * H] = (p - delta * s3).float()
+
     def _alpha(self, a_src, a_dst, row_stats, i, j, ns, H):
         e = a_src[j] + a_dst[i]
         m = row_stats[i, 0:H]

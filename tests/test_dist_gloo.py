@@ -56,15 +56,15 @@ def _torch_tail(hicgat):
     on the HIP GEMM / LayerNorm kernels)."""
     import torch.nn.functional as F
 
-    def tail(self, x):
-        x = F.relu(x)
+    def post_act(self, x):   # after the relu, which the trainer fuses into the aggregation
         res = self.align_densea(x)
         x = F.relu(self.norm_a(self.densea(x))) + res
         res = self.align_dense1(x)
         x = F.relu(self.norm1(self.dense1(x))) + res
         x = F.relu(self.norm2(self.dense2(x)))
         return self.dense3(x)
-    hicgat.GATNetSelectiveResidualsUpdated.tail = tail
+    hicgat.GATNetSelectiveResidualsUpdated.post_act = post_act
+    hicgat.GATNetSelectiveResidualsUpdated.tail = lambda self, x: post_act(self, F.relu(x))
 
 
 def _worker(rank, world, port, n, kind, out):

@@ -155,6 +155,67 @@ def test_gatconv_forward_backward_matches_oracle(n, p):
         assert _rel(pm.grad.cpu(), pr.grad) < 1e-4, name
 
 
+@pytest.mark.parametrize("n,p", [(58, 1.0), (257, 0.02), (600, 0.5)])
+def test_gatconv_fused_relu_matches_oracle(n, p):
+    """GATConv(x, act="relu") == relu(GATConv(x)) of the oracle, forward and backward (the relu
+    of models.py:637 in the aggregation epilogue, its backward in the gather-free row pass)."""
+    import hicgat
+    a = _random_graph(n, p, n + 1)
+    ref, mine = _gat_pair(seed=n + 1)
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    rng = np.random.default_rng(n)
+    x = torch.tensor((0.1 * rng.standard_normal((n, 512))).astype(np.float32))
+    g = torch.tensor(rng.standard_normal((n, 512)).astype(np.float32))
+    xr = x.clone().requires_grad_(True)
+    out_r = torch.relu(ref(xr, (adj.storage.rowptr(), adj.storage.col())))
+    (out_r * g).sum().backward()
+    xm = x.to(DEV).requires_grad_(True)
+    out_m = mine(xm, adj, act="relu")
+    (out_m * g.to(DEV)).sum().backward()
+    np.testing.assert_allclose(out_m.detach().cpu().numpy(), out_r.detach().numpy(), rtol=1e-5, atol=1e-6)
+    assert _rel(xm.grad.cpu(), xr.grad) < 1e-4
+    for (name, pr), (_, pm) in zip(ref.named_parameters(), mine.named_parameters()):
+        assert _rel(pm.grad.cpu(), pr.grad) < 1e-4, name
+    with torch.no_grad():                     # inference form (no out2) gives the same output
+        assert torch.equal(mine(x.to(DEV), adj, act="relu"), out_m.detach())
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_bwd_rows_equals_gather_dst(act):
+    """The gather-free destination pass (delta = <dout, out - bias>, da_dst = <dout, out2> -
+    delta S3) equals the gathering pass (per-edge <dout_i, h_j>) on the same inputs."""
+    import hicgat
+    from hicgat import synth
+    K = hicgat.kernels.default()
+    n = 3000
+    i, j, c = synth.contact_pairs(n, density=0.03, seed=7)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    torch.manual_seed(3)
+    h = torch.randn(n, 512, device=DEV) * 0.1
+    a_s = torch.randn(n, 2, device=DEV)
+    a_d = torch.randn(n, 2, device=DEV)
+    b = torch.randn(512, device=DEV) * 0.1
+    out = torch.empty(n, 512, device=DEV)
+    out2 = torch.empty(n, 512, device=DEV)
+    rs = torch.empty(n, 8, device=DEV)
+    K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, act, out, out2, rs)
+    out_plain = torch.empty_like(out)
+    rs_plain = torch.empty_like(rs)
+    K.agg_fwd(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, out_plain, rs_plain)
+    assert torch.equal(out, torch.relu(out_plain) if act else out_plain)
+    assert torch.equal(rs[:, :4], rs_plain[:, :4])
+    g = torch.randn(n, 512, device=DEV)
+    dout = torch.empty_like(g)
+    K.agg_bwd_rows(0, n, act, g, out, b, out2, dout, rs)
+    dref = torch.where(out_plain > 0, g, torch.zeros_like(g)) if act else g
+    if act:
+        assert torch.equal(dout, dref)
+    K.agg_bwd_dst(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, dref, 0.2, rs_plain)
+    for k in (4, 5, 6, 7):
+        assert _rel(rs[:, k].cpu(), rs_plain[:, k].cpu()) < 2e-5, k
+
+
 def test_gat_linear_att_matches_torch():
     import hicgat
     from hicgat import _lib

@@ -38,7 +38,8 @@ def main():
     h, a_s, a_d = K0.linear_att(x, W, al, ar)
     out = torch.empty_like(h)
     rs = torch.zeros(n, 8, device=dev)
-    K0.agg_fwd(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, out, rs)
+    out2 = torch.empty_like(h)
+    K0.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out, out2, rs)
     dout = torch.randn_like(h) * 1e-3
     dh = torch.empty_like(h)
     da = torch.empty_like(a_s)
@@ -71,7 +72,10 @@ def main():
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
         "gat_agg_fwd": lambda K: K.agg_fwd(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, out, rs),
+        "gat_agg_fwd_train": lambda K: K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out,
+                                                     out2, rs),
         "gat_agg_bwd_dst": lambda K: K.agg_bwd_dst(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, dout, 0.2, rs),
+        "gat_agg_bwd_rows": lambda K: K.agg_bwd_rows(0, n, 1, dout, out, b, out2, dh, rs),
         "gat_agg_bwd_src": lambda K: K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, al, ar,
                                                    0.2, dh, da),
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
@@ -103,8 +107,9 @@ def main():
                 res.setdefault((lname, jname), []).append(e0.elapsed_time(e1) / a.reps)
     for (lname, jname), ts in res.items():
         alg = ""
-        if jname in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_src", "pairdist_mse_fused", "pairdist_combined"):
-            kb = "pairdist_mse_fused" if jname == "pairdist_combined" else jname
+        if jname in ("gat_agg_fwd", "gat_agg_fwd_train", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src",
+                     "pairdist_mse_fused", "pairdist_combined"):
+            kb = {"pairdist_combined": "pairdist_mse_fused", "gat_agg_fwd_train": "gat_agg_fwd"}.get(jname, jname)
             alg = f"{bench.agg_bytes(kb, n, nnz) / (min(ts) * 1e-3) / 1e9:9.0f} GB/s alg"
         print(f"{lname:28s} {jname:22s} med {np.median(ts):8.4f} ms  min {min(ts):8.4f} ms  {alg}", flush=True)
 
