@@ -151,11 +151,12 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the step as one "
-                         "captured hipGraph (the default at N=1; the per-kernel timing then comes from an "
-                         "eager pass of the same length right after the timed region)")
+                         "captured hipGraph (the default; at N > 1 the graph holds the RCCL collectives too; the "
+                         "per-kernel timing then comes from an eager pass of the same length right after the "
+                         "timed region)")
     ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
     args = ap.parse_args()
-    args.graph = not args.eager   # refined below: graph capture at N=1 only
+    args.graph = not args.eager
 
     import hicgat
     from hicgat import kernels
@@ -169,7 +170,6 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    args.graph = args.graph and world == 1
     wl = build_workload(args.workload, args.seed, dev)
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
@@ -185,7 +185,9 @@ def main():
             return hicgat.train.train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss, stats)
 
     eager_step = step
-    if args.graph:
+    if args.graph and world > 1:
+        step = runner.captured(warmup=max(1, args.warmup))   # kernels + RCCL collectives in one graph
+    elif args.graph:
         step = hicgat.graphs.captured_train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss,
                                                  warmup=max(1, args.warmup))
     else:

@@ -91,6 +91,17 @@ class ShardedTrainer:
         self.t1 = T * (self.rank + 1) // P
         self.opt = FlatAdam(model.parameters(), lr=lr, kern=kern)
 
+    def captured(self, warmup=2):
+        """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
+        per step removes the ~70 host launches that would otherwise bound a small per-rank shard.
+        The ``warmup`` eager steps are real training steps."""
+        from .graphs import CapturedStep
+        if dist.get_backend(self.group) != "nccl":
+            raise RuntimeError("graph capture of the sharded step needs the nccl (RCCL) backend")
+        if getattr(self.opt, "step_ctr", None) is None:
+            self.opt.enable_device_step()
+        return CapturedStep(self.step, warmup=warmup)
+
     def step(self):
         K, g, r0, r1, N = self.K, self.group, self.r0, self.r1, self.N
         n_loc = r1 - r0

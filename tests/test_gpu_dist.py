@@ -40,6 +40,47 @@ def _inputs(n, dev):
     return hicgat, adj, truth, x
 
 
+def _graph_worker(rank, world, port, n, out):
+    """RCCL, captured sharded step (kernels + collectives in one hipGraph) vs eager steps."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        hicgat, adj, truth, x = _inputs(n, dev)
+        res = []
+        for graphed in (False, True):
+            torch.manual_seed(0)
+            model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
+            tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3)
+            losses = []
+            if graphed:
+                step = tr.captured(warmup=2)
+                losses += [None, None]
+                for _ in range(3):
+                    losses.append(float(step()[0]))
+            else:
+                tr.opt.enable_device_step()
+                for _ in range(5):
+                    losses.append(float(tr.step()[0]))
+            torch.cuda.synchronize()
+            res.append((losses, tr.opt.flat.clone().cpu()))
+        if rank == 0:
+            torch.save({"eager": res[0][0], "graph": res[1][0], "pe": res[0][1], "pg": res[1][1]}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rccl_graph_replay_equals_eager(tmp_path):
+    out = str(tmp_path / "graph.pt")
+    mp.spawn(_graph_worker, args=(1, _port(), 700, out), nprocs=1, join=True)
+    r = torch.load(out, weights_only=True)
+    assert r["eager"][2:] == r["graph"][2:]
+    assert torch.equal(r["pe"], r["pg"])
+
+
 def _worker(rank, world, port, backend, n, out):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
