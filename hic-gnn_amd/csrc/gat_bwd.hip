@@ -116,9 +116,11 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
-    const float *__restrict__ row_stats, const float *__restrict__ dout,
+    const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout, int64_t ldq,
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
     float *__restrict__ dh, float *__restrict__ da_src) {
+  // ldq: dout row stride in float4, ldr: row_stats row stride in floats (both multiples of 4, so
+  // a multi-GPU caller can all-gather [dout | row stats] rows as one packed buffer)
   constexpr int U = HICGAT_SRC_U;
   const int lane = lane_id();
   const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
@@ -139,8 +141,8 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     if (e < end) {
       inb = col[e];
       const float2 ad = ad2[inb];
-      const float4 ms = rs4[2 * (size_t)inb];                                 // max0 max1 sum0 sum1
-      const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)inb + 4);  // delta
+      const float4 ms = rs4[(size_t)inb * (ldr / 4)];                         // max0 max1 sum0 sum1
+      const float2 dl = *reinterpret_cast<const float2 *>(row_stats + ldr * inb + 4);       // delta
       const float e0 = asr.x + ad.x, e1 = asr.y + ad.y;
       al0 = expf(lrelu(e0, ns) - ms.x) / (ms.z + 1e-16f);
       al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
@@ -155,8 +157,8 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const size_t ii = (size_t)readlane_i(inb, k + u);
-        g0[u] = g4[ii * 128 + lane];
-        g1[u] = g4[ii * 128 + 64 + lane];
+        g0[u] = g4[ii * ldq + lane];
+        g1[u] = g4[ii * ldq + 64 + lane];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   transpose_reduce<4>(v, lane);   // lane 0: v0, 16: v1, 32: v2, 48: v3 (summed over the wave)
   const float ds0 = readlane_f(v[0], 0) - readlane_f(v[0], 32);
   const float ds1 = readlane_f(v[0], 16) - readlane_f(v[0], 48);
-  const float2 dd = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)r + 6);
+  const float2 dd = *reinterpret_cast<const float2 *>(row_stats + ldr * r + 6);
   const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
   const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
   const float4 as0 = s4[lane], as1 = s4[64 + lane], at0 = t4[lane], at1 = t4[64 + lane];
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
                                                            const float *__restrict__ y,
                                                            const float *__restrict__ bias,
                                                            const float *__restrict__ out2,
-                                                           float *__restrict__ dout,
+                                                           float *__restrict__ dout, int64_t ldq,
                                                            float *__restrict__ row_stats) {
   const int lane = lane_id();
   const int i = row_begin + blockIdx.x * 4 + wave_in_block();
@@ -217,9 +219,9 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
                      y0.w <= 0.f ? 0.f : d0.w);
     d1 = make_float4(y1.x <= 0.f ? 0.f : d1.x, y1.y <= 0.f ? 0.f : d1.y, y1.z <= 0.f ? 0.f : d1.z,
                      y1.w <= 0.f ? 0.f : d1.w);
-    float4 *d4 = reinterpret_cast<float4 *>(dout);
-    d4[o0] = d0;
-    d4[o1] = d1;
+    float4 *d4 = reinterpret_cast<float4 *>(dout) + (size_t)i * ldq + lane;   // ldq: row stride, float4
+    d4[0] = d0;
+    d4[64] = d1;
   }
   const float4 e0 = make_float4(y0.x - b0.x, y0.y - b0.y, y0.z - b0.z, y0.w - b0.w);
   const float4 e1 = make_float4(y1.x - b1.x, y1.y - b1.y, y1.z - b1.z, y1.w - b1.w);
@@ -308,15 +310,16 @@ extern "C" int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col,
   return HICGAT_OK;
 }
 
-extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H,
-                                      int C, int row_begin, int row_end, const float *h,
-                                      const float *a_src, const float *a_dst,
-                                      const float *row_stats, const float *dout,
-                                      const float *att_src, const float *att_dst,
-                                      float neg_slope, float *dh, float *da_src,
-                                      hicgat_stream_t stream) {
+extern "C" int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, int H,
+                                         int C, int row_begin, int row_end, const float *h,
+                                         const float *a_src, const float *a_dst,
+                                         const float *row_stats, int64_t ld_stats, const float *dout,
+                                         int64_t ld_dout, const float *att_src, const float *att_dst,
+                                         float neg_slope, float *dh, float *da_src,
+                                         hicgat_stream_t stream) {
   if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (ld_stats < 4 * H || ld_stats % 4 || ld_dout < H * C || ld_dout % 4) return HICGAT_EINVAL;
   if (row_end == row_begin) return HICGAT_OK;
   if (!rowptr || !col || !h || !a_src || !a_dst || !row_stats || !dout || !att_src || !att_dst ||
       !dh || !da_src)
@@ -324,16 +327,29 @@ extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col,
   const int rows = row_end - row_begin;
   hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
-                     row_stats, dout, att_src, att_dst, neg_slope, dh, da_src);
+                     row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
+extern "C" int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H,
+                                      int C, int row_begin, int row_end, const float *h,
+                                      const float *a_src, const float *a_dst,
+                                      const float *row_stats, const float *dout,
+                                      const float *att_src, const float *att_dst,
+                                      float neg_slope, float *dh, float *da_src,
+                                      hicgat_stream_t stream) {
+  return hicgat_gat_agg_bwd_src_ld(rowptr, col, N, H, C, row_begin, row_end, h, a_src, a_dst,
+                                   row_stats, 4 * (int64_t)H, dout, (int64_t)H * C, att_src, att_dst,
+                                   neg_slope, dh, da_src, stream);
+}
+
 extern "C" int hicgat_gat_agg_bwd_rows(int N, int H, int C, int row_begin, int row_end, int act,
                                        const float *g, const float *y, const float *bias,
-                                       const float *out2, float *dout, float *row_stats,
-                                       hicgat_stream_t stream) {
+                                       const float *out2, float *dout, int64_t ld_dout,
+                                       float *row_stats, hicgat_stream_t stream) {
   if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (act && (ld_dout < (int64_t)H * C || ld_dout % 4)) return HICGAT_EINVAL;
   if (act != 0 && act != 1) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (row_end == row_begin) return HICGAT_OK;
@@ -341,10 +357,10 @@ extern "C" int hicgat_gat_agg_bwd_rows(int N, int H, int C, int row_begin, int r
   const int rows = row_end - row_begin;
   if (act)
     hipLaunchKernelGGL(agg_bwd_rows_kernel<1>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                       row_begin, row_end, g, y, bias, out2, dout, row_stats);
+                       row_begin, row_end, g, y, bias, out2, dout, ld_dout / 4, row_stats);
   else
     hipLaunchKernelGGL(agg_bwd_rows_kernel<0>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                       row_begin, row_end, g, y, bias, out2, dout, row_stats);
+                       row_begin, row_end, g, y, bias, out2, dout, (int64_t)0, row_stats);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

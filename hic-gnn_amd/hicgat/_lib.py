@@ -32,7 +32,9 @@ SIGNATURES = {
     "hicgat_gat_agg_bwd_dst": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_f, c_p, c_p]),
     "hicgat_gat_agg_bwd_rows": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p,
-                                        c_p, c_p]),
+                                        c_i64, c_p, c_p]),
+    "hicgat_gat_agg_bwd_src_ld": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                          c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,

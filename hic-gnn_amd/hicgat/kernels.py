@@ -39,10 +39,13 @@ class HipKernels:
         self.lib = _lib.lib()
 
     # -- a2 ---------------------------------------------------------------------------------------
-    def linear_att(self, x, W, att_l, att_r):
+    def linear_att(self, x, W, att_l, att_r, h=None):
+        """h = x W^T (into ``h``, e.g. a rank's rows of the all-gather buffer, if given) + logits."""
         N, F = x.shape
         H, C = att_l.shape[-2], att_l.shape[-1]
-        h = torch.empty((N, H * C), dtype=torch.float32, device=x.device)
+        if h is None:
+            h = torch.empty((N, H * C), dtype=torch.float32, device=x.device)
+        assert h.shape == (N, H * C) and h.is_contiguous()
         a_src = torch.empty((N, H), dtype=torch.float32, device=x.device)
         a_dst = torch.empty_like(a_src)
         with _timed("gat_linear_att"):
@@ -81,12 +84,15 @@ class HipKernels:
                        "hicgat_gat_agg_fwd_act")
 
     def agg_bwd_rows(self, r0, r1, act, g, y, bias, out2, dout, row_stats):
-        """Destination half of the backward without a gather (after ``agg_fwd_act`` with out2)."""
+        """Destination half of the backward without a gather (after ``agg_fwd_act`` with out2);
+        ``dout`` (act = 1) may be a row-strided view, e.g. the dout columns of a packed buffer."""
         N, D = y.shape
         H = row_stats.shape[1] // 4
+        assert row_stats.stride(0) == 4 * H and y.stride(0) == D
         with _timed("gat_agg_bwd_rows"):
             _lib.check(self.lib.hicgat_gat_agg_bwd_rows(N, H, D // H, r0, r1, int(act), P(g), P(y), P(bias), P(out2),
-                                                        P(dout), P(row_stats), _lib.stream(y.device)),
+                                                        P(dout), 0 if dout is None else dout.stride(0),
+                                                        P(row_stats), _lib.stream(y.device)),
                        "hicgat_gat_agg_bwd_rows")
 
     def agg_bwd_dst(self, rowptr, col, r0, r1, h, a_src, a_dst, dout, ns, row_stats):
@@ -102,11 +108,14 @@ class HipKernels:
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
+        # row_stats / dout may be row-strided views (the packed all-gather buffer of hicgat.dist)
+        assert row_stats.stride(1) == 1 and dout.stride(1) == 1
         with _timed("gat_agg_bwd_src"):
-            _lib.check(self.lib.hicgat_gat_agg_bwd_src(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
-                                                       P(a_dst), P(row_stats), P(dout), P(att_l), P(att_r),
-                                                       float(ns), P(dh), P(da_src), _lib.stream(h.device)),
-                       "hicgat_gat_agg_bwd_src")
+            _lib.check(self.lib.hicgat_gat_agg_bwd_src_ld(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
+                                                          P(a_dst), P(row_stats), row_stats.stride(0), P(dout),
+                                                          dout.stride(0), P(att_l), P(att_r), float(ns), P(dh),
+                                                          P(da_src), _lib.stream(h.device)),
+                       "hicgat_gat_agg_bwd_src_ld")
 
     def param_grad(self, h, dout, da_src, row_stats, H, out=None, accumulate=False):
         """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D]); ``out`` =

@@ -108,17 +108,27 @@ int hicgat_gat_agg_bwd_dst(const int32_t *rowptr, const int32_t *col, int N, int
                            const float *a_dst, const float *dout, float neg_slope,
                            float *row_stats, hicgat_stream_t stream);
 /* Pass 1 without a gather, after hicgat_gat_agg_fwd_act(..., out2, ...) (same row_stats):
- *   dout = g * [y > 0] (act = 1, written to dout; torch's relu backward on the output y) or g
+ *   dout = g * [y > 0] (act = 1, written to dout with row stride ld_dout floats; torch's relu
+ *   backward on the output y) or g
  *   (act = 0, dout unused); delta = <dout, y - bias>; da_dst = <dout, out2> - delta * S3,
  * per row of the range and head -> row_stats[i, 2H..4H) exactly as hicgat_gat_agg_bwd_dst. */
 int hicgat_gat_agg_bwd_rows(int N, int H, int C, int row_begin, int row_end, int act, const float *g,
                             const float *y, const float *bias, const float *out2, float *dout,
-                            float *row_stats, hicgat_stream_t stream);
+                            int64_t ld_dout, float *row_stats, hicgat_stream_t stream);
 int hicgat_gat_agg_bwd_src(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
                            int row_begin, int row_end, const float *h, const float *a_src,
                            const float *a_dst, const float *row_stats, const float *dout,
                            const float *att_src, const float *att_dst, float neg_slope, float *dh,
                            float *da_src, hicgat_stream_t stream);
+/* The same with strided rows: dout row i at dout + i*ld_dout, row_stats row i at
+ * row_stats + i*ld_stats (floats, multiples of 4) -- e.g. one all-gathered [dout | row stats]
+ * buffer per row (hicgat.dist). */
+int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, int H, int C,
+                              int row_begin, int row_end, const float *h, const float *a_src,
+                              const float *a_dst, const float *row_stats, int64_t ld_stats,
+                              const float *dout, int64_t ld_dout, const float *att_src,
+                              const float *att_dst, float neg_slope, float *dh, float *da_src,
+                              hicgat_stream_t stream);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;

@@ -27,9 +27,13 @@ def _tri(I, J, nb):
 
 
 class CpuKernels:
-    def linear_att(self, x, W, att_l, att_r):
+    def linear_att(self, x, W, att_l, att_r, h=None):
         H, C = att_l.shape[-2], att_l.shape[-1]
-        h = (x.double() @ W.double().t()).float()
+        hv_ = (x.double() @ W.double().t()).float()
+        if h is None:
+            h = hv_
+        else:
+            h.copy_(hv_)
         hv = h.view(-1, H, C).double()
         return h, (hv * att_l.double()).sum(-1).float(), (hv * att_r.double()).sum(-1).float()
 
