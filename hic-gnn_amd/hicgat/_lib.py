@@ -59,6 +59,8 @@ SIGNATURES = {
     "hicgat_sage_weights": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_agg": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_int, c_int, c_p, c_i64,
                                 c_p]),
+    "hicgat_kr_matvec": (c_int, [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p]),
+    "hicgat_kr_scale": (c_int, [c_p, c_i64, c_int, c_p, c_p, c_i64, c_p]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
 }

@@ -192,7 +192,7 @@ def load_input(input, features, device="cuda"):
     np.fill_diagonal(adj_mat, 0)
     y = torch.tensor(adj_mat, dtype=torch.double, device=device)
     edge_index = Adj.from_dense_device(y)
-    x = torch.tensor(features).to(device)
+    x = features.to(device) if isinstance(features, torch.Tensor) else torch.tensor(features).to(device)
     return Data(x=x, edge_index=edge_index, y=y)
 
 

@@ -212,6 +212,16 @@ int hicgat_sage_agg(const int32_t *rowptr, const int32_t *col, const float *weig
                     int N, int F, int row_begin, int row_end, const float *x, int transpose, int write_trunc,
                     float *z, int64_t ldz, hicgat_stream_t stream);
 
+/* ---- f2: Knight-Ruiz normalisation (r_utils.R:1-93 KRnorm, run by normalize.R from
+ * HiC-GNN_main.py:85) -- the O(N^2) parts; the O(N) CG bookkeeping is the caller's (hicgat/kr.py).
+ * A: float64 row-major n x n (leading dim lda), NaN entries count as 0.
+ *   hicgat_kr_matvec: out_i = x_i * sum_j A_ij x_j p_j (+ v_i p_i if v != NULL)   (r_utils.R:24,42,64)
+ *   hicgat_kr_scale:  out_ij = rint(((x_i A_ij) x_j) * 1e6) / 1e6, NaN kept        (r_utils.R:74-89) */
+int hicgat_kr_matvec(const double *A, int64_t lda, int n, const double *x, const double *p, const double *v,
+                     double *out, hicgat_stream_t stream);
+int hicgat_kr_scale(const double *A, int64_t lda, int n, const double *x, double *out, int64_t ldo,
+                    hicgat_stream_t stream);
+
 /* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
  * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
  *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);

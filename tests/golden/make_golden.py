@@ -2,7 +2,7 @@
 
 Run in the build container only (the reference tree does not exist on the GPU box):
 
-    python tests/golden/make_golden.py /root/reference
+    python tests/golden/make_golden.py /root/reference [align]   # "align": only the align_* fixtures
 
 It imports the reference ``utils.py`` / ``models.py`` (``/root/reference``) with the stand-ins in
 ``tests/golden/_stubs`` for the absent ``torch_geometric`` / ``torch_sparse`` packages and records:
@@ -18,6 +18,9 @@ It imports the reference ``utils.py`` / ``models.py`` (``/root/reference``) with
 * ``model_Net.npz``    -- the baseline SAGE model (models.py:14-55 over layers.py:12-79) on chr19
   1mb: init state, SAGE aggregate, distances, coordinates, MSE, gradients; plus the key/shape
   layout of the shipped ``Outputs/GM12878_1mb_chr19_list_weights.pt`` (safe loader).
+* ``align_chr19_f<F>.npz`` -- ``utils.domain_alignment`` (utils.py:83-109) on the chr19 1 mb /
+  500 kb lists with seeded float32 embeddings of width F (512: rank-deficient Procrustes, 32: full
+  rank).
 * ``train_<name>.npz``  -- the ``HiC-GNN_main.py:117-132`` loop run for a fixed K on the same input
   (deterministic algorithms), loss history and final coordinates.
 
@@ -161,11 +164,30 @@ def train_case(ref_utils, ref_models, cls_name, data, steps=25, seed=0):
     print(f"train_{cls_name}: loss {hist[0]:.6g} -> {hist[-1]:.6g}")
 
 
-def main(ref):
+def align_case(ref_utils, l1, l5, f=512, seed=11):
+    """utils.domain_alignment (utils.py:83-109) on the chr19 1 mb / 500 kb lists with seeded float32
+    embeddings (node2vec's dtype): the fitted 500 kb embeddings the reference produces."""
+    n1 = len(np.unique(np.concatenate([l1[:, 0], l1[:, 1]])))
+    n5 = len(np.unique(np.concatenate([l5[:, 0], l5[:, 1]])))
+    rng = np.random.default_rng(seed)
+    e1 = rng.standard_normal((n1, f)).astype(np.float32)
+    e5 = rng.standard_normal((n5, f)).astype(np.float32)
+    fit = ref_utils.domain_alignment(l1, l5, e1, e5)
+    np.savez_compressed(os.path.join(HERE, f"align_chr19_f{f}.npz"), list1=l1, list2=l5, emb1=e1, emb2=e5,
+                        fitembed=fit)
+    print(f"align_chr19_f{f}: {e1.shape} {e5.shape} -> {fit.shape} {fit.dtype}")
+
+
+def main(ref, only=None):
     torch.set_num_threads(1)
     ref_utils, ref_models = _import_reference(ref)
     l1 = np.loadtxt(os.path.join(ref, "Data", "GM12878_1mb_chr19_list.txt"))
     l5 = np.loadtxt(os.path.join(ref, "Data", "GM12878_500kb_chr19_list.txt"))
+    if only in (None, "align"):
+        align_case(ref_utils, l1, l5, 512)
+        align_case(ref_utils, l1, l5, 32)
+    if only is not None:
+        return
     _, data1 = graph_case(ref_utils, "chr19_1mb", l1)
     graph_case(ref_utils, "chr19_500kb", l5)
     graph_case(ref_utils, "synth256", synth_list())
@@ -176,4 +198,4 @@ def main(ref):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference", sys.argv[2] if len(sys.argv) > 2 else None)

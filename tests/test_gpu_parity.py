@@ -815,3 +815,120 @@ def test_grad_sink_equals_autograd_accumulation(name):
     opt.zero_grad()
     m1.loss(x, adj, tr)[0].backward()
     assert g.abs().sum() > 0 and torch.all(opt.grad.abs().sum() > 0)
+
+
+# ---------------------------------------------------------------- f2: KR normalisation on the GPU
+def _kr_inputs():
+    rng = np.random.default_rng(4)
+    n = 600
+    a = rng.random((n, n)) * (rng.random((n, n)) < 0.3) * 100
+    a = np.triu(a, 1)
+    a = a + a.T
+    a[17, :] = 0
+    a[:, 17] = 0
+    a[40, 41] = a[41, 40] = np.nan
+    return a
+
+
+@pytest.mark.parametrize("case", ["chr19_1mb", "chr19_500kb", "synth600"])
+def test_kr_device_matches_oracle(case):
+    """hicgat.kr.KRnorm (HIP matvec / scale + device CG bookkeeping) vs the r_utils.R restatement:
+    the same kept rows and NaN positions, values equal after the 6-digit rounding except where the
+    two summation orders straddle a rounding boundary (one unit of 1e-6, rare)."""
+    import hicgat
+    from oracle import kr
+    if case == "synth600":
+        m = _kr_inputs()
+    else:
+        m = load_golden(f"graph_{case}.npz")["matrix"].copy()
+        np.fill_diagonal(m, 0)
+    ref, keep_r = kr.krnorm(m)
+    out, keep, info = hicgat.kr.KRnorm(m, return_info=True)
+    out = out.cpu().numpy()
+    assert np.array_equal(keep.cpu().numpy(), keep_r)
+    assert np.array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    diff = np.abs(out[ok] - ref[ok])
+    assert diff.max() <= 1.0000001e-6
+    assert (diff > 0).mean() < 0.01
+    assert np.array_equal(out[ok], np.rint(out[ok] * 1e6) / 1e6)
+
+
+@pytest.mark.parametrize("case,pdb,logged", [
+    ("chr19_1mb", "GM12878_1mb_chr19_list_structure.pdb", 0.945986103111681),
+    ("chr19_500kb", "GM12878_500kb_chr19_list_generalized_structure.pdb", 0.8074002899996215)])
+def test_kr_device_reproduces_logged_dscc(case, pdb, logged):
+    """Device KR -> device load_input / cont2dist(0.4) -> dSCC against the reference's PDB
+    coordinates = the dSCC of the reference's log."""
+    import os
+    import hicgat
+    from conftest import GOLDEN
+    m = load_golden(f"graph_{case}.npz")["matrix"].copy()
+    np.fill_diagonal(m, 0)
+    normed, _ = hicgat.kr.KRnorm(m)
+    data = hicgat.load_input(normed.cpu().numpy(), np.zeros((m.shape[0], 1), np.float32))
+    t = hicgat.cont2dist(data.y, 0.4)
+    c = torch.tensor(hicgat.io.read_pdb_coords(os.path.join(GOLDEN, pdb)), dtype=torch.float64)
+    d = torch.cdist(c, c, compute_mode="donot_use_mm_for_euclid_dist").to(DEV)
+    rho = hicgat.metrics.spearman(hicgat.metrics.triu_pairs(t), hicgat.metrics.triu_pairs(d))
+    assert abs(rho - logged) < 3e-6
+
+
+# ---------------------------------------------------------------- f3: Procrustes / generalisation
+def test_domain_alignment_device_full_rank_matches_reference():
+    """F = 32 < matched bins: the Procrustes rotation is unique -> the reference's fitembed."""
+    import hicgat
+    fx = load_golden("align_chr19_f32.npz")
+    fit = hicgat.align.domain_alignment(fx["list1"], fx["list2"], fx["emb1"], fx["emb2"]).cpu().numpy()
+    assert _rel(fit, fx["fitembed"]) < 2e-5
+
+
+def test_domain_alignment_device_rank_deficient_is_a_procrustes_optimum():
+    """F = 512 > matched bins (the real 1 mb -> 500 kb case): R is orthogonal and reaches the same
+    optimum ||A R - B||_F as the reference's scipy solution (R itself is not unique there)."""
+    import hicgat
+    from oracle import align
+    fx = load_golden("align_chr19_f512.npz")
+    ia, ib = hicgat.align.matched_rows(fx["list1"], fx["list2"])
+    ra, rb = align.matched_rows(fx["list1"], fx["list2"])
+    assert np.array_equal(ia, ra) and np.array_equal(ib, rb)
+    A = torch.tensor(fx["emb2"][ia], device=DEV)
+    B = torch.tensor(fx["emb1"][ib], device=DEV)
+    R = hicgat.align.procrustes(A, B).double()
+    assert (R.t() @ R - torch.eye(512, dtype=torch.float64, device=DEV)).abs().max().item() < 1e-5
+    _, Rr, Ar, Br = align.domain_alignment(fx["list1"], fx["list2"], fx["emb1"], fx["emb2"])
+    obj = torch.linalg.norm(A.double() @ R - B.double()).item()
+    obj_ref = np.linalg.norm(Ar.astype(np.float64) @ Rr.astype(np.float64) - Br)
+    assert abs(obj - obj_ref) <= 1e-5 * obj_ref
+    fit = hicgat.align.domain_alignment(fx["list1"], fx["list2"], fx["emb1"], fx["emb2"])
+    assert _rel(fit.cpu(), (torch.tensor(fx["emb2"], device=DEV).double() @ R).cpu()) < 1e-5
+
+
+def test_generalize_matches_oracle_pipeline():
+    """HiC_GAT_generalize_directly.py:312-336 on chr19 500 kb: aligned embeddings -> load_input ->
+    get_model -> dSCC vs cont2dist(normed, 1); the oracle model with the same weights on the same
+    aligned embeddings gives the same dSCC."""
+    import hicgat
+    from scipy.stats import spearmanr
+    from oracle import gat as og
+    from oracle import graph as ogr
+    from oracle import kr
+    fx = load_golden("align_chr19_f512.npz")
+    emb1 = (0.1 * fx["emb1"]).astype(np.float32)
+    emb2 = (0.1 * fx["emb2"]).astype(np.float32)
+    m = load_golden("graph_chr19_500kb.npz")["matrix"].copy()
+    np.fill_diagonal(m, 0)
+    normed, _ = kr.krnorm(m)
+    torch.manual_seed(0)
+    ref = og.GATNetSelectiveResidualsUpdated()
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    rho, coords = hicgat.align.generalize(model, fx["list1"], fx["list2"], emb1, emb2, normed, 1)
+    fit = hicgat.align.domain_alignment(fx["list1"], fx["list2"], emb1, emb2).cpu()
+    d = ogr.load_input(normed.copy(), fit.numpy())
+    c_ref = ref.get_model(d["x"], (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))).detach()
+    np.testing.assert_allclose(coords.cpu().numpy(), c_ref.numpy(), rtol=1e-5, atol=1e-6)
+    t = ogr.cont2dist(d["y"], 1).float().numpy()
+    iu = np.triu_indices(len(t), 1)
+    dd = torch.cdist(c_ref, c_ref, compute_mode="donot_use_mm_for_euclid_dist").numpy()
+    assert abs(rho - spearmanr(t[iu], dd[iu])[0]) < 1e-4

@@ -2,9 +2,13 @@
 
 Fixtures: tests/golden/make_golden.py (imports reference utils.py / models.py with PyG stubs).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+
+from conftest import GOLDEN
 
 from oracle import gat, graph, loop
 
@@ -189,3 +193,58 @@ def test_sage_adjoint_is_transpose():
     inv = sage.degree_inverse(rp, c, v, 40)
     dense = (np.asarray(a, np.float32) * inv[:, None]).astype(np.float64)   # fp32 weights, as N
     np.testing.assert_allclose(x.grad.numpy(), dense.T @ gout.numpy(), rtol=1e-6)
+
+
+# ---------------------------------------------------------------- f2: KR normalisation (r_utils.R)
+@pytest.mark.parametrize("case,pdb,logged", [
+    ("chr19_1mb", "GM12878_1mb_chr19_list_structure.pdb", 0.945986103111681),
+    ("chr19_500kb", "GM12878_500kb_chr19_list_generalized_structure.pdb", 0.8074002899996215)])
+def test_kr_reproduces_logged_dscc(golden, case, pdb, logged):
+    """The KR restatement + load_input + cont2dist(., 0.4) + Spearman against the coordinates of the
+    reference's own Outputs/*_structure.pdb gives the dSCC logged in Outputs/*_log.txt (SURVEY fact
+    9).  The PDB stores coordinates * 100 to 3 decimals, which moves the rank correlation by ~1e-6."""
+    from scipy.stats import spearmanr
+    from hicgat.io import read_pdb_coords
+    from oracle import graph as og
+    from oracle import kr
+    g = golden(f"graph_{case}.npz")
+    m = g["matrix"].copy()
+    np.fill_diagonal(m, 0)
+    normed, keep = kr.krnorm(m)
+    assert np.array_equal(keep, np.arange(m.shape[0]))
+    assert np.array_equal(normed, kr.round6(normed)) and np.allclose(normed, normed.T, atol=1e-6)
+    t = og.cont2dist(og.load_input(normed.copy(), np.zeros((len(keep), 1), np.float32))["y"], 0.4).numpy()
+    c = read_pdb_coords(os.path.join(GOLDEN, pdb))
+    iu = np.triu_indices(len(c), 1)
+    d = np.sqrt(((c[:, None, :] - c[None, :, :]) ** 2).sum(-1))
+    assert abs(spearmanr(t[iu], d[iu])[0] - logged) < 3e-6
+
+
+def test_kr_quirks_nan_zero_columns_and_balance():
+    """Zero columns dropped (rows follow), NaN restored in place, the balanced matrix has unit row
+    sums (to the 6-digit rounding of r_utils.R:89)."""
+    from oracle import kr
+    rng = np.random.default_rng(0)
+    n = 80
+    a = rng.random((n, n)) * (rng.random((n, n)) < 0.4)
+    a = np.triu(a, 1)
+    a = a + a.T
+    a[9, :] = 0
+    a[:, 9] = 0
+    a[3, 5] = a[5, 3] = np.nan
+    normed, keep = kr.krnorm(a)
+    assert 9 not in keep and len(keep) == n - 1
+    i3, i5 = int(np.where(keep == 3)[0][0]), int(np.where(keep == 5)[0][0])
+    assert np.isnan(normed[i3, i5]) and np.isnan(normed[i5, i3]) and np.isnan(normed).sum() == 2
+    rs = np.nansum(normed, axis=1)
+    assert np.abs(rs - 1).max() < 1e-4
+
+
+# ---------------------------------------------------------------- f3: domain alignment (utils.py)
+@pytest.mark.parametrize("f", [512, 32])
+def test_domain_alignment_oracle_matches_reference(golden, f):
+    from oracle import align
+    fx = golden(f"align_chr19_f{f}.npz")
+    fit, R, A, B = align.domain_alignment(fx["list1"], fx["list2"], fx["emb1"], fx["emb2"])
+    np.testing.assert_array_equal(fit, fx["fitembed"])
+    assert np.abs(R.T @ R - np.eye(f)).max() < 1e-5
