@@ -178,7 +178,7 @@ def main():
         runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss)
         step = runner.step
     else:
-        opt = hicgat.FlatAdam(model.parameters(), lr=1e-3)
+        opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
         stats = torch.empty(12, dtype=torch.float64, device=dev)
 
         def step():

@@ -6,7 +6,8 @@
 //   forward : z = relu((y - mean) * rstd * gamma + beta) + res,   rstd = 1/sqrt(var + eps)
 //             (biased variance, torch.nn.LayerNorm semantics), saves (mean, rstd) per row;
 //   backward: g = dz * [pre > 0];  dgamma += g * yhat;  dbeta += g;  dyhat = g * gamma;
-//             dy = rstd * (dyhat - mean(dyhat) - yhat * mean(dyhat * yhat));  dres = dz.
+//             dy = rstd * (dyhat - mean(dyhat) - yhat * mean(dyhat * yhat));  dres = dz (optionally
+//             written beside dy, so a packed [dy | dres] feeds one dual-Linear backward GEMM).
 // dgamma/dbeta: per-wave register partials over a grid-stride row loop, then the fixed-order
 // column reduction of reduce.hip over the waves (deterministic).  Width W in {64, 128, 256} (W/64 values per lane).
 #include "reduce.hpp"
@@ -55,6 +56,7 @@ __global__ __launch_bounds__(256) void ln_relu_res_bwd_kernel(const float *__res
                                                               const float *__restrict__ gamma,
                                                               const float *__restrict__ beta,
                                                               float *__restrict__ dy, int64_t lddy,
+                                                              float *__restrict__ dres, int64_t lddres,
                                                               float *__restrict__ part) {
   constexpr int V = W / 64;
   const int lane = lane_id();
@@ -76,7 +78,9 @@ __global__ __launch_bounds__(256) void ln_relu_res_bwd_kernel(const float *__res
       const int c = q * 64 + lane;
       yh[q] = (y[(size_t)row * ldy + c] - st.x) * st.y;
       const float pre = fmaf(yh[q], g_[q], b_[q]);
-      const float g = pre > 0.f ? dz[(size_t)row * W + c] : 0.f;
+      const float dzv = dz[(size_t)row * W + c];
+      if (dres) dres[(size_t)row * lddres + c] = dzv;   // d(residual) = dz, written beside dy
+      const float g = pre > 0.f ? dzv : 0.f;
       pg[q] = fmaf(g, yh[q], pg[q]);
       pb[q] += g;
       dh[q] = g * g_[q];
@@ -123,8 +127,9 @@ extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W) {
 
 extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, int W,
                                       const float *row_stats, const float *gamma, const float *beta, float *dy,
-                                      int64_t lddy, float *dgamma, float *dbeta, int accumulate, void *workspace,
-                                      size_t workspace_bytes, hicgat_stream_t stream) {
+                                      int64_t lddy, float *dres, int64_t lddres, float *dgamma, float *dbeta,
+                                      int accumulate, void *workspace, size_t workspace_bytes,
+                                      hicgat_stream_t stream) {
   if (M < 0 || (W != 64 && W != 128 && W != 256)) return M < 0 ? HICGAT_EINVAL : HICGAT_EUNSUPPORTED;
   if (!dz || !y || !row_stats || !gamma || !beta || !dy || !dgamma || !dbeta || !workspace) return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_ln_relu_res_workspace_bytes(W)) return HICGAT_EINVAL;
@@ -133,11 +138,11 @@ extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t l
   const float2 *st = reinterpret_cast<const float2 *>(row_stats);
   const dim3 grid(kLnWaves / 4);
   if (W == 64)
-    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<64>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, part);
+    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<64>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, dres, lddres, part);
   else if (W == 128)
-    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<128>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, part);
+    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<128>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, dres, lddres, part);
   else
-    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<256>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, part);
+    hipLaunchKernelGGL(ln_relu_res_bwd_kernel<256>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, dres, lddres, part);
   HICGAT_CHECK_LAUNCH();
   // dgamma / dbeta = column sums of the per-wave partials [kLnWaves, 2W] (fixed order)
   const ColOut o{dgamma, 0, W, dbeta, nullptr, accumulate};

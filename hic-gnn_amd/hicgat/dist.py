@@ -92,7 +92,7 @@ class ShardedTrainer:
         T = kern.num_tiles(N)
         self.t0 = T * self.rank // P
         self.t1 = T * (self.rank + 1) // P
-        self.opt = FlatAdam(model.parameters(), lr=lr, kern=kern)
+        self.opt = FlatAdam(model.flat_parameters(), lr=lr, kern=kern)
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay

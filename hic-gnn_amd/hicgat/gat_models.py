@@ -23,6 +23,10 @@ def _lin(layer, x):
 
 
 class _CoordsModel(torch.nn.Module):
+    def flat_parameters(self):
+        """Parameter order for ``FlatAdam``'s flat buffers (default: ``parameters()``)."""
+        return list(self.parameters())
+
     def forward(self, x, edge_index):
         return ops.pairwise_dist(self.get_model(x, edge_index))
 
@@ -49,14 +53,23 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
 
     conv_act = "relu"   # the relu of models.py:637 runs in the GAT aggregation's epilogue
 
+    def flat_parameters(self):
+        """dense* / align_dense* weights and biases adjacent in the flat buffers, so each residual
+        block's [W1; W2] and [b1; b2] are views (one GEMM / one column sum in the backward)."""
+        return [self.conv.lin_l.weight, self.conv.att_l, self.conv.att_r, self.conv.bias,
+                self.densea.weight, self.align_densea.weight, self.densea.bias, self.align_densea.bias,
+                self.norm_a.weight, self.norm_a.bias,
+                self.dense1.weight, self.align_dense1.weight, self.dense1.bias, self.align_dense1.bias,
+                self.norm1.weight, self.norm1.bias,
+                self.dense2.weight, self.dense2.bias, self.norm2.weight, self.norm2.bias,
+                self.dense3.weight, self.dense3.bias]
+
     def post_act(self, x):
-        """models.py:638-659 (after the relu): [densea | align_densea] as one GEMM,
-        relu(norm_a(.)) + residual in one pass; the same for dense1 / align_dense1 / norm1;
+        """models.py:638-659 (after the relu): each residual block relu(norm(dense(x))) +
+        align_dense(x) as one fused op (one GEMM over [W; W_align], one row pass);
         relu(norm2(dense2(.))); dense3."""
-        y, res = ops.dual_linear(x, self.densea, self.align_densea)
-        x = ops.ln_relu_res(y, self.norm_a, res)
-        y, res = ops.dual_linear(x, self.dense1, self.align_dense1)
-        x = ops.ln_relu_res(y, self.norm1, res)
+        x = ops.dual_ln_relu_res(x, self.densea, self.align_densea, self.norm_a)
+        x = ops.dual_ln_relu_res(x, self.dense1, self.align_dense1, self.norm1)
         x = ops.ln_relu_res(_lin(self.dense2, x), self.norm2)
         return _lin(self.dense3, x)
 

@@ -254,6 +254,84 @@ def ln_relu_res(y, norm, res=None):
     return _LnReluResFn.apply(y, norm.weight, norm.bias, res, norm.eps)
 
 
+def _adjacent(a, b):
+    """``b`` starts right where ``a`` ends in memory (two flat-buffer parameter views): the pair
+    is then one [a; b] tensor without a copy."""
+    return (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size())
+
+
+def _joined(a, b):
+    """[a; b] along dim 0 -- a view when the two are adjacent (``flat_parameters`` order)."""
+    if _adjacent(a, b):
+        return torch.as_strided(a, (a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride())
+    return torch.cat([a, b])
+
+
+class _DualLnReluResFn(torch.autograd.Function):
+    """relu(norm(lin1(x))) + lin2(x) -- the residual blocks of models.py:638-649 -- as
+    ONE GEMM Y = x [W1; W2]^T + [b1; b2] and one row pass over Y = [y | res].  The backward's LN
+    pass writes dY = [dy | dz] packed, so dx is ONE GEMM (K = 2W) and, with the pairs adjacent in
+    FlatAdam's buffer (``flat_parameters``), dW and db are one GEMM / one column sum each."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, gamma, beta, eps):
+        K = kernels.default()
+        x = x.contiguous()
+        M = x.shape[0]
+        w = W1.shape[0]
+        Wc = _joined(W1, W2)
+        bc = _joined(b1, b2)
+        Y = torch.empty((M, 2 * w), dtype=torch.float32, device=x.device)
+        K.gemm(0, 0, M, 2 * w, x.shape[1], x, Wc.contiguous(), Y, bias=bc.contiguous(), name="gemm_fwd")
+        z = torch.empty((M, w), dtype=torch.float32, device=x.device)
+        stats = torch.empty((M, 2), dtype=torch.float32, device=x.device)
+        K.ln_relu_res_fwd(Y[:, :w], gamma, beta, eps, Y[:, w:], z, stats)
+        ctx.save_for_backward(x, Y, stats, gamma, beta)
+        ctx.params = (W1, b1, W2, b2, gamma, beta)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        K = kernels.default()
+        x, Y, stats, gamma, beta = ctx.saved_tensors
+        W1, b1, W2, b2, pg, pb = ctx.params
+        dz = dz.contiguous()
+        M, w = dz.shape
+        dY = torch.empty((M, 2 * w), dtype=torch.float32, device=dz.device)
+        sg, sb = _sink(pg), _sink(pb)
+        dgamma = dbeta = None
+        if sg is not None and sb is not None:
+            K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], sg, sb, accumulate=True, dres=dY[:, w:])
+        else:
+            dgamma, dbeta = torch.empty_like(gamma), torch.empty_like(beta)
+            K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], dgamma, dbeta, dres=dY[:, w:])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(0, 1, M, x.shape[1], 2 * w, dY, _joined(W1, W2).contiguous(), torch.empty_like(x),
+                        name="gemm_dx")
+        sW1, sW2, sb1, sb2 = _sink(W1), _sink(W2), _sink(b1), _sink(b2)
+        dW1 = dW2 = db1 = db2 = None
+        if sW1 is not None and sW2 is not None and _adjacent(sW1, sW2):
+            weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True)
+        else:
+            dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
+            dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
+        if sb1 is not None and sb2 is not None and _adjacent(sb1, sb2):
+            K.colsum(dY, _joined(sb1, sb2), accumulate=True)
+        else:
+            db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
+            db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
+        return dx, dW1, db1, dW2, db2, dgamma, dbeta, None
+
+
+def dual_ln_relu_res(x, lin1, lin2, norm):
+    """relu(norm(lin1(x))) + lin2(x) (models.py:638-641 / :646-649) on the fused kernels."""
+    _dev_check(x)
+    return _DualLnReluResFn.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias, norm.weight, norm.bias,
+                                  norm.eps)
+
+
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):
     """GATConv forward; ``act="relu"`` returns relu(GATConv(x)) with the relu fused."""
     if adj.rowptr32 is None or adj.rowptr32.device != x.device:

@@ -1,4 +1,5 @@
-"""The HiC-GNN_main.py training loop on the HIP path (a14), plus a CLI mirroring its flags.
+"""The HiC-GNN_main.py training loop on the HIP path (a14), plus a CLI mirroring its flags
+(list -> convert_to_matrix -> KRnorm on the GPU -> load_input -> train per conversion -> dSCC).
 
 Loop semantics kept from HiC-GNN_main.py:117-132:
   Adam(lr) over model.parameters(); oldloss, lossdiff = 1, 1; truth = cont2dist(y, 0.5);
@@ -34,7 +35,7 @@ def train_step(model, opt, x, edge_index, truth, kind="mse", stats=None):
 def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_steps=1_000_000,
           on_step=None):
     """Returns (optimizer, per-step loss list).  ``truth`` is a ``graph.Truth``."""
-    opt = FlatAdam(model.parameters(), lr=lr)
+    opt = FlatAdam(model.flat_parameters(), lr=lr)
     old, diff, hist = 1.0, 1.0, []
     stats = torch.empty(12, dtype=torch.float64, device=data.x.device)
     while (diff > thresh if steps is None else len(hist) < steps) and len(hist) < max_steps:
@@ -55,7 +56,7 @@ def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_
 def main(argv=None):
     p = argparse.ArgumentParser(description="Train a GAT-HiC model on the MI355X path "
                                             "(HiC-GNN_main.py flags).")
-    p.add_argument("matrix", help="Hi-C list (bin_i bin_j count) or (normalised) dense matrix text file")
+    p.add_argument("matrix", help="Hi-C list (bin_i bin_j count) or dense matrix text file")
     p.add_argument("features", help="N x F embedding text file (np.loadtxt)")
     p.add_argument("-c", "--conversions", default="[.5]", help="conversion factor list, '[a, step, b]' or '[f]'")
     p.add_argument("-lr", "--learningrate", type=float, default=1e-3)
@@ -65,11 +66,20 @@ def main(argv=None):
     p.add_argument("--loss", default="mse", choices=["mse", "combined"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--out", default=None, help="prefix for <out>_weights.pt / _structure.pdb / _log.txt")
+    p.add_argument("--no-kr", action="store_true", help="the input is already KR-normalised (skip KRnorm)")
     a = p.parse_args(argv)
     conv = ast.literal_eval(a.conversions)
     conv = list(np.arange(conv[0], conv[2], conv[1])) if len(conv) == 3 else [conv[0]]
     mat = np.loadtxt(a.matrix)
     feats = np.loadtxt(a.features).astype(np.float32)
+    if mat.shape[1] == 3:                       # HiC-GNN_main.py:75-78
+        mat = graph.convert_to_matrix(mat)
+    np.fill_diagonal(mat, 0)                    # :80
+    if not a.no_kr:                             # :85-89 (Rscript normalize.R -> r_utils.R KRnorm)
+        from .kr import KRnorm
+        normed, keep = KRnorm(mat)
+        mat = normed.cpu().numpy()
+        feats = feats[keep.cpu().numpy()] if len(keep) != len(feats) else feats
     data = graph.load_input(mat, feats)
     best = None
     for f in conv:

@@ -187,15 +187,16 @@ size_t hicgat_colsum_workspace_bytes(int K, int N);
 /* ---- a6: LayerNorm + ReLU (+ residual) of the flagship tail (models.py:641-655) --------------
  * z = relu(LayerNorm(y) * gamma + beta) + res (res may be NULL), W in {64, 128, 256}, eps as in
  * torch.nn.LayerNorm (biased variance); row_stats [M, 2] = (mean, rstd) saved for the backward.
- * Backward: dy (ld lddy), dgamma/dbeta (accumulate != 0 adds into them); dres = dz is the
- * caller's (no copy).  workspace: hicgat_ln_relu_res_workspace_bytes(W). */
+ * Backward: dy (ld lddy), dgamma/dbeta (accumulate != 0 adds into them); dres = dz: the caller's
+ * dz, or (dres != NULL) also written to dres (ld lddres), e.g. beside dy in one packed [dy | dres]
+ * row for the fused dual-Linear backward.  workspace: hicgat_ln_relu_res_workspace_bytes(W). */
 int hicgat_ln_relu_res_fwd(const float *y, int64_t ldy, int M, int W, const float *gamma, const float *beta,
                            float eps, const float *res, int64_t ldr, float *z, float *row_stats,
                            hicgat_stream_t stream);
 int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, int W, const float *row_stats,
-                           const float *gamma, const float *beta, float *dy, int64_t lddy, float *dgamma,
-                           float *dbeta, int accumulate, void *workspace, size_t workspace_bytes,
-                           hicgat_stream_t stream);
+                           const float *gamma, const float *beta, float *dy, int64_t lddy, float *dres,
+                           int64_t lddres, float *dgamma, float *dbeta, int accumulate, void *workspace,
+                           size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_ln_relu_res_workspace_bytes(int W);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------

@@ -86,7 +86,14 @@ def _worker(rank, world, port, n, kind, out):
             if grad1 is None:
                 grad1, stats1 = tr.opt.grad.clone(), stats.clone()   # all-reduced step-1 gradient
         if rank == 0:
-            torch.save({"losses": losses, "flat": tr.opt.flat.clone(), "grad1": grad1, "stats": stats1}, out)
+            # per-parameter step-1 gradients by name (the flat layout follows model.flat_parameters())
+            off, by_name = {}, {}
+            for p, o in zip(tr.opt.params, tr.opt.offsets):
+                off[id(p)] = o
+            for name, p in model.named_parameters():
+                by_name[name] = grad1[off[id(p)]:off[id(p)] + p.numel()].view_as(p).clone()
+            torch.save({"losses": losses, "flat": tr.opt.flat.clone(), "grad1": grad1, "stats": stats1,
+                        "grads": by_name}, out)
     finally:
         dist.destroy_process_group()
 
@@ -138,10 +145,8 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
     model = hicgat.GATNetSelectiveResidualsUpdated()
-    off = 0
     for (name, p), pr in zip(model.named_parameters(), ref.parameters()):
-        mine = one["grad1"][off:off + p.numel()].view_as(pr.grad)
-        off += (p.numel() + 3) // 4 * 4
+        mine = one["grads"][name]
         scale = pr.grad.abs().max().item()
         if name == "dense3.bias":   # exact value 0 (translation invariance): rounding noise only
             assert mine.abs().max().item() < 1e-6 * max(1.0, scale)
