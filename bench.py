@@ -261,7 +261,10 @@ def main():
         "graph": bool(args.graph),
         "config": {"workload": args.workload, "model": "GATNetSelectiveResidualsUpdated",
                    "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz, "d": D_FEAT, "heads": HEADS,
-                   "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single"},
+                   "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single",
+                   "gemm": {0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl],
+                   "aggregation": (f"xcd column strips x{kernels.default().slice_width}"
+                                   if kernels.default().slice_width else "row per wave")},
         "final_loss": loss_v,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,

@@ -37,6 +37,12 @@ SIGNATURES = {
                                           c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_sliced_workspace_bytes": (c_sz, [c_int, c_int, c_int, c_int]),
+    "hicgat_gat_agg_fwd_sliced": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p,
+                                          c_p, c_f, c_int, c_int, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "hicgat_gat_agg_bwd_src_sliced": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p,
+                                              c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_int, c_p, c_p, c_p,
+                                              c_sz, c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),
@@ -50,6 +56,8 @@ SIGNATURES = {
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),
     "hicgat_gemm_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
+    "hicgat_gemm_ex": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
+                               c_int, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_ln_relu_res_fwd": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_p]),

@@ -5,12 +5,19 @@ stream-ordered on torch's current stream; the ``timed`` names feed bench.py's li
 The distributed trainer (``hicgat.dist``) is written against this interface only, so its
 partitioning / collective logic can be exercised on CPU in tests with a stand-in object.
 """
+import os
+
 import torch
 
 from . import _lib
 
 # name -> list of (start, end) torch.cuda.Event pairs recorded around launches (bench.py)
 TIMERS = None
+SLICE_DEFAULT = 0
+GEMM_IMPLS = {"auto": 0, "f32": 1, "x3": 2}
+# the product default is the plain fp32 MFMA GEMM; HICGAT_GEMM=auto opts into the fp32-accurate x3
+# split where it applies (10-25 % faster GEMMs, profiles/r01_kbench_x3_sliced.txt)
+GEMM_DEFAULT = "f32"
 
 
 class _timed:
@@ -37,6 +44,12 @@ class HipKernels:
 
     def __init__(self):
         self.lib = _lib.lib()
+        # column-strip width of the XCD-sliced aggregation kernels (csrc/gat_sliced.hip); 0 = the
+        # row-per-wave kernels (gat_fwd.hip / gat_bwd.hip)
+        self.slice_width = int(os.environ.get("HICGAT_SLICE", str(SLICE_DEFAULT)))
+        # matrix-core arithmetic of the GEMMs (include/hicgat.h HICGAT_GEMM_*): 0 auto (x3 where
+        # supported), 1 fp32 MFMA only, 2 x3 only
+        self.gemm_impl = GEMM_IMPLS[os.environ.get("HICGAT_GEMM", GEMM_DEFAULT)]
 
     # -- a2 ---------------------------------------------------------------------------------------
     def linear_att(self, x, W, att_l, att_r, h=None):
@@ -48,6 +61,15 @@ class HipKernels:
         assert h.shape == (N, H * C) and h.is_contiguous()
         a_src = torch.empty((N, H), dtype=torch.float32, device=x.device)
         a_dst = torch.empty_like(a_src)
+        if self.gemm_impl != 1 and N >= 32 and F % 4 == 0 and x.stride(0) % 4 == 0:
+            # x3 GEMM into h, then the logits in one pass over h
+            st = _lib.stream(x.device)
+            with _timed("gat_linear_att"):
+                _lib.check(self.lib.hicgat_gemm_ex(0, 0, N, H * C, F, P(x), x.stride(0), P(W), W.stride(0), None, P(h),
+                                                   h.stride(0), 0, 1, self.gemm_impl, None, 0, st), "hicgat_gemm_ex")
+                _lib.check(self.lib.hicgat_gat_att_logits(P(h), P(att_l), P(att_r), N, H, C, P(a_src), P(a_dst), st),
+                           "hicgat_gat_att_logits")
+            return h, a_src, a_dst
         with _timed("gat_linear_att"):
             _lib.check(self.lib.hicgat_gat_linear_att(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(h), P(a_src),
                                                       P(a_dst), _lib.stream(x.device)), "hicgat_gat_linear_att")
@@ -64,6 +86,8 @@ class HipKernels:
 
     # -- a4 + a5 ----------------------------------------------------------------------------------
     def agg_fwd(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats):
+        if self.slice_width:
+            return self.agg_fwd_act(rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, 0, out, None, row_stats)
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
@@ -77,6 +101,15 @@ class HipKernels:
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
+        if self.slice_width:
+            nnz = col.numel()
+            ws = _lib.workspace(self.lib.hicgat_gat_sliced_workspace_bytes(N, nnz, H, self.slice_width), h.device)
+            with _timed("gat_agg_fwd"):
+                _lib.check(self.lib.hicgat_gat_agg_fwd_sliced(P(rowptr), P(col), N, nnz, H, C, r0, r1, P(h), P(a_src),
+                                                              P(a_dst), P(bias), float(ns), int(act), self.slice_width,
+                                                              P(out), P(out2), P(row_stats), P(ws), ws.numel(),
+                                                              _lib.stream(h.device)), "hicgat_gat_agg_fwd_sliced")
+            return
         with _timed("gat_agg_fwd"):
             _lib.check(self.lib.hicgat_gat_agg_fwd_act(P(rowptr), P(col), N, col.numel(), H, C, r0, r1, P(h),
                                                        P(a_src), P(a_dst), P(bias), float(ns), int(act), P(out),
@@ -110,6 +143,15 @@ class HipKernels:
         C = h.shape[1] // H
         # row_stats / dout may be row-strided views (the packed all-gather buffer of hicgat.dist)
         assert row_stats.stride(1) == 1 and dout.stride(1) == 1
+        if self.slice_width:
+            nnz = col.numel()
+            ws = _lib.workspace(self.lib.hicgat_gat_sliced_workspace_bytes(N, nnz, H, self.slice_width), h.device)
+            with _timed("gat_agg_bwd_src"):
+                _lib.check(self.lib.hicgat_gat_agg_bwd_src_sliced(
+                    P(rowptr), P(col), N, nnz, H, C, r0, r1, P(h), P(a_src), P(a_dst), P(row_stats), row_stats.stride(0),
+                    P(dout), dout.stride(0), P(att_l), P(att_r), float(ns), self.slice_width, P(dh), P(da_src), P(ws),
+                    ws.numel(), _lib.stream(h.device)), "hicgat_gat_agg_bwd_src_sliced")
+            return
         with _timed("gat_agg_bwd_src"):
             _lib.check(self.lib.hicgat_gat_agg_bwd_src_ld(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
                                                           P(a_dst), P(row_stats), row_stats.stride(0), P(dout),
@@ -181,17 +223,19 @@ class HipKernels:
                                                 _lib.stream(coords.device)), "hicgat_pairdist_bwd")
         return dc
 
-    # -- a6: Linear layers on the fp32 MFMA GEMM ---------------------------------------------------
-    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=1, name="gemm"):
+    # -- a6: Linear layers on the MFMA GEMM (fp32, or the fp32-accurate x3 split) ------------------
+    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=1, name="gemm",
+             impl=None):
         dev = C.device
         ws = None
         if splits > 1:
             ws = _lib.workspace(self.lib.hicgat_gemm_workspace_bytes(M, N, splits), dev)
+        impl = self.gemm_impl if impl is None else impl
         with _timed(name):
-            _lib.check(self.lib.hicgat_gemm(int(a_kmajor), int(b_kmajor), M, N, K, P(A), A.stride(0), P(B),
-                                            B.stride(0), P(bias), P(C), C.stride(0), int(accumulate), int(splits),
-                                            P(ws), 0 if ws is None else ws.numel(), _lib.stream(dev)),
-                       "hicgat_gemm")
+            _lib.check(self.lib.hicgat_gemm_ex(int(a_kmajor), int(b_kmajor), M, N, K, P(A), A.stride(0), P(B),
+                                               B.stride(0), P(bias), P(C), C.stride(0), int(accumulate), int(splits),
+                                               int(impl), P(ws), 0 if ws is None else ws.numel(), _lib.stream(dev)),
+                       "hicgat_gemm_ex")
         return C
 
     def colsum(self, A, out, accumulate=False):

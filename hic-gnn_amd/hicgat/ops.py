@@ -105,13 +105,14 @@ def _splits(m, n, k, target=1024):
     return max(1, min(k // 256, target // tiles))
 
 
-def weight_grad(K, dy, x, out=None, accumulate=False):
+def weight_grad(K, dy, x, out=None, accumulate=False, impl=None):
     """dW = dy^T x (Linear / lin_l weight gradient), K = rows, split-K MFMA GEMM."""
     rows, m = dy.shape
     n = x.shape[1]
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=dy.device)
-    return K.gemm(1, 1, m, n, rows, dy, x, out, accumulate=accumulate, splits=_splits(m, n, rows), name="gemm_dw")
+    return K.gemm(1, 1, m, n, rows, dy, x, out, accumulate=accumulate, splits=_splits(m, n, rows), name="gemm_dw",
+                  impl=impl)
 
 
 def _weight_grad_to(K, p, dy, x):

@@ -129,6 +129,25 @@ int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, 
                               const float *dout, int64_t ld_dout, const float *att_src,
                               const float *att_dst, float neg_slope, float *dh, float *da_src,
                               hicgat_stream_t stream);
+/* Column-sliced forms of hicgat_gat_agg_fwd_act and hicgat_gat_agg_bwd_src_ld: the same outputs
+ * (row_stats max / sum / S3 bit-identical, out / out2 / dh / da_src up to fp32 summation order).
+ * The H*C = 512 columns are cut into 512/slice_width strips (slice_width 32 or 64) and each of the
+ * 8 XCDs aggregates its own strips, so the rows one XCD gathers fit its L2; the per-edge softmax
+ * weights are formed once into edge records in the workspace
+ * (hicgat_gat_sliced_workspace_bytes(N, nnz, H, slice_width), nnz = the whole CSR). */
+size_t hicgat_gat_sliced_workspace_bytes(int N, int nnz, int H, int slice_width);
+int hicgat_gat_agg_fwd_sliced(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
+                              int row_begin, int row_end, const float *h, const float *a_src,
+                              const float *a_dst, const float *bias, float neg_slope, int act,
+                              int slice_width, float *out, float *out2, float *row_stats, void *workspace,
+                              size_t workspace_bytes, hicgat_stream_t stream);
+int hicgat_gat_agg_bwd_src_sliced(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
+                                  int row_begin, int row_end, const float *h, const float *a_src,
+                                  const float *a_dst, const float *row_stats, int64_t ld_stats,
+                                  const float *dout, int64_t ld_dout, const float *att_src,
+                                  const float *att_dst, float neg_slope, int slice_width, float *dh,
+                                  float *da_src, void *workspace, size_t workspace_bytes,
+                                  hicgat_stream_t stream);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;
@@ -179,6 +198,18 @@ int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A,
                 const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
                 int splits, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_gemm_workspace_bytes(int M, int N, int splits);
+/* The same GEMM with the matrix-core arithmetic chosen explicitly (hicgat_gemm = HICGAT_GEMM_AUTO):
+ *   HICGAT_GEMM_F32: v_mfma_f32_32x32x2_f32 (fp32 products, fp32 accumulate);
+ *   HICGAT_GEMM_X3:  every fp32 operand split exactly into three bf16 terms, the six products of
+ *     order <= 2 on v_mfma_f32_32x32x16_bf16 with fp32 accumulate -- fp32-GEMM accuracy (the dropped
+ *     terms are O(2^-24 |a b|)) at 2.7x the fp32 matrix rate; needs 16-B aligned operands, float4
+ *     rows (K, or the row dim of a K-major operand, a multiple of 4), N >= 64 and M >= 32, else
+ *     HICGAT_EUNSUPPORTED;
+ *   HICGAT_GEMM_AUTO: X3 where supported, else F32. */
+enum { HICGAT_GEMM_AUTO = 0, HICGAT_GEMM_F32 = 1, HICGAT_GEMM_X3 = 2 };
+int hicgat_gemm_ex(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A, int64_t lda,
+                   const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
+                   int splits, int impl, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 /* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
 int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                   size_t workspace_bytes, hicgat_stream_t stream);

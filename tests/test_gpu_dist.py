@@ -126,7 +126,7 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path):
     hicgat, adj, truth, x = _inputs(n, "cuda")
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
-    opt = hicgat.FlatAdam(model.parameters(), lr=1e-3)
+    opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)   # the trainer's flat layout
     loss, stats, _ = hicgat.train.train_step(model, opt, x, adj, truth)
     assert abs(float(loss) - res["loss"][0]) <= 1e-6 * abs(float(loss))
     g = opt.grad.cpu()

@@ -938,3 +938,60 @@ def test_generalize_matches_oracle_pipeline():
     iu = np.triu_indices(len(t), 1)
     dd = torch.cdist(c_ref, c_ref, compute_mode="donot_use_mm_for_euclid_dist").numpy()
     assert abs(rho - spearmanr(t[iu], dd[iu])[0]) < 1e-4
+
+
+# ---------------------------------------------------------------- north star: dSCC band
+def test_dscc_chr19_1mb_within_north_star_band():
+    """BASELINE north star: dSCC on GM12878 chr19 1 mb within +-0.005 of the reference.  The
+    HiC-GNN_main.py pipeline on both sides from identical inputs -- KR-normalised contacts
+    (oracle/kr.py on the host, hicgat.kr on the device), the fixture's 512-d features (node2vec is
+    absent), seed-0 initial weights, a fixed K = 200 steps (the threshold stop is
+    chaotic) -- then get_model -> Spearman of the upper-triangle distances against
+    the truth (HiC-GNN_main.py:135-139).  The CPU reference is itself not reproducible across
+    thread counts (its summation order changes; SURVEY 8(d) protocol: report the difference next to
+    that noise floor), so the band is +-0.005 around the oracle's 1- and 8-thread results."""
+    import hicgat
+    from oracle import gat as og
+    from oracle import graph as ogr
+    from oracle import kr as okr
+    from oracle import loop as ol
+    g = load_golden("graph_chr19_1mb.npz")
+    mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz")
+    K = 200
+    a = np.array(g["matrix"], dtype=np.float64)
+    np.fill_diagonal(a, 0)
+    normed, keep = okr.krnorm(a.copy())
+    x = np.asarray(mfx["x"], dtype=np.float32)
+    x = x[np.asarray(keep)] if len(keep) != len(x) else x
+    d = ogr.load_input(normed.copy(), x)
+    truth = ogr.cont2dist(d["y"], 0.5)
+    radj = (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))
+    threads = torch.get_num_threads()
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    refs = {}
+    try:
+        for th in (1, 8):
+            torch.set_num_threads(th)
+            torch.manual_seed(0)
+            ref = og.GATNetSelectiveResidualsUpdated()
+            ol.train(ref, d["x"], radj, truth, steps=K)
+            with torch.no_grad():
+                refs[th] = ol.dscc(ref.get_model(d["x"], radj), truth)
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+        torch.set_num_threads(threads)
+    normed_d, keep_d = hicgat.kr.KRnorm(a.copy())
+    assert np.array_equal(keep_d.cpu().numpy(), np.asarray(keep))
+    data = hicgat.load_input(normed_d.cpu().numpy(), x)
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    tr = hicgat.Truth.from_contacts(data.y, 0.5)
+    hicgat.train.train(model, data, tr, steps=K)
+    with torch.no_grad():
+        coords = model.get_model(data.x.float(), data.edge_index)
+    rho = hicgat.metrics.dscc(coords, tr.dense())
+    lo, hi = min(refs.values()), max(refs.values())
+    print(f"dSCC chr19 1mb after {K} steps: device {rho:.6f}; oracle 1 thread {refs[1]:.6f}, 8 threads "
+          f"{refs[8]:.6f} (noise floor {hi - lo:.2e}); distance to the oracle band "
+          f"{max(0.0, lo - rho, rho - hi):.2e}")
+    assert lo - 0.005 <= rho <= hi + 0.005, (rho, refs)

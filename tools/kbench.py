@@ -60,6 +60,17 @@ def main():
     g256, g256b, g256c = torch.randn(256, device=dev), torch.empty(256, device=dev), torch.empty(256, device=dev)
     ya2 = torch.empty(n, 256, device=dev)
     libs = [s for s in a.libs.split(",") if s] or [_lib.LIB_PATH]
+    sliced = {}
+
+    def _sliced(K, sw):
+        """The same library with the XCD column-strip aggregation of width sw."""
+        key = (id(K), sw)
+        if key not in sliced:
+            S = kernels.HipKernels.__new__(kernels.HipKernels)
+            S.lib, S.slice_width = K.lib, sw
+            S.gemm_impl = getattr(K, "gemm_impl", 0)
+            sliced[key] = S
+        return sliced[key]
     kset = []
     for path in libs:
         lib = ctypes.CDLL(path)
@@ -68,6 +79,8 @@ def main():
             fn.restype, fn.argtypes = res, args
         K = kernels.HipKernels.__new__(kernels.HipKernels)
         K.lib = lib
+        K.slice_width = 0            # the row-per-wave kernels; "@sw" jobs time the strip kernels
+        K.gemm_impl = 0              # GEMMs: auto (x3 where supported); "#f32" / "#x3" jobs force one
         kset.append((os.path.basename(path), K))
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
@@ -79,6 +92,10 @@ def main():
         "gat_agg_bwd_src": lambda K: K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, al, ar,
                                                    0.2, dh, da),
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
+        **{f"gat_agg_fwd_train@{sw}": (lambda K, sw=sw: _sliced(K, sw).agg_fwd_act(
+            adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out, out2, rs)) for sw in (32, 64)},
+        **{f"gat_agg_bwd_src@{sw}": (lambda K, sw=sw: _sliced(K, sw).agg_bwd_src(
+            adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, al, ar, 0.2, dh, da)) for sw in (32, 64)},
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
         "pairdist_combined": lambda K: K.fused_loss(coords, truth.buf, n, 1, 0, -1, stats, loss, dc),
         "colsum_20000x512": lambda K: K.colsum(out, cs),
@@ -88,6 +105,16 @@ def main():
         "gemm_fwd_densea": lambda K: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba),
         "gemm_dx_densea": lambda K: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa),
         "gemm_dw_densea": lambda K: hicgat.ops.weight_grad(K, ya, out),
+        **{f"gemm_fwd_densea#{nm}": (lambda K, i=i: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba, impl=i))
+           for nm, i in (("f32", 1), ("x3", 2))},
+        **{f"gemm_fwd_512#{nm}": (lambda K, i=i: K.gemm(0, 0, n, 512, 512, x, W, dh, impl=i))
+           for nm, i in (("f32", 1), ("x3", 2))},
+        **{f"gemm_dx_densea#{nm}": (lambda K, i=i: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa, impl=i))
+           for nm, i in (("f32", 1), ("x3", 2))},
+        **{f"gemm_dw_512x512#{nm}": (lambda K, i=i: hicgat.ops.weight_grad(K, dh, x, impl=i))
+           for nm, i in (("f32", 1), ("x3", 2))},
+        **{f"gemm_dw_densea#{nm}": (lambda K, i=i: hicgat.ops.weight_grad(K, ya, out, impl=i))
+           for nm, i in (("f32", 1), ("x3", 2))},
         "torch_dw_densea": lambda K: ya.t().mm(out),
         "torch_fwd_densea": lambda K: torch.nn.functional.linear(out, Wa, ba),
     }
@@ -107,9 +134,10 @@ def main():
                 res.setdefault((lname, jname), []).append(e0.elapsed_time(e1) / a.reps)
     for (lname, jname), ts in res.items():
         alg = ""
-        if jname in ("gat_agg_fwd", "gat_agg_fwd_train", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src",
-                     "pairdist_mse_fused", "pairdist_combined"):
-            kb = {"pairdist_combined": "pairdist_mse_fused", "gat_agg_fwd_train": "gat_agg_fwd"}.get(jname, jname)
+        base = jname.split("@")[0]
+        if base in ("gat_agg_fwd", "gat_agg_fwd_train", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src",
+                    "pairdist_mse_fused", "pairdist_combined"):
+            kb = {"pairdist_combined": "pairdist_mse_fused", "gat_agg_fwd_train": "gat_agg_fwd"}.get(base, base)
             alg = f"{bench.agg_bytes(kb, n, nnz) / (min(ts) * 1e-3) / 1e9:9.0f} GB/s alg"
         print(f"{lname:28s} {jname:22s} med {np.median(ts):8.4f} ms  min {min(ts):8.4f} ms  {alg}", flush=True)
 
