@@ -67,13 +67,13 @@ struct TileAcc {
 // bounds, i < j on the diagonal, the diagonal moment); interior tiles take MASK = false and do
 // no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
 // w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
-template <int MODE, bool VEC, bool PEARSON, bool MASK>
+template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1>
 __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int N, int I, int J,
                                           const float *tile, const float (*sc)[BT][3], int tx, int ty,
                                           const float *cx, const float *cy, const float *cz, const int *gj,
                                           float4 *__restrict__ prow, TileAcc &A) {
 #pragma unroll 1
-  for (int k = 0; k < 8; ++k) {
+  for (int k = K0; k < K1; ++k) {
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
     const int gi = I * BT + lr;
     const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
@@ -171,18 +171,6 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     J = (int)(t % nb);
   }
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, lane = tid & 63, wv = tid >> 6;
-  if (VEC) {
-    // LDS-DMA the whole T tile (global_load_lds_dwordx4: each wave instruction moves 1 KiB = two
-    // 512-B tile rows, wave-uniform LDS base + lane*16).  Rows past N are clamped to a valid row
-    // (their values are masked below); columns past N lie inside the padded leading dimension.
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int row = wv * 32 + q * 2 + (lane >> 5);
-      const int gi = min(I * BT + row, N - 1);
-      const float *src = T + (size_t)gi * ldt + (size_t)J * BT + (lane & 31) * 4;
-      __builtin_amdgcn_global_load_lds(src, &tile[(wv * 32 + q * 2) * BT], 16, 0, 0);
-    }
-  }
   for (int k = tid; k < 2 * BT; k += 256) {
     const int which = k / BT, li = k % BT;
     const int g = (which ? J : I) * BT + li;
@@ -196,8 +184,24 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     sc[which][li][1] = y;
     sc[which][li][2] = z;
   }
-  if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (VEC) {
+    // LDS-DMA of the T tile (global_load_lds_dwordx4: each wave instruction moves 1 KiB = two 512-B
+    // tile rows, wave-uniform LDS base + lane*16), each wave only the 32 rows its threads read:
+    // rows 16w .. 16w+15 (k = 0..3 of tile_rows) first, then 64+16w .. 64+16w+15 (k = 4..7), so the
+    // first half is computed while the second is in flight.  Rows past N are clamped to a valid row
+    // (their values are masked); columns past N lie inside the padded leading dimension.
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r0 = (q < 8 ? 0 : 64) + wv * 16 + (q & 7) * 2;
+      const int gi = min(I * BT + r0 + (lane >> 5), N - 1);
+      const float *src = T + (size_t)gi * ldt + (size_t)J * BT + (lane & 31) * 4;
+      __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
+    }
+  }
+  // sc[] (written above with ds_write) to all waves: LDS drain + raw barrier -- __syncthreads()
+  // would also drain vmcnt and so wait for the whole tile
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   float cx[8], cy[8], cz[8];
   int gj[8];
@@ -213,10 +217,16 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   }
   float4 *prow = part + (size_t)t * 2 * BT;
   const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
+  if (VEC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // this wave's first 16 rows landed
   if (interior)
-    tile_rows<MODE, VEC, PEARSON, false>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   else
-    tile_rows<MODE, VEC, PEARSON, true>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
+  if (interior)
+    tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  else
+    tile_rows<MODE, VEC, PEARSON, true, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
 #pragma unroll
