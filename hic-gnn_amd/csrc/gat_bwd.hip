@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
 // ---- GATConv parameter gradients: deterministic two-stage column reductions over N rows. ------
 // stage 1: block b sums rows [b*R, (b+1)*R) into part[b][3][D] (datt_src, datt_dst, dbias);
 // stage 2: one thread per output column sums the partials in block order.
-constexpr int kParamBlocks = 128;
+constexpr int kParamBlocks = 512;   // 2 blocks per CU (128 left half the CUs idle)
 
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
                                                          const float *__restrict__ dout,

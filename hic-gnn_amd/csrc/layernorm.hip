@@ -14,7 +14,7 @@
 
 namespace hicgat {
 
-constexpr int kLnWaves = 1024;  // waves of the backward grid (partials: kLnWaves x 2 x W)
+constexpr int kLnWaves = 4096;  // waves of the backward grid (partials: kLnWaves x 2 x W; 4 blocks per CU)
 
 template <int W>
 __global__ __launch_bounds__(256) void ln_relu_res_fwd_kernel(const float *__restrict__ y, int64_t ldy, int M,

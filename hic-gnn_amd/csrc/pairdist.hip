@@ -319,28 +319,39 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
   }
 }
 
-// stats[0..6] = sum over tiles [t0,t1) of the tile moments (fixed order, fp64).
-__global__ __launch_bounds__(1024) void moments_reduce_kernel(const double *__restrict__ mom,
-                                                              int64_t t0, int64_t t1,
-                                                              double *__restrict__ stats) {
-  __shared__ double red[7][1024];
+// stats[0..6] = sum over tiles [t0,t1) of the tile moments (fp64, fixed order): kMomBlocks blocks
+// each sum a contiguous tile range (tree over 256 threads), one block adds the block sums in order.
+constexpr int kMomBlocks = 64;
+
+__global__ __launch_bounds__(256) void moments_partial_kernel(const double *__restrict__ mom, int64_t t0,
+                                                              int64_t t1, double *__restrict__ part) {
+  __shared__ double red[7][256];
+  const int64_t per = (t1 - t0 + kMomBlocks - 1) / kMomBlocks;
+  const int64_t b0 = t0 + (int64_t)blockIdx.x * per, b1 = min(t1, b0 + per);
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += 1024) {
+  for (int64_t t = b0 + threadIdx.x; t < b1; t += 256) {
 #pragma unroll
     for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
   }
 #pragma unroll
   for (int c = 0; c < 7; ++c) red[c][threadIdx.x] = s[c];
   __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
+  for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
 #pragma unroll
       for (int c = 0; c < 7; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + o];
     }
     __syncthreads();
   }
-  if (threadIdx.x < 7) stats[threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x < 7) part[blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(64) void moments_final_kernel(const double *__restrict__ part,
+                                                           double *__restrict__ stats) {
+  if (threadIdx.x >= 7) return;
+  double s = 0.0;
+  for (int b = 0; b < kMomBlocks; ++b) s += part[b * 8 + threadIdx.x];
+  stats[threadIdx.x] = s;
 }
 
 // stats[7..10] and loss from the all-reduced moments stats[0..6]: mse, pearson r, alpha, total.
@@ -395,7 +406,7 @@ extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
   // mode 1 (fused, triangular tiles) and mode 0 (backward, square tiles) of the public API.
   const int64_t tiles = hicgat_pairdist_num_tiles(N, mode == 1 ? MODE_SYM : MODE_FULL);
-  return (size_t)tiles * (2 * BT * sizeof(float4) + 8 * sizeof(double)) + 256;
+  return (size_t)tiles * (2 * BT * sizeof(float4) + 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) + 256;
 }
 
 static void carve(void *ws, int64_t tiles, float4 **part, double **mom) {
@@ -485,8 +496,11 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
                        scale, dcoords);
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(moments_reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mom,
-                     tile_begin, tile_end, stats);
+  double *mpart = mom + (size_t)tiles * 8;
+  hipLaunchKernelGGL(moments_partial_kernel, dim3(kMomBlocks), dim3(256), 0, (hipStream_t)stream, mom,
+                     tile_begin, tile_end, mpart);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, stats);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
                      stats, loss);

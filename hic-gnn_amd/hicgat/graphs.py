@@ -20,7 +20,9 @@ class CapturedStep:
                 fn()
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: only this thread is in capture mode, so a concurrent thread's legal stream
+        # queries (the RCCL process group's watchdog polls its work events) do not invalidate it
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = fn()
         self.fn = fn
 
