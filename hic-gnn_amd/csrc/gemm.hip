@@ -22,7 +22,10 @@ namespace hicgat {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int GK = 16;  // K-step
+#ifndef HICGAT_GK
+#define HICGAT_GK 16
+#endif
+constexpr int GK = HICGAT_GK;  // K-step of the fp32 kernel
 
 template <int BM, int BN, bool A_KM, bool B_KM, bool VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, int64_t lda,

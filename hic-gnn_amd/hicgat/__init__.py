@@ -11,9 +11,10 @@ Drop-in surface of the reference (beyzoskaya/HiC-GNN):
   hicgat.metrics.dscc, hicgat.io.write_pdb    ~ HiC-GNN_main.py:135-139, utils.WritePDB
   hicgat.kr.KRnorm                            ~ r_utils.R:1-93 (normalize.R)
   hicgat.align.domain_alignment / generalize  ~ utils.py:83-109, HiC_GAT_generalize_directly.py:312-336
+  hicgat.embed.node2vec                       ~ Node2Vec(...).fit(...) at HiC_GAT_generalize_directly.py:150-155
 Compute runs in libhicgat.so (include/hicgat.h); there is no CPU fallback.
 """
-from . import _lib, align, dist, graph, graphs, io, kernels, kr, metrics, nn, ops, optim, synth, train  # noqa: F401
+from . import _lib, align, dist, embed, graph, graphs, io, kernels, kr, metrics, nn, ops, optim, synth, train  # noqa: F401
 from .gat_models import (GATNetHeadsChanged3LayersLeakyReLUv2,  # noqa: F401
                          GATNetSelectiveResidualsUpdated, MODELS, Net)
 from .graph import Adj, Data, Truth, cont2dist, convert_to_matrix, load_input  # noqa: F401

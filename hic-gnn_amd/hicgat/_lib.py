@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("HICGAT_LIB", os.path.join(_HERE, "libhicgat.so"))
 
 c_int, c_i64, c_f, c_d, c_sz, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double,
                                      ctypes.c_size_t, ctypes.c_void_p)
+c_u64 = ctypes.c_uint64
 
 # name -> (restype, argtypes); mirrors include/hicgat.h one to one
 SIGNATURES = {
@@ -69,6 +70,9 @@ SIGNATURES = {
                                 c_p]),
     "hicgat_kr_matvec": (c_int, [c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_kr_scale": (c_int, [c_p, c_i64, c_int, c_p, c_p, c_i64, c_p]),
+    "hicgat_n2v_walks": (c_int, [c_p, c_p, c_p, c_int, c_p, c_int, c_int, c_f, c_f, c_u64, c_p, c_p]),
+    "hicgat_n2v_sgns_epoch": (c_int, [c_p, c_int, c_int, c_p, c_p, c_int, c_int, c_int, c_int, c_f, c_f, c_int,
+                                      c_int, c_u64, c_int, c_p, c_p, c_p]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
 }

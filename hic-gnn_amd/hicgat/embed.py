@@ -1,0 +1,111 @@
+"""node2vec embeddings on the GPU.
+
+Reference call (HiC_GAT_generalize_directly.py:150-155; the same at evaluate_combined_loss.py:78 and
+HiC-GNN_node2vec_conversion.py:118 with other p / q / walk lengths):
+
+    G = nx.from_numpy_matrix(matrix)
+    Node2Vec(G, dimensions=512, walk_length=150, num_walks=50, p=1.75, q=0.4, workers=1, seed=42)
+        .fit(window=25, min_count=1, batch_words=4)      # gensim Word2Vec, sg=1
+    embeddings = [model.wv[str(node)] for node in G.nodes()]
+
+``node2vec(matrix, ...)`` returns the [N, dimensions] embedding matrix in node order.  The walks
+(``hicgat_n2v_walks``) and the skip-gram epochs (``hicgat_n2v_sgns_epoch``) run in libhicgat.so;
+the host builds the weighted CSR (networkx's edge / weight rule) and gensim's vocabulary tables
+(downsampling keep probabilities, unigram^0.75 negative-sampling table) from the walk counts.
+Differences from the reference, by construction: the random streams (a counter-based RNG instead of
+Python's / numpy's), the initial vectors (same distribution, U(-0.5/D, 0.5/D)) and the Hogwild
+update order -- node2vec output is stochastic, so no two implementations agree bit for bit.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+P = _lib.ptr
+
+
+def graph_csr(A):
+    """Sorted CSR (rowptr, col, weight) of ``networkx.from_numpy_matrix(A)``: edge {i, j} when
+    A[i, j] or A[j, i] is non-zero (self loops included), weight A[max, min] if non-zero else
+    A[min, max] (the undirected Graph keeps the later assignment); NaN entries are no edge."""
+    A = np.nan_to_num(np.asarray(A, dtype=np.float64), nan=0.0)
+    n = A.shape[0]
+    lo = np.tril(A, -1)
+    wl = np.where(lo != 0, lo, np.triu(A, 1).T)
+    W = wl + wl.T + np.diag(np.diag(A))
+    rows, cols = np.nonzero(W)
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    return np.cumsum(rowptr), cols.astype(np.int64), W[rows, cols]
+
+
+def random_walks(A, num_walks=50, walk_length=150, p=1.75, q=0.4, seed=42, device="cuda"):
+    """[num_walks * N, walk_length] int32 walks (-1 padded): num_walks rounds, each starting one walk
+    from every node in a shuffled order (node2vec's ``_generate_walks``)."""
+    lib = _lib.lib()
+    rowptr, col, w = graph_csr(A)
+    n = len(rowptr) - 1
+    # inclusive per-row cumulative weights (float64 prefix sums, stored as float32)
+    cs = np.cumsum(w)
+    base = np.repeat(np.concatenate([[0.0], cs])[rowptr[:-1]], np.diff(rowptr))
+    cumw = (cs - base).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    starts = np.concatenate([rng.permutation(n) for _ in range(num_walks)]).astype(np.int32)
+    dev = torch.device(device)
+    t_rowptr = torch.tensor(rowptr, dtype=torch.int32, device=dev)
+    t_col = torch.tensor(col, dtype=torch.int32, device=dev)
+    t_cumw = torch.tensor(cumw if len(cumw) else np.zeros(1, np.float32), device=dev)
+    t_starts = torch.tensor(starts, device=dev)
+    walks = torch.empty((len(starts), walk_length), dtype=torch.int32, device=dev)
+    _lib.check(lib.hicgat_n2v_walks(P(t_rowptr), P(t_col), P(t_cumw), n, P(t_starts), len(starts), walk_length,
+                                    float(p), float(q), int(seed) & (2 ** 64 - 1), P(walks), _lib.stream(dev)),
+               "hicgat_n2v_walks")
+    return walks
+
+
+def vocab_tables(counts, sample=1e-3, ns_exponent=0.75):
+    """gensim 4 ``prepare_vocab`` keep probabilities and ``make_cum_table`` (domain 2^31 - 1)."""
+    counts = np.asarray(counts, dtype=np.float64)
+    thr = sample * counts.sum()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        keep = np.where(counts > 0, np.minimum((np.sqrt(counts / thr) + 1.0) * (thr / counts), 1.0), 0.0)
+    pw = counts ** ns_exponent
+    cum = np.round(np.cumsum(pw) / pw.sum() * (2 ** 31 - 1)).astype(np.uint32)
+    return keep.astype(np.float32), cum
+
+
+def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, alpha=0.025, min_alpha=1e-4,
+             sample=1e-3, seed=42, max_waves=None):
+    """Word2Vec(sg=1, hs=0) over the walks: returns the input vectors syn0 [n_words, dimensions].
+    ``max_waves`` bounds the walks trained concurrently (default n_words // 4, within [8, 4096]):
+    on a Hi-C-sized vocabulary (58 loci for chr19 1 mb) thousands of concurrent Hogwild writers
+    to the same rows would lose most updates."""
+    lib = _lib.lib()
+    dev = walks.device
+    nwalks, L = walks.shape
+    counts = torch.bincount(walks[walks >= 0].long(), minlength=n_words).cpu().numpy()
+    keep, cum = vocab_tables(counts, sample)
+    t_keep = torch.tensor(keep, device=dev)
+    t_cum = torch.tensor(cum.view(np.int32), device=dev)          # uint32 bits
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    syn0 = (torch.rand((n_words, dimensions), generator=g, device=dev) - 0.5) / dimensions
+    syn1 = torch.zeros_like(syn0)
+    st = _lib.stream(dev)
+    if max_waves is None:
+        max_waves = min(4096, max(8, n_words // 4))
+    for ep in range(epochs):
+        _lib.check(lib.hicgat_n2v_sgns_epoch(P(walks), nwalks, L, P(t_keep), P(t_cum), n_words, dimensions, window,
+                                             negative, float(alpha), float(min_alpha), ep, epochs,
+                                             int(seed) & (2 ** 64 - 1), int(max_waves), P(syn0), P(syn1), st),
+                   "hicgat_n2v_sgns_epoch")
+    return syn0
+
+
+def node2vec(matrix, dimensions=512, walk_length=150, num_walks=50, p=1.75, q=0.4, window=25, epochs=5,
+             negative=5, alpha=0.025, min_alpha=1e-4, sample=1e-3, seed=42, device="cuda"):
+    """[N, dimensions] node2vec embeddings of ``matrix`` (node order), HiC_GAT_generalize_directly.py's
+    defaults."""
+    walks = random_walks(matrix, num_walks, walk_length, p, q, seed, device)
+    return skipgram(walks, np.asarray(matrix).shape[0], dimensions, window, epochs, negative, alpha, min_alpha,
+                    sample, seed)

@@ -5,6 +5,8 @@
 * ``fused_dist_loss`` -- cdist + MSELoss (+ Pearson / combined loss value) fused (a7-a9), D never
                          materialised; returns the loss scalar and keeps the fp64 stats.
 """
+import os
+
 import torch
 
 from . import _lib, kernels
@@ -97,9 +99,15 @@ class _GATConvFn(torch.autograd.Function):
         return (dx, dW, datt_l, datt_r, dbias, None, None, None, None)
 
 
-def _splits(m, n, k, target=1024):
+# target workgroups of a split-K weight-gradient GEMM (512 measured best at N = 20000: 0.094 vs
+# 0.108 ms for 512x512x20000 at 1024, fewer fp32 slabs to add; profiles/r01_kbench_x3_sliced.txt)
+_DW_BLOCKS = int(os.environ.get("HICGAT_DW_BLOCKS", "512"))
+
+
+def _splits(m, n, k, target=None):
     """K-split for a weight-gradient GEMM whose K is the node count: enough workgroups to fill
     the 256 CUs, each split at least 256 rows deep."""
+    target = _DW_BLOCKS if target is None else target
     bm = 128 if (m >= 128 and n >= 128) else 64
     tiles = -(-m // bm) * -(-n // bm)
     return max(1, min(k // 256, target // tiles))

@@ -254,6 +254,26 @@ int hicgat_kr_matvec(const double *A, int64_t lda, int n, const double *x, const
 int hicgat_kr_scale(const double *A, int64_t lda, int n, const double *x, double *out, int64_t ldo,
                     hicgat_stream_t stream);
 
+/* ---- f4: node2vec embeddings (HiC_GAT_generalize_directly.py:150-155: node2vec 0.4 + gensim 4
+ * Word2Vec, restated; see csrc/node2vec.hip).
+ * hicgat_n2v_walks: nwalks biased walks of walk_length nodes from starts[w] over the weighted CSR
+ *   (rows sorted, cum_weights[k] = inclusive per-row cumulative edge weight); second-order factors
+ *   1/p (back to the previous node), 1 (a neighbour of it), 1/q (otherwise), by rejection sampling
+ *   with a counter-based RNG (deterministic for a seed); a walk that reaches a node without
+ *   neighbours ends and is padded with -1.  walks [nwalks, walk_length] int32.
+ * hicgat_n2v_sgns_epoch: one skip-gram negative-sampling epoch over the walks (window, negative,
+ *   learning rate decaying linearly from alpha0 to alpha1 over `epochs`), gensim's downsampling
+ *   (keep_prob[v]) and unigram^0.75 negative table (cum_table[V], cumulative), syn0 / syn1 [V, D]
+ *   fp32 (D a multiple of 64, <= 1024; negative <= 7), updated Hogwild-style by at most max_waves walks in flight
+ *   (one wave per walk; a small vocabulary wants few, the reference trains with one worker). */
+int hicgat_n2v_walks(const int32_t *rowptr, const int32_t *col, const float *cum_weights, int N,
+                     const int32_t *starts, int nwalks, int walk_length, float p, float q, uint64_t seed,
+                     int32_t *walks, hicgat_stream_t stream);
+int hicgat_n2v_sgns_epoch(const int32_t *walks, int nwalks, int walk_length, const float *keep_prob,
+                          const uint32_t *cum_table, int V, int D, int window, int negative, float alpha0,
+                          float alpha1, int epoch, int epochs, uint64_t seed, int max_waves, float *syn0,
+                          float *syn1, hicgat_stream_t stream);
+
 /* ---- a10 (part): torch.optim.Adam step (HiC-GNN_main.py:118,130) over one flat fp32 buffer ----
  * Same arithmetic as torch's single-tensor CPU Adam (lerp / addcmul / addcdiv, no weight decay):
  *   m = fma(1-b1, g-m, m); v = fma((1-b2)*g, g, b2*v);

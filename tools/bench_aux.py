@@ -16,7 +16,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "hic-gnn_amd")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hic-gnn_amd"), os.path.join(ROOT, "tests")]
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -73,6 +73,27 @@ def main():
     hicgat.align.domain_alignment(l1, l2, e1, e2)
     torch.cuda.synchronize()
     res["procrustes"] = {"bins_1mb": 2000, "bins_500kb": 4000, "F": 512, "gpu_s": time.perf_counter() - t0}
+    # f4: node2vec with the reference's call (HiC_GAT_generalize_directly.py:153-154) on chr19 1 mb
+    # (the config-1 graph) and on a synthetic 2000-locus Hi-C matrix
+    from conftest import load_golden
+    from hicgat import embed, synth
+    n2v = {}
+    for name, mat in (("chr19_1mb", load_golden("graph_chr19_1mb.npz")["matrix"].copy()),
+                      ("synth2000_1pct", dense_contacts(2000, 0, device="cpu").numpy())):
+        embed.node2vec(mat[:32, :32], dimensions=64, walk_length=10, num_walks=2, epochs=1)   # warm up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        walks = embed.random_walks(mat)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        embed.skipgram(walks, mat.shape[0])
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        steps = int((walks >= 0).sum().item())
+        n2v[name] = {"n": int(mat.shape[0]), "walks": int(walks.shape[0]), "walk_steps": steps,
+                     "walks_s": t1 - t0, "skipgram_5_epochs_s": t2 - t1,
+                     "note": "dimensions 512, walk_length 150, num_walks 50, p 1.75, q 0.4, window 25, 5 epochs"}
+    res["node2vec"] = n2v
     print(json.dumps(res), flush=True)
 
 

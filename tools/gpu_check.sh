@@ -22,6 +22,8 @@ for s in $STAGES; do
     benchs) HICGAT_SLICE=${SLICE:-32} run bench_s${SLICE:-32} 600 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ;;
     benchx3) HICGAT_GEMM=auto run bench_x3 600 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ;;
     dscc) run dscc 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k dscc_chr19 -s -v --timeout 240 --timeout-method thread ;;
+    n2v) run n2v 300 python -u -m pytest tests/test_gpu_node2vec.py -m gpu -v -rf --timeout 180 --timeout-method thread ;;
+    aux) run bench_aux 300 python tools/bench_aux.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} ;;
     benche) run bench_eager 600 python bench.py --steps ${STEPS:-20} --warmup 3 --eager --no-cpu-baseline ;;
