@@ -57,7 +57,9 @@ def main(argv=None):
     p = argparse.ArgumentParser(description="Train a GAT-HiC model on the MI355X path "
                                             "(HiC-GNN_main.py flags).")
     p.add_argument("matrix", help="Hi-C list (bin_i bin_j count) or dense matrix text file")
-    p.add_argument("features", help="N x F embedding text file (np.loadtxt)")
+    p.add_argument("features", help="N x F embedding text file (np.loadtxt), or 'node2vec' to generate the "
+                                    "embeddings on the GPU from the contact matrix (hicgat.embed, the "
+                                    "HiC_GAT_generalize_directly.py:150-155 call)")
     p.add_argument("-c", "--conversions", default="[.5]", help="conversion factor list, '[a, step, b]' or '[f]'")
     p.add_argument("-lr", "--learningrate", type=float, default=1e-3)
     p.add_argument("-th", "--threshold", type=float, default=1e-8)
@@ -71,9 +73,13 @@ def main(argv=None):
     conv = ast.literal_eval(a.conversions)
     conv = list(np.arange(conv[0], conv[2], conv[1])) if len(conv) == 3 else [conv[0]]
     mat = np.loadtxt(a.matrix)
-    feats = np.loadtxt(a.features).astype(np.float32)
     if mat.shape[1] == 3:                       # HiC-GNN_main.py:75-78
         mat = graph.convert_to_matrix(mat)
+    if a.features == "node2vec":                # node2vec on the raw contact graph (:150-155)
+        from .embed import node2vec
+        feats = node2vec(mat, seed=a.seed if a.seed else 42).cpu().numpy()
+    else:
+        feats = np.loadtxt(a.features).astype(np.float32)
     np.fill_diagonal(mat, 0)                    # :80
     if not a.no_kr:                             # :85-89 (Rscript normalize.R -> r_utils.R KRnorm)
         from .kr import KRnorm
