@@ -148,6 +148,81 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
   }
 }
 
+// Interior tiles of the training loss (MODE_SYM, T from the LDS image, no masks) in packed fp32:
+// the thread's 8 columns as 4 float2 pairs, so the subtractions, multiplies and FMAs issue as
+// v_pk_{add,mul,fma}_f32 (two pairs per instruction); v_rsq stays scalar.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <bool PEARSON, int K0, int K1>
+__device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc)[BT][3], int tx, int ty,
+                                             const float *cx, const float *cy, const float *cz,
+                                             float4 *__restrict__ prow, TileAcc &A) {
+  f2 cx2[4], cy2[4], cz2[4], ax2[4], ay2[4], az2[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    cx2[h] = f2{cx[2 * h], cx[2 * h + 1]};
+    cy2[h] = f2{cy[2 * h], cy[2 * h + 1]};
+    cz2[h] = f2{cz[2 * h], cz[2 * h + 1]};
+    ax2[h] = f2{A.ax[2 * h], A.ax[2 * h + 1]};
+    ay2[h] = f2{A.ay[2 * h], A.ay[2 * h + 1]};
+    az2[h] = f2{A.az[2 * h], A.az[2 * h + 1]};
+  }
+  const f2 z2 = f2{0.f, 0.f};
+  f2 L2 = z2, sd2 = z2, sdd2 = z2, sdt2 = z2, st2 = z2, stt2 = z2;
+#pragma unroll 1
+  for (int k = K0; k < K1; ++k) {
+    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
+    const f2 rx = f2{sc[0][lr][0], sc[0][lr][0]}, ry = f2{sc[0][lr][1], sc[0][lr][1]},
+             rz = f2{sc[0][lr][2], sc[0][lr][2]};
+    const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
+    const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
+    const f2 tv[4] = {f2{a.x, a.y}, f2{a.z, a.w}, f2{b.x, b.y}, f2{b.z, b.w}};
+    f2 px = z2, py = z2, pz = z2;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const f2 dx = rx - cx2[h], dy = ry - cy2[h], dz = rz - cz2[h];
+      const f2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+      const f2 inv = f2{fminf(__builtin_amdgcn_rsqf(d2.x), 1e30f), fminf(__builtin_amdgcn_rsqf(d2.y), 1e30f)};
+      const f2 d = d2 * inv;
+      const f2 r = d - tv[h];
+      L2 = __builtin_elementwise_fma(r, r, L2);
+      if (PEARSON) {
+        sd2 += d;
+        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
+        sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
+        st2 += tv[h];
+        stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
+      }
+      const f2 w = r * inv;
+      px = __builtin_elementwise_fma(w, dx, px);
+      py = __builtin_elementwise_fma(w, dy, py);
+      pz = __builtin_elementwise_fma(w, dz, pz);
+      ax2[h] = __builtin_elementwise_fma(-w, dx, ax2[h]);
+      ay2[h] = __builtin_elementwise_fma(-w, dy, ay2[h]);
+      az2[h] = __builtin_elementwise_fma(-w, dz, az2[h]);
+    }
+    const float sx = sum16(px.x + px.y), sy = sum16(py.x + py.y), sz = sum16(pz.x + pz.y);
+    if (tx == 0) prow[lr] = make_float4(sx, sy, sz, 0.f);
+  }
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    A.ax[2 * h] = ax2[h].x;
+    A.ax[2 * h + 1] = ax2[h].y;
+    A.ay[2 * h] = ay2[h].x;
+    A.ay[2 * h + 1] = ay2[h].y;
+    A.az[2 * h] = az2[h].x;
+    A.az[2 * h + 1] = az2[h].y;
+  }
+  A.L += L2.x + L2.y;
+  if (PEARSON) {
+    A.sd += sd2.x + sd2.y;
+    A.sdd += sdd2.x + sdd2.y;
+    A.sdt += sdt2.x + sdt2.y;
+    A.st += st2.x + st2.y;
+    A.stt += stt2.x + stt2.y;
+  }
+}
+
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
 // PEARSON: also the d / t moments of the Pearson term (combined loss only).
@@ -218,15 +293,20 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   float4 *prow = part + (size_t)t * 2 * BT;
   const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
   if (VEC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // this wave's first 16 rows landed
-  if (interior)
-    tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
-  else
+  constexpr bool PK = VEC && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
+  if (interior) {
+    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4>(tile, sc, tx, ty, cx, cy, cz, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  } else {
     tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
-  if (interior)
-    tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
-  else
+  if (interior) {
+    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8>(tile, sc, tx, ty, cx, cy, cz, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  } else {
     tile_rows<MODE, VEC, PEARSON, true, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+  }
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
 #pragma unroll
