@@ -239,7 +239,10 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
 // ---- GATConv parameter gradients: deterministic two-stage column reductions over N rows. ------
 // stage 1: block b sums rows [b*R, (b+1)*R) into part[b][3][D] (datt_src, datt_dst, dbias);
 // stage 2: one thread per output column sums the partials in block order.
-constexpr int kParamBlocks = 512;   // 2 blocks per CU (128 left half the CUs idle)
+#ifndef HICGAT_PG_BLOCKS
+#define HICGAT_PG_BLOCKS 512    // 1024 measured slower (stage 2 sums twice the partials)
+#endif
+constexpr int kParamBlocks = HICGAT_PG_BLOCKS;   // row blocks of stage 1 (128 left half the CUs idle)
 
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
                                                          const float *__restrict__ dout,
@@ -255,6 +258,7 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
   for (int q = threadIdx.x; q < Q; q += blockDim.x) {
     const int hd = (4 * q) / C;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f), t = s, b = s;
+#pragma unroll 4   // several rows' loads in flight per thread (one wave per SIMD at this grid size)
     for (int n = r0; n < r1; ++n) {
       const float4 hv = h4[(size_t)n * Q + q], gv = g4[(size_t)n * Q + q];
       s = f4_fma(da_src[(size_t)n * H + hd], hv, s);
