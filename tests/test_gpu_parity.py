@@ -995,3 +995,28 @@ def test_dscc_chr19_1mb_within_north_star_band():
           f"{refs[8]:.6f} (noise floor {hi - lo:.2e}); distance to the oracle band "
           f"{max(0.0, lo - rho, rho - hi):.2e}")
     assert lo - 0.005 <= rho <= hi + 0.005, (rho, refs)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5])
+def test_gatconv_tiny_graphs_match_oracle(n):
+    """Degenerate inputs: a single node, nodes without any contact (rows = the self loop only),
+    fewer rows than a wave / a block -- forward and backward against the oracle."""
+    import hicgat
+    a = np.zeros((n, n))
+    if n >= 3:
+        a[0, 2] = a[2, 0] = 4.0
+    ref, mine = _gat_pair(seed=100 + n)
+    adj = hicgat.Adj.from_dense_device(torch.tensor(a, device=DEV))
+    rng = np.random.default_rng(n)
+    x = torch.tensor((0.1 * rng.standard_normal((n, 512))).astype(np.float32))
+    g = torch.tensor(rng.standard_normal((n, 512)).astype(np.float32))
+    xr = x.clone().requires_grad_(True)
+    out_r = ref(xr, (adj.storage.rowptr(), adj.storage.col()))
+    (out_r * g).sum().backward()
+    xm = x.to(DEV).requires_grad_(True)
+    out_m = mine(xm, adj)
+    (out_m * g.to(DEV)).sum().backward()
+    np.testing.assert_allclose(out_m.detach().cpu().numpy(), out_r.detach().numpy(), rtol=1e-5, atol=1e-6)
+    assert _rel(xm.grad.cpu(), xr.grad) < 1e-4
+    for (name, pr), (_, pm) in zip(ref.named_parameters(), mine.named_parameters()):
+        assert _rel(pm.grad.cpu(), pr.grad) < 1e-4 or pr.grad.abs().max() < 1e-30, name
