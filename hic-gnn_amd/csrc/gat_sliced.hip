@@ -138,17 +138,59 @@ __device__ __forceinline__ void strip_step(const long long *st, int k, int sub, 
   }
 }
 
-// The gather loop shared by the forward and the backward strip kernels: row i's records
-// [beg, end) of one head, 64 per LDS chunk; padded slots gather the (valid) own row with weight +0.
-template <int G, bool TRAIN>
-__device__ __forceinline__ void strip_rows(const long long *__restrict__ rh, int beg, int end, int i,
-                                           long long *st, int lane, int sub, const float4 *m4, int64_t ld4,
-                                           float ns, float4 &acc, float4 &acs) {
-  for (int base = beg; base < end; base += 64) {
-    const int e = base + lane;
-    st[lane] = e < end ? __builtin_nontemporal_load(rh + e) : (long long)(uint32_t)i;
+__device__ __forceinline__ float4 f4_xor_sum(float4 a, int o) {
+  a.x += __shfl_xor(a.x, o);
+  a.y += __shfl_xor(a.y, o);
+  a.z += __shfl_xor(a.z, o);
+  a.w += __shfl_xor(a.w, o);
+  return a;
+}
+
+#ifndef HICGAT_STRIP_RPW
+#define HICGAT_STRIP_RPW 4   // consecutive rows one strip wave walks (amortises the per-row latencies)
+#endif
+constexpr int kRPW = HICGAT_STRIP_RPW;
+
+// Block -> (strip, 4 waves x kRPW consecutive rows): XCD x = b & 7 walks strips x, x + 8, ... one
+// pass after the other.
+struct Strip {
+  int slice, row0;
+  __device__ Strip(int row_begin, int row_blocks) {
+    const int q = blockIdx.x >> 3;
+    slice = (blockIdx.x & 7) + 8 * (q / row_blocks);
+    row0 = row_begin + ((q % row_blocks) * 4 + wave_in_block()) * kRPW;
+  }
+};
+
+// The gather loop shared by the forward and the backward strip kernels: rows row0 .. row0+kRPW-1
+// (< row_end) of one head's records, 64 records per LDS chunk; the NEXT chunk's records (possibly
+// the next row's) are loaded while the current chunk is gathered, so a record round trip is paid
+// once per wave, not once per chunk.  Padded slots gather the (valid) own row with weight +0.
+// finish(i, acc, acs) runs when row i is complete.
+template <int G, bool TRAIN, typename Finish>
+__device__ __forceinline__ void strip_wave(const int *__restrict__ rowptr, const long long *__restrict__ rh,
+                                           int row0, int row_end, long long *st, int lane, int sub,
+                                           const float4 *m4, int64_t ld4, float ns, Finish finish) {
+  const int rlast = min(row_end, row0 + kRPW);
+  int i = row0, end = rowptr[i + 1], base = rowptr[i];
+  long long pre = base + lane < end ? __builtin_nontemporal_load(rh + base + lane) : (long long)(uint32_t)i;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc = z4, acs = z4;
+  while (true) {
+    st[lane] = pre;
     __builtin_amdgcn_wave_barrier();
     const int cnt = min(64, end - base);
+    // the next chunk: the rest of this row, else the next row of the wave
+    int ni = i, nbase = base + 64, nend = end;
+    const bool row_done = nbase >= end;
+    if (row_done) {
+      ni = i + 1;
+      if (ni < rlast) {
+        nbase = rowptr[ni];
+        nend = rowptr[ni + 1];
+      }
+    }
+    if (ni < rlast) pre = nbase + lane < nend ? __builtin_nontemporal_load(rh + nbase + lane) : (long long)(uint32_t)ni;
     int k = 0;
     while (k < cnt) {   // the widest step the remaining records fill at least half of
       const int r = cnt - k;
@@ -167,26 +209,17 @@ __device__ __forceinline__ void strip_rows(const long long *__restrict__ rh, int
       }
     }
     __builtin_amdgcn_wave_barrier();
+    if (row_done) {
+      finish(i, acc, acs);
+      acc = z4;
+      acs = z4;
+      if (ni >= rlast) break;
+    }
+    i = ni;
+    base = nbase;
+    end = nend;
   }
 }
-
-__device__ __forceinline__ float4 f4_xor_sum(float4 a, int o) {
-  a.x += __shfl_xor(a.x, o);
-  a.y += __shfl_xor(a.y, o);
-  a.z += __shfl_xor(a.z, o);
-  a.w += __shfl_xor(a.w, o);
-  return a;
-}
-
-// Block -> (strip, 4 rows): XCD x = b & 7 walks strips x, x + 8, ... one pass after the other.
-struct Strip {
-  int slice, row;
-  __device__ Strip(int row_begin, int row_blocks) {
-    const int q = blockIdx.x >> 3;
-    slice = (blockIdx.x & 7) + 8 * (q / row_blocks);
-    row = row_begin + (q % row_blocks) * 4 + wave_in_block();
-  }
-};
 
 template <int SW, bool TRAIN, int ACT>
 __global__ __launch_bounds__(256) void agg_fwd_strip_kernel(const int *__restrict__ rowptr, int row_begin,
@@ -198,26 +231,24 @@ __global__ __launch_bounds__(256) void agg_fwd_strip_kernel(const int *__restric
   constexpr int L = SW / 4, G = 64 / L;
   __shared__ long long stage[4][64];
   const Strip s(row_begin, row_blocks);
-  const int i = s.row;
-  if (i >= row_end) return;
+  if (s.row0 >= row_end) return;
   const int lane = lane_id(), sub = lane / L, c4 = s.slice * L + lane % L;
   const long long *rh = reinterpret_cast<const long long *>(rec) + (size_t)((s.slice * SW) >> 8) * nnz;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 acc = z4, acs = z4;
-  strip_rows<G, TRAIN>(rh, rowptr[i], rowptr[i + 1], i, stage[wave_in_block()], lane, sub,
-                       reinterpret_cast<const float4 *>(h) + c4, 128, ns, acc, acs);
+  const float4 b = reinterpret_cast<const float4 *>(bias)[c4];
+  strip_wave<G, TRAIN>(rowptr, rh, s.row0, row_end, stage[wave_in_block()], lane, sub,
+                       reinterpret_cast<const float4 *>(h) + c4, 128, ns, [&](int i, float4 acc, float4 acs) {
 #pragma unroll
-  for (int o = L; o < 64; o <<= 1) {
-    acc = f4_xor_sum(acc, o);
-    if (TRAIN) acs = f4_xor_sum(acs, o);
-  }
-  if (sub == 0) {
-    const float4 b = reinterpret_cast<const float4 *>(bias)[c4];
-    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
-    if (ACT == 1) acc = f4_relu(acc);
-    reinterpret_cast<float4 *>(out)[(size_t)i * 128 + c4] = acc;
-    if (TRAIN) reinterpret_cast<float4 *>(out2)[(size_t)i * 128 + c4] = acs;
-  }
+    for (int o = L; o < 64; o <<= 1) {
+      acc = f4_xor_sum(acc, o);
+      if (TRAIN) acs = f4_xor_sum(acs, o);
+    }
+    if (sub == 0) {
+      acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+      if (ACT == 1) acc = f4_relu(acc);
+      reinterpret_cast<float4 *>(out)[(size_t)i * 128 + c4] = acc;
+      if (TRAIN) reinterpret_cast<float4 *>(out2)[(size_t)i * 128 + c4] = acs;
+    }
+  });
 }
 
 // dh[r, strip] = sum_i alpha_ir dout_i[strip] and part[r][strip] = <sum_i alpha_ir lrelu'_ir dout_i, h_r>
@@ -233,19 +264,18 @@ __global__ __launch_bounds__(256) void agg_bwd_src_strip_kernel(const int *__res
   constexpr int L = SW / 4, G = 64 / L, NS = 512 / SW;
   __shared__ long long stage[4][64];
   const Strip s(row_begin, row_blocks);
-  const int r = s.row;
-  if (r >= row_end) return;
+  if (s.row0 >= row_end) return;
   const int lane = lane_id(), sub = lane / L, c4 = s.slice * L + lane % L;
   const long long *rh = reinterpret_cast<const long long *>(rec) + (size_t)((s.slice * SW) >> 8) * nnz;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 acc = z4, cc = z4;
-  strip_rows<G, true>(rh, rowptr[r], rowptr[r + 1], r, stage[wave_in_block()], lane, sub,
-                      reinterpret_cast<const float4 *>(dout) + c4, ld4, ns, acc, cc);
-  const float d = wave_sum(f4_dot(cc, reinterpret_cast<const float4 *>(h)[(size_t)r * 128 + c4]));
+  const int slice = s.slice;
+  strip_wave<G, true>(rowptr, rh, s.row0, row_end, stage[wave_in_block()], lane, sub,
+                      reinterpret_cast<const float4 *>(dout) + c4, ld4, ns, [&](int r, float4 acc, float4 cc) {
+    const float d = wave_sum(f4_dot(cc, reinterpret_cast<const float4 *>(h)[(size_t)r * 128 + c4]));
 #pragma unroll
-  for (int o = L; o < 64; o <<= 1) acc = f4_xor_sum(acc, o);
-  if (sub == 0) reinterpret_cast<float4 *>(dh)[(size_t)r * 128 + c4] = acc;
-  if (lane == 0) part[(size_t)r * NS + s.slice] = d;
+    for (int o = L; o < 64; o <<= 1) acc = f4_xor_sum(acc, o);
+    if (sub == 0) reinterpret_cast<float4 *>(dh)[(size_t)r * 128 + c4] = acc;
+    if (lane == 0) part[(size_t)r * NS + slice] = d;
+  });
 }
 
 // da_src[r,h] = (sum of head h's strip shares) - sb[r,h];  dh_r += da_src (x) att_src + da_dst (x) att_dst.
@@ -311,6 +341,7 @@ extern "C" int hicgat_gat_agg_fwd_sliced(const int32_t *rowptr, const int32_t *c
     return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_gat_sliced_workspace_bytes(N, nnz, H, slice_width)) return HICGAT_EINVAL;
   const int rb = (row_end - row_begin + 3) / 4;
+  const int sb = (row_end - row_begin + 4 * kRPW - 1) / (4 * kRPW);   // strip row blocks
   hipStream_t s = (hipStream_t)stream;
   int2 *rec = static_cast<int2 *>(workspace);
   if (out2)
@@ -320,10 +351,10 @@ extern "C" int hicgat_gat_agg_fwd_sliced(const int32_t *rowptr, const int32_t *c
     hipLaunchKernelGGL(agg_edge_rec_kernel<false>, dim3(rb), dim3(256), 0, s, rowptr, col, row_begin, row_end,
                        nnz, a_src, a_dst, neg_slope, rec, row_stats);
   HICGAT_CHECK_LAUNCH();
-  const dim3 grid((512 / slice_width) * rb), block(256);
+  const dim3 grid((512 / slice_width) * sb), block(256);
 #define HICGAT_STRIP(SW, TR, AC)                                                                     \
   hipLaunchKernelGGL((agg_fwd_strip_kernel<SW, TR, AC>), grid, block, 0, s, rowptr, row_begin, row_end, \
-                     nnz, rb, rec, h, bias, neg_slope, out, out2)
+                     nnz, sb, rec, h, bias, neg_slope, out, out2)
 #define HICGAT_STRIP_W(SW)                   \
   do {                                       \
     if (out2) {                              \
@@ -359,21 +390,22 @@ extern "C" int hicgat_gat_agg_bwd_src_sliced(const int32_t *rowptr, const int32_
     return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_gat_sliced_workspace_bytes(N, nnz, H, slice_width)) return HICGAT_EINVAL;
   const int rb = (row_end - row_begin + 3) / 4;
+  const int sb = (row_end - row_begin + 4 * kRPW - 1) / (4 * kRPW);   // strip row blocks
   hipStream_t s = (hipStream_t)stream;
   int2 *rec = static_cast<int2 *>(workspace);
   float *part = reinterpret_cast<float *>(static_cast<char *>(workspace) + rec_bytes(nnz, H));
   hipLaunchKernelGGL(agg_src_rec_kernel, dim3(rb), dim3(256), 0, s, rowptr, col, row_begin, row_end, nnz, a_src,
                      a_dst, row_stats, ld_stats, neg_slope, rec, da_src);
   HICGAT_CHECK_LAUNCH();
-  const dim3 grid((512 / slice_width) * rb), block(256);
+  const dim3 grid((512 / slice_width) * sb), block(256);
   if (slice_width == 32) {
-    hipLaunchKernelGGL(agg_bwd_src_strip_kernel<32>, grid, block, 0, s, rowptr, row_begin, row_end, nnz, rb, rec,
+    hipLaunchKernelGGL(agg_bwd_src_strip_kernel<32>, grid, block, 0, s, rowptr, row_begin, row_end, nnz, sb, rec,
                        h, dout, ld_dout / 4, neg_slope, dh, part);
     HICGAT_CHECK_LAUNCH();
     hipLaunchKernelGGL(agg_src_finalize_kernel<16>, dim3(rb), block, 0, s, row_begin, row_end, part, row_stats,
                        ld_stats, att_src, att_dst, dh, da_src);
   } else {
-    hipLaunchKernelGGL(agg_bwd_src_strip_kernel<64>, grid, block, 0, s, rowptr, row_begin, row_end, nnz, rb, rec,
+    hipLaunchKernelGGL(agg_bwd_src_strip_kernel<64>, grid, block, 0, s, rowptr, row_begin, row_end, nnz, sb, rec,
                        h, dout, ld_dout / 4, neg_slope, dh, part);
     HICGAT_CHECK_LAUNCH();
     hipLaunchKernelGGL(agg_src_finalize_kernel<8>, dim3(rb), block, 0, s, row_begin, row_end, part, row_stats,
