@@ -245,6 +245,7 @@ def main():
         b = agg_bytes(k, n if k == "pairdist_mse_fused" else n_loc, nnz)
         kern[k]["alg_GBps"] = b / (kern[k]["avg_ms"] * 1e-3) / 1e9
 
+    traffic = pmc_traffic(dom, args.workload) if world == 1 else None
     result = {
         "metric": "training steps/sec (GATNetSelectiveResidualsUpdated, fwd+loss+bwd+Adam)",
         "value": args.steps / elapsed,
@@ -268,8 +269,12 @@ def main():
         "final_loss": loss_v,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(dom, args.workload) if world == 1 else None,
-                     "alg_bytes_per_launch": alg, "avg_launch_ms": kern[dom]["avg_ms"]},
+                     "traffic": traffic,
+                     "alg_bytes_per_launch": alg, "avg_launch_ms": kern[dom]["avg_ms"],
+                     # the HBM bytes the kernel really moves (PMC) over the same launch time: frac > 1
+                     # above because the gathered rows are largely L2 / Infinity-Cache hits
+                     "traffic_GBps": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 if traffic else None,
+                     "traffic_frac": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None},
         "kernels": kern,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

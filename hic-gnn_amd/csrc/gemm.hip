@@ -461,7 +461,10 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
   if (impl == HICGAT_GEMM_X3) return HICGAT_EUNSUPPORTED;
   // tall row-major problems (M = node rows): 64 x 128 tiles keep >= 2 blocks per CU in flight;
   // square-ish weight gradients (M, N = features, K = rows split): 128 x 128
-  if (M >= 128 && N >= 128 && M <= 1024)
+#ifndef HICGAT_GEMM_TALL128
+#define HICGAT_GEMM_TALL128 0   // 1: 128 x 128 tiles for the tall (M = node rows) problems too
+#endif
+  if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
     return launch<128, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   if (N >= 128) return launch<64, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   return launch<64, 64, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
