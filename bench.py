@@ -54,10 +54,11 @@ def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
 
 # timer name (kernels.py) -> HIP kernels launched inside that timed region
 PMC_KERNELS = {
-    "gat_agg_fwd": ["agg_fwd_h2c256_kernel"],
+    "gat_agg_fwd": ["agg_fwd_h2c256_kernel", "agg_edge_rec_kernel", "agg_fwd_strip_kernel"],
     "gat_agg_bwd_dst": ["agg_bwd_dst_h2c256_kernel"],
     "gat_agg_bwd_rows": ["agg_bwd_rows_kernel"],
-    "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel"],
+    "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel", "agg_src_rec_kernel", "agg_bwd_src_strip_kernel",
+                        "agg_src_finalize_kernel"],
     "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_reduce_kernel", "moments_reduce_kernel"],
 }
 
