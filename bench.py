@@ -45,6 +45,8 @@ def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
         return nnz * (4 * d + 4 + 4 * h) + n * 4 * d + (n + 1) * 4 + 5 * n * h * 4
     if kind == "gat_agg_bwd_src":  # gather dout_i + col + (a_dst, max, sum, delta)_i, read h_r, write dh_r
         return nnz * (4 * d + 4 + 16 * h) + 2 * n * 4 * d + (n + 1) * 4 + 4 * n * h * 4
+    if kind == "sage_agg":          # f1 SAGEConv: gather x_j (4d) + col + weight per edge, read x_i (trunc), write z [N, 2d]
+        return nnz * (4 * d + 8) + n * 4 * d + n * 8 * d + (n + 1) * 4 + n * 4
     if kind == "pairdist_mse_fused":  # upper-triangle tiles of T once + partial slabs
         nb = (n + 127) // 128
         tiles = nb * (nb + 1) // 2
@@ -57,6 +59,7 @@ PMC_KERNELS = {
     "gat_agg_fwd": ["agg_fwd_h2c256_kernel", "agg_edge_rec_kernel", "agg_fwd_strip_kernel"],
     "gat_agg_bwd_dst": ["agg_bwd_dst_h2c256_kernel"],
     "gat_agg_bwd_rows": ["agg_bwd_rows_kernel"],
+    "sage_agg": ["sage_agg_f512_kernel", "sage_agg_generic_kernel"],
     "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel", "agg_src_rec_kernel", "agg_bwd_src_strip_kernel",
                         "agg_src_finalize_kernel"],
     "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_reduce_kernel", "moments_reduce_kernel"],
@@ -147,6 +150,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="synth-20000", choices=["synth-20000", "synth-2000"])
     ap.add_argument("--loss", default="mse", choices=["mse", "combined"])
+    ap.add_argument("--model", default="GATNetSelectiveResidualsUpdated",
+                    choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
+                    help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
+                         "N > 1 shards the GAT models only")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -173,7 +180,9 @@ def main():
 
     wl = build_workload(args.workload, args.seed, dev)
     torch.manual_seed(0)
-    model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
+    model = hicgat.MODELS[args.model]().to(dev)
+    if world > 1 and args.model == "Net":
+        raise SystemExit("the sharded step covers the GAT models (Net is the single-GPU f1 baseline)")
     if world > 1:
         from hicgat import dist as hdist
         runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss)
@@ -234,8 +243,8 @@ def main():
         n_loc = runner.local_rows
     else:
         n_loc = n
-    cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "pairdist_mse_fused")
-             if k in kern]
+    cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "sage_agg",
+                         "pairdist_mse_fused") if k in kern]
     dom = max(cands, key=lambda k: kern[k]["total_ms"])
     if dom == "pairdist_mse_fused":
         alg = agg_bytes(dom, n, nnz) / (world if world > 1 else 1)
@@ -248,7 +257,7 @@ def main():
 
     traffic = pmc_traffic(dom, args.workload) if world == 1 else None
     result = {
-        "metric": "training steps/sec (GATNetSelectiveResidualsUpdated, fwd+loss+bwd+Adam)",
+        "metric": f"training steps/sec ({args.model}, fwd+loss+bwd+Adam)",
         "value": args.steps / elapsed,
         "unit": "steps/s",
         "n_gpus": world,
@@ -261,7 +270,7 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
         "graph": bool(args.graph),
-        "config": {"workload": args.workload, "model": "GATNetSelectiveResidualsUpdated",
+        "config": {"workload": args.workload, "model": args.model,
                    "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz, "d": D_FEAT, "heads": HEADS,
                    "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single",
                    "gemm": {0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl],
@@ -278,7 +287,7 @@ def main():
                      "traffic_frac": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None},
         "kernels": kern,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "GATNetSelectiveResidualsUpdated":
         log("[bench] cpu baseline (oracle) ...")
         result["cpu_baseline"] = cpu_baseline(wl, args.seed, steps=args.cpu_steps)
     if rank == 0:
