@@ -196,7 +196,14 @@ def main():
 
     eager_step = step
     if args.graph and world > 1:
-        step = runner.captured(warmup=max(1, args.warmup))   # kernels + RCCL collectives in one graph
+        try:
+            step = runner.captured(warmup=max(1, args.warmup))   # kernels + RCCL collectives in one graph
+        except RuntimeError as exc:   # keep a number on record: eager RCCL steps instead of the graph
+            log(f"[bench] rank {rank}: graph capture of the sharded step failed ({exc}); timing eager steps")
+            torch.cuda.synchronize()
+            args.graph = False
+            for w in range(args.warmup):
+                step()
     elif args.graph:
         step = hicgat.graphs.captured_train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss,
                                                  warmup=max(1, args.warmup))
