@@ -27,7 +27,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 constexpr int GK = HICGAT_GK;  // K-step of the fp32 kernel
 
-template <int BM, int BN, bool A_KM, bool B_KM, bool VEC>
+template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB>
 __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, int64_t lda,
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
@@ -39,8 +39,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, 
   constexpr int AE = VEC ? BM * GK / 1024 : BM * GK / 256;
   constexpr int BE = VEC ? BN * GK / 1024 : BN * GK / 256;
   constexpr int W = VEC ? 4 : 1;
-  __shared__ __attribute__((aligned(16))) float As[GK][BM + 4];
-  __shared__ __attribute__((aligned(16))) float Bs[GK][BN + 4];
+  // DB: double-buffered LDS, one barrier per K-step instead of two (it doubles the LDS footprint;
+  // measured faster only for the input-gradient layout, profiles/r01_kbench_x3_sliced.txt)
+  constexpr int NB = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) float As[NB][GK][BM + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[NB][GK][BN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
@@ -81,18 +84,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, 
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&](int sb) {
 #pragma unroll
     for (int e = 0; e < AE; ++e) {
       const int idx = e * 256 + tid;
       if (A_KM) {
         const int m = (idx % (BM / W)) * W, k = idx / (BM / W);
-        if (VEC) *reinterpret_cast<float4 *>(&As[k][m]) = make_float4(ra[e][0], ra[e][W > 1 ? 1 : 0], ra[e][W > 2 ? 2 : 0], ra[e][W > 3 ? 3 : 0]);
-        else As[k][m] = ra[e][0];
+        if (VEC) *reinterpret_cast<float4 *>(&As[sb][k][m]) = make_float4(ra[e][0], ra[e][W > 1 ? 1 : 0], ra[e][W > 2 ? 2 : 0], ra[e][W > 3 ? 3 : 0]);
+        else As[sb][k][m] = ra[e][0];
       } else {
         const int k = (idx % (GK / W)) * W, m = idx / (GK / W);
 #pragma unroll
-        for (int c = 0; c < W; ++c) As[k + c][m] = ra[e][c];
+        for (int c = 0; c < W; ++c) As[sb][k + c][m] = ra[e][c];
       }
     }
 #pragma unroll
@@ -100,12 +103,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, 
       const int idx = e * 256 + tid;
       if (B_KM) {
         const int n = (idx % (BN / W)) * W, k = idx / (BN / W);
-        if (VEC) *reinterpret_cast<float4 *>(&Bs[k][n]) = make_float4(rb[e][0], rb[e][W > 1 ? 1 : 0], rb[e][W > 2 ? 2 : 0], rb[e][W > 3 ? 3 : 0]);
-        else Bs[k][n] = rb[e][0];
+        if (VEC) *reinterpret_cast<float4 *>(&Bs[sb][k][n]) = make_float4(rb[e][0], rb[e][W > 1 ? 1 : 0], rb[e][W > 2 ? 2 : 0], rb[e][W > 3 ? 3 : 0]);
+        else Bs[sb][k][n] = rb[e][0];
       } else {
         const int k = (idx % (GK / W)) * W, n = idx / (GK / W);
 #pragma unroll
-        for (int c = 0; c < W; ++c) Bs[k + c][n] = rb[e][c];
+        for (int c = 0; c < W; ++c) Bs[sb][k + c][n] = rb[e][c];
       }
     }
   };
@@ -119,24 +122,42 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, 
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   const int li = lane & 31, lk = lane >> 5;
-  if (kb < ke) load(kb);
-  for (int k0 = kb; k0 < ke; k0 += GK) {
-    __syncthreads();
-    store();
-    __syncthreads();
-    if (k0 + GK < ke) load(k0 + GK);
+  auto mma = [&](int cb) {
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 2) {
       float av[TM], bv[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) av[a] = As[kk + lk][wm * WM + a * 32 + li];
+      for (int a = 0; a < TM; ++a) av[a] = As[cb][kk + lk][wm * WM + a * 32 + li];
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bv[b] = Bs[kk + lk][wn * WN + b * 32 + li];
+      for (int b = 0; b < TN; ++b) bv[b] = Bs[cb][kk + lk][wn * WN + b * 32 + li];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  if (kb < ke) load(kb);
+  if (DB) {
+    // stage k0 + GK into the other buffer while k0's MFMAs run; one barrier per K-step
+    if (kb < ke) store(0);
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = kb; k0 < ke; k0 += GK) {
+      const bool more = k0 + GK < ke;
+      if (more) load(k0 + GK);
+      mma(cur);
+      if (more) store(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    for (int k0 = kb; k0 < ke; k0 += GK) {
+      __syncthreads();
+      store(0);
+      __syncthreads();
+      if (k0 + GK < ke) load(k0 + GK);
+      mma(0);
     }
   }
 
@@ -411,10 +432,10 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
   const bool b_ok = BK_ ? (N % 4 == 0 && ldb % 4 == 0) : (K % 4 == 0 && ldb % 4 == 0);
   const bool al = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
   if (a_ok && b_ok && al)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true, !AK && BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
                        K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, false, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M,
                        N, K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
   HICGAT_CHECK_LAUNCH();
   if (splits > 1) {
