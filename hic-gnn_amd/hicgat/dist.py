@@ -28,6 +28,7 @@ partitioning and collectives are testable on CPU with gloo and a torch stand-in.
 import torch
 import torch.distributed as dist
 
+from . import ops
 from .ops import _ACTS, weight_grad
 from .optim import FlatAdam
 
@@ -131,6 +132,10 @@ class ShardedTrainer:
         self.dcoords.view(-1).copy_(self.red[7:])
         K.loss_finalize(N, self.kind, self.stats, self.loss)
         # ---- backward -----------------------------------------------------------------------
+        # parameter gradients on the side stream from here to the gradient all-reduce (ops.py)
+        overlap = self.x_loc.is_cuda and ops.OVERLAP_DEFAULT
+        if overlap:
+            ops.side_begin()
         coords_loc.backward(self.dcoords[r0:r1])
         dout, rs_all = self.pack[:, :D], self.pack[:, D:]
         self.gbuf[r0:r1].copy_(o.grad)
@@ -148,6 +153,8 @@ class ShardedTrainer:
         with torch.no_grad():
             weight_grad(K, self.dh[r0:r1], self.x_loc, out=self.W.grad, accumulate=True) if self.x_loc.is_cuda \
                 else self.W.grad.addmm_(self.dh[r0:r1].t(), self.x_loc)
+        if overlap:
+            ops.side_join()
         dist.all_reduce(self.opt.grad, group=g)
         self.opt.step()
         return self.loss, self.stats, coords

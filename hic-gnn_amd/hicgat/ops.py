@@ -5,7 +5,9 @@
 * ``fused_dist_loss`` -- cdist + MSELoss (+ Pearson / combined loss value) fused (a7-a9), D never
                          materialised; returns the loss scalar and keeps the fp64 stats.
 """
+import contextlib
 import os
+import threading
 
 import torch
 
@@ -20,6 +22,68 @@ def _sink(p):
     if p is not None and getattr(p, "_hicgat_grad_sink", False) and p.grad is not None:
         return p.grad
     return None
+
+
+# ---- weight-gradient side stream ---------------------------------------------------------------
+# The parameter-gradient kernels (split-K dW GEMMs, bias column sums, GAT param_grad) feed only the
+# optimizer, never the next backward op, so inside ``overlapped_param_grads`` they are issued on a
+# side stream that forks from the backward's stream and is joined back before anything reads the
+# flat gradient buffer (Adam / the gradient all-reduce).  The MFMA-bound GEMMs then run beside the
+# L2-bound aggregation backward instead of in series with it; in a captured step the fork and join
+# are graph edges.  Only sink-bound gradients (``_sink``) go to the side stream -- a gradient that
+# is returned to autograd is consumed on the backward's stream and must be produced there.
+_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": []}
+_SIDE_LOCK = threading.Lock()
+OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
+
+
+def side_begin():
+    """Route sink-bound parameter gradients to the side stream until ``side_join``."""
+    with _SIDE_LOCK:
+        _SIDE["on"] += 1
+
+
+def side_join():
+    """Make every stream that forked work onto the side stream wait for it; drop the held inputs."""
+    with _SIDE_LOCK:
+        _SIDE["on"] = max(0, _SIDE["on"] - 1)
+        for dev, main in _SIDE["mains"].items():
+            main.wait_stream(_SIDE["streams"][dev])
+        _SIDE["mains"].clear()
+        _SIDE["hold"].clear()
+
+
+@contextlib.contextmanager
+def overlapped_param_grads(enabled=None):
+    """``with overlapped_param_grads(): loss.backward()`` -- parameter gradients overlap the rest
+    of the backward and are complete (ordered before the caller's stream) on exit."""
+    if not (OVERLAP_DEFAULT if enabled is None else enabled):
+        yield
+        return
+    side_begin()
+    try:
+        yield
+    finally:
+        side_join()
+
+
+def _side(*keep):
+    """Stream context for a sink-bound gradient kernel: the side stream (after a fork from the
+    current stream) while overlapping, else a no-op.  ``keep`` are the inputs the side kernels
+    read; they stay referenced until the join so the caching allocator cannot hand their memory
+    to a later backward kernel while the side stream still reads it."""
+    if not _SIDE["on"]:
+        return contextlib.nullcontext()
+    cur = torch.cuda.current_stream()
+    dev = cur.device
+    with _SIDE_LOCK:
+        side = _SIDE["streams"].get(dev)
+        if side is None:
+            side = _SIDE["streams"][dev] = torch.cuda.Stream(device=dev)
+        _SIDE["mains"].setdefault(dev, cur)
+        _SIDE["hold"].extend(keep)
+    side.wait_stream(cur)
+    return torch.cuda.stream(side)
 
 
 def _dev_check(*ts):
@@ -81,8 +145,9 @@ class _GATConvFn(torch.autograd.Function):
         pW, pl, pr, pb = ctx.params
         sinks = (_sink(pl), _sink(pr), _sink(pb) if ctx.has_bias else None)
         if all(t is not None for t in sinks):
-            K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
-                         accumulate=True)
+            with _side(h, dout, da_src, row_stats):
+                K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
+                             accumulate=True)
             datt_l = datt_r = dbias = None
         else:
             datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
@@ -90,9 +155,7 @@ class _GATConvFn(torch.autograd.Function):
             dbias = dbias if ctx.has_bias else None
         dW = None
         if ctx.needs_input_grad[1]:
-            gW = _sink(pW)
-            dW = weight_grad(K, dh, x, out=gW, accumulate=gW is not None)
-            dW = None if gW is not None else dW
+            dW = _weight_grad_to(K, pW, dh, x)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
@@ -126,15 +189,19 @@ def weight_grad(K, dy, x, out=None, accumulate=False, impl=None):
 def _weight_grad_to(K, p, dy, x):
     """dW = dy^T x into the parameter's sink (returns None) or a new tensor (returned)."""
     g = _sink(p)
-    dW = weight_grad(K, dy, x, out=g, accumulate=g is not None)
-    return None if g is not None else dW
+    if g is not None:
+        with _side(dy, x):
+            weight_grad(K, dy, x, out=g, accumulate=True)
+        return None
+    return weight_grad(K, dy, x)
 
 
 def _bias_grad_to(K, p, dy):
     """db = column sums of dy into the parameter's sink (returns None) or a new tensor."""
     g = _sink(p)
     if g is not None:
-        K.colsum(dy, g, accumulate=True)
+        with _side(dy):
+            K.colsum(dy, g, accumulate=True)
         return None
     return K.colsum(dy, torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device))
 
@@ -322,12 +389,14 @@ class _DualLnReluResFn(torch.autograd.Function):
         sW1, sW2, sb1, sb2 = _sink(W1), _sink(W2), _sink(b1), _sink(b2)
         dW1 = dW2 = db1 = db2 = None
         if sW1 is not None and sW2 is not None and _adjacent(sW1, sW2):
-            weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True)
+            with _side(dY, x):
+                weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True)
         else:
             dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
             dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
         if sb1 is not None and sb2 is not None and _adjacent(sb1, sb2):
-            K.colsum(dY, _joined(sb1, sb2), accumulate=True)
+            with _side(dY):
+                K.colsum(dY, _joined(sb1, sb2), accumulate=True)
         else:
             db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
             db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())

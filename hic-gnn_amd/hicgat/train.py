@@ -17,7 +17,7 @@ import sys
 import numpy as np
 import torch
 
-from . import graph, metrics
+from . import graph, metrics, ops
 from .gat_models import MODELS
 from .optim import FlatAdam
 
@@ -27,7 +27,8 @@ def train_step(model, opt, x, edge_index, truth, kind="mse", stats=None):
     model.train()
     opt.zero_grad()
     loss, stats, coords = model.loss(x, edge_index, truth, kind, stats=stats)
-    loss.backward()
+    with ops.overlapped_param_grads(None if x.is_cuda else False):   # dW, db beside the backward
+        loss.backward()
     opt.step()
     return loss, stats, coords
 

@@ -573,6 +573,40 @@ def test_graph_replay_equals_eager_steps():
     assert torch.equal(pe, pg)
 
 
+def test_overlapped_param_grads_same_bits():
+    """Parameter gradients on the side stream (ops.overlapped_param_grads, the train_step default)
+    give the same bits as the serial backward, eagerly and inside a captured step."""
+    import hicgat
+    from hicgat import ops, synth
+    n = 1200
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=2)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    x = torch.tensor(synth.features(n, seed=2), device=DEV)
+    saved = ops.OVERLAP_DEFAULT
+    res = []
+    try:
+        for overlap, graphed in ((False, False), (True, False), (True, True)):
+            ops.OVERLAP_DEFAULT = overlap
+            torch.manual_seed(0)
+            model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+            opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+            if graphed:
+                step = hicgat.graphs.captured_train_step(model, opt, x, adj, tr, warmup=1)
+                losses = [float(step()[0]) for _ in range(3)]
+            else:
+                losses = [float(hicgat.train.train_step(model, opt, x, adj, tr)[0]) for _ in range(4)][1:]
+            torch.cuda.synchronize()
+            res.append((losses, opt.flat.clone(), opt.grad.clone()))
+    finally:
+        ops.OVERLAP_DEFAULT = saved
+    (l0, p0, g0), (l1, p1, g1), (l2, p2, g2) = res
+    assert l0 == l1 == l2
+    assert torch.equal(p0, p1) and torch.equal(p0, p2)
+    assert torch.equal(g0, g1) and torch.equal(g0, g2)
+
+
 def test_dscc_matches_scipy():
     import hicgat
     from scipy.stats import spearmanr
