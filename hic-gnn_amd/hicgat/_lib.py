@@ -44,6 +44,12 @@ SIGNATURES = {
     "hicgat_gat_agg_bwd_src_sliced": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p,
                                               c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_int, c_p, c_p, c_p,
                                               c_sz, c_p]),
+    "hicgat_gat_blk_workspace_bytes": (c_sz, [c_int, c_int]),
+    "hicgat_gat_blk_fwd": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p,
+                                   c_p, c_p, c_f, c_int, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "hicgat_gat_blk_bwd_src": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
+                                       c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_sz,
+                                       c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),

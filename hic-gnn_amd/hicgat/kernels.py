@@ -18,6 +18,7 @@ GEMM_IMPLS = {"auto": 0, "f32": 1, "x3": 2}
 # the product default is the plain fp32 MFMA GEMM; HICGAT_GEMM=auto opts into the fp32-accurate x3
 # split where it applies (10-25 % faster GEMMs, profiles/r01_kbench_x3_sliced.txt)
 GEMM_DEFAULT = "f32"
+AGG_DEFAULT = "row"
 
 
 class _timed:
@@ -50,6 +51,17 @@ class HipKernels:
         # matrix-core arithmetic of the GEMMs (include/hicgat.h HICGAT_GEMM_*): 0 auto (x3 where
         # supported), 1 fp32 MFMA only, 2 x3 only
         self.gemm_impl = GEMM_IMPLS[os.environ.get("HICGAT_GEMM", GEMM_DEFAULT)]
+        # aggregation form: "row" = one wave per row (gat_fwd.hip / gat_bwd.hip), "block" = 16-row
+        # blocks over the union of their neighbour lists (gat_block.hip); the strips above win
+        self.agg_form = os.environ.get("HICGAT_AGG", AGG_DEFAULT)
+        if self.agg_form not in ("row", "block"):
+            raise ValueError(f"HICGAT_AGG must be 'row' or 'block', got {self.agg_form!r}")
+
+    def _blk(self, rowptr, col, r0, r1, N, device):
+        from .graph import device_block_csr
+        runs, run_ptr, pos = device_block_csr(rowptr, col, r0, r1)
+        ws = _lib.workspace(self.lib.hicgat_gat_blk_workspace_bytes(N, col.numel()), device)
+        return runs, run_ptr, pos, ws
 
     # -- a2 ---------------------------------------------------------------------------------------
     def linear_att(self, x, W, att_l, att_r, h=None):
@@ -86,7 +98,7 @@ class HipKernels:
 
     # -- a4 + a5 ----------------------------------------------------------------------------------
     def agg_fwd(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats):
-        if self.slice_width:
+        if self.slice_width or self.agg_form == "block":
             return self.agg_fwd_act(rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, 0, out, None, row_stats)
         N = h.shape[0]
         H = a_src.shape[1]
@@ -109,6 +121,14 @@ class HipKernels:
                                                               P(a_dst), P(bias), float(ns), int(act), self.slice_width,
                                                               P(out), P(out2), P(row_stats), P(ws), ws.numel(),
                                                               _lib.stream(h.device)), "hicgat_gat_agg_fwd_sliced")
+            return
+        if self.agg_form == "block":
+            runs, run_ptr, pos, ws = self._blk(rowptr, col, r0, r1, N, h.device)
+            with _timed("gat_agg_fwd"):
+                _lib.check(self.lib.hicgat_gat_blk_fwd(P(rowptr), P(col), P(pos), P(runs), P(run_ptr), N, col.numel(),
+                                                       H, C, r0, r1, P(h), P(a_src), P(a_dst), P(bias), float(ns),
+                                                       int(act), P(out), P(out2), P(row_stats), P(ws), ws.numel(),
+                                                       _lib.stream(h.device)), "hicgat_gat_blk_fwd")
             return
         with _timed("gat_agg_fwd"):
             _lib.check(self.lib.hicgat_gat_agg_fwd_act(P(rowptr), P(col), N, col.numel(), H, C, r0, r1, P(h),
@@ -151,6 +171,14 @@ class HipKernels:
                     P(rowptr), P(col), N, nnz, H, C, r0, r1, P(h), P(a_src), P(a_dst), P(row_stats), row_stats.stride(0),
                     P(dout), dout.stride(0), P(att_l), P(att_r), float(ns), self.slice_width, P(dh), P(da_src), P(ws),
                     ws.numel(), _lib.stream(h.device)), "hicgat_gat_agg_bwd_src_sliced")
+            return
+        if self.agg_form == "block":
+            runs, run_ptr, pos, ws = self._blk(rowptr, col, r0, r1, N, h.device)
+            with _timed("gat_agg_bwd_src"):
+                _lib.check(self.lib.hicgat_gat_blk_bwd_src(
+                    P(rowptr), P(col), P(pos), P(runs), P(run_ptr), N, col.numel(), H, C, r0, r1, P(h), P(a_src),
+                    P(a_dst), P(row_stats), row_stats.stride(0), P(dout), dout.stride(0), P(att_l), P(att_r),
+                    float(ns), P(dh), P(da_src), P(ws), ws.numel(), _lib.stream(h.device)), "hicgat_gat_blk_bwd_src")
             return
         with _timed("gat_agg_bwd_src"):
             _lib.check(self.lib.hicgat_gat_agg_bwd_src_ld(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),

@@ -148,6 +148,28 @@ int hicgat_gat_agg_bwd_src_sliced(const int32_t *rowptr, const int32_t *col, int
                                   const float *att_dst, float neg_slope, int slice_width, float *dh,
                                   float *da_src, void *workspace, size_t workspace_bytes,
                                   hicgat_stream_t stream);
+/* Row-block forms of hicgat_gat_agg_fwd_act and hicgat_gat_agg_bwd_src_ld (csrc/gat_block.hip):
+ * the same outputs (row_stats bit-identical, out / out2 / dh / da_src up to fp32 summation order).
+ * 16 consecutive rows share one workgroup that loads each distinct neighbour row once for all of
+ * them.  `runs` / `run_ptr` / `pos` is the static block structure of rows [row_begin, row_end)
+ * (hicgat/graph.py block_csr): runs[u] = j | (mask << 32) sorted by (block, j), block b's runs in
+ * [run_ptr[b], run_ptr[b+1]), pos[e - rowptr[row_begin]] = edge e's block-order position.  The
+ * per-step edge weights go to the workspace (hicgat_gat_blk_workspace_bytes(N, nnz), nnz = the
+ * whole CSR).  Replaces the same reference interface as the row forms (PyG GATConv propagate). */
+size_t hicgat_gat_blk_workspace_bytes(int N, int nnz);
+int hicgat_gat_blk_fwd(const int32_t *rowptr, const int32_t *col, const int32_t *pos,
+                       const int64_t *runs, const int32_t *run_ptr, int N, int nnz, int H, int C,
+                       int row_begin, int row_end, const float *h, const float *a_src,
+                       const float *a_dst, const float *bias, float neg_slope, int act, float *out,
+                       float *out2, float *row_stats, void *workspace, size_t workspace_bytes,
+                       hicgat_stream_t stream);
+int hicgat_gat_blk_bwd_src(const int32_t *rowptr, const int32_t *col, const int32_t *pos,
+                           const int64_t *runs, const int32_t *run_ptr, int N, int nnz, int H, int C,
+                           int row_begin, int row_end, const float *h, const float *a_src,
+                           const float *a_dst, const float *row_stats, int64_t ld_stats,
+                           const float *dout, int64_t ld_dout, const float *att_src,
+                           const float *att_dst, float neg_slope, float *dh, float *da_src,
+                           void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;

@@ -1,0 +1,118 @@
+"""GPU parity of the row-block aggregation form (csrc/gat_block.hip, HICGAT_AGG=block).
+
+* the GATConv oracle tests of test_gpu_parity.py re-run with the block form selected
+  (rtol 1e-5 on the output, 1e-4 of the max magnitude on gradients, as there);
+* block vs row-per-wave kernels on the same inputs, including row ranges that do not start on a
+  block boundary and the row-strided [dout | row stats] buffer of the sharded step: row_stats
+  bit-identical (same per-row arithmetic), out / out2 / dh / da_src to fp32 summation order;
+* training steps of the flagship model with either form.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import (test_gatconv_forward_backward_matches_oracle as _oracle_fb,
+                             test_gatconv_fused_relu_matches_oracle as _oracle_relu,
+                             test_gatconv_tiny_graphs_match_oracle as _oracle_tiny)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _block_form():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hicgat import kernels
+    K = kernels.default()
+    saved = K.agg_form
+    K.agg_form = "block"
+    yield
+    K.agg_form = saved
+
+
+@pytest.mark.parametrize("n,p", [(58, 1.0), (130, 0.3), (257, 0.02), (600, 0.5)])
+def test_block_gatconv_matches_oracle(n, p):
+    _oracle_fb(n, p)
+
+
+@pytest.mark.parametrize("n,p", [(58, 1.0), (257, 0.02)])
+def test_block_gatconv_fused_relu_matches_oracle(n, p):
+    _oracle_relu(n, p)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 17])
+def test_block_tiny_graphs(n):
+    _oracle_tiny(n)
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / max(float(b.double().abs().max()), 1e-30))
+
+
+@pytest.mark.parametrize("r0,r1", [(0, 3000), (37, 2011), (2990, 3000)])
+def test_block_equals_row_form(r0, r1):
+    import hicgat
+    from hicgat import kernels, synth
+    n = 3000
+    i, j, c = synth.contact_pairs(n, density=0.02, seed=4)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    rowptr, col = adj.rowptr32, adj.col32
+    g = torch.Generator(device="cpu").manual_seed(0)
+    h = torch.randn(n, 512, generator=g).to(DEV)
+    a_src = torch.randn(n, 2, generator=g).to(DEV)
+    a_dst = torch.randn(n, 2, generator=g).to(DEV)
+    bias = (0.1 * torch.randn(512, generator=g)).to(DEV)
+    att_l = torch.randn(2, 256, generator=g).to(DEV)
+    att_r = torch.randn(2, 256, generator=g).to(DEV)
+    Kb = kernels.default()
+    Kr = kernels.HipKernels()
+    Kr.agg_form, Kr.slice_width = "row", 0
+    res = {}
+    for name, K in (("row", Kr), ("block", Kb)):
+        out = torch.zeros(n, 512, device=DEV)
+        out2 = torch.zeros(n, 512, device=DEV)
+        rs = torch.zeros(n, 8, device=DEV)
+        K.agg_fwd_act(rowptr, col, r0, r1, h, a_src, a_dst, bias, 0.2, 1, out, out2, rs)
+        # backward inputs: the packed [dout | row stats] rows of the sharded step (row stride 520)
+        pack = torch.zeros(n, 520, device=DEV)
+        pack[:, :512] = torch.randn(n, 512, generator=torch.Generator().manual_seed(1)).to(DEV)
+        rs_all = torch.zeros(n, 8, device=DEV)
+        K.agg_fwd_act(rowptr, col, 0, n, h, a_src, a_dst, bias, 0.2, 1, torch.empty_like(out),
+                      torch.empty_like(out2), rs_all)
+        pack[:, 512:] = rs_all
+        pack[:, 516:] = torch.randn(n, 4, generator=torch.Generator().manual_seed(2)).to(DEV)
+        dh = torch.zeros(n, 512, device=DEV)
+        da = torch.zeros(n, 2, device=DEV)
+        K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, pack[:, 512:], pack[:, :512], att_l, att_r, 0.2, dh, da)
+        torch.cuda.synchronize()
+        res[name] = (out, out2, rs, dh, da)
+    (o, o2, rs, dh, da), (ob, o2b, rsb, dhb, dab) = res["row"], res["block"]
+    assert torch.equal(rs, rsb)                       # max / sum / S3: same arithmetic, same order
+    assert _rel(ob, o) < 1e-5 and _rel(o2b, o2) < 1e-5
+    assert _rel(dhb, dh) < 1e-5 and _rel(dab, da) < 1e-4
+    outside = torch.ones(n, dtype=torch.bool)
+    outside[r0:r1] = False
+    assert not ob[outside.to(DEV)].any() and not dhb[outside.to(DEV)].any()
+
+
+def test_block_train_steps_track_row_form():
+    import hicgat
+    from hicgat import kernels, synth
+    n = 1500
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=1)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    x = torch.tensor(synth.features(n, seed=1), device=DEV)
+    K = kernels.default()
+    hist = {}
+    for form in ("row", "block"):
+        K.agg_form = form
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+        opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+        hist[form] = [float(hicgat.train.train_step(model, opt, x, adj, tr)[0]) for _ in range(5)]
+    K.agg_form = "block"
+    np.testing.assert_allclose(hist["block"], hist["row"], rtol=1e-5)
