@@ -485,6 +485,13 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 #ifndef HICGAT_GEMM_TALL128
 #define HICGAT_GEMM_TALL128 0   // 1: 128 x 128 tiles for the tall (M = node rows) problems too
 #endif
+#ifndef HICGAT_GEMM_TALL_TILE
+#define HICGAT_GEMM_TALL_TILE 0   // tall problems: 0 = 64 x 128, 2 = 128 x 256, 3 = 256 x 128 (A/B builds)
+#endif
+  if (HICGAT_GEMM_TALL_TILE == 2 && M > 1024 && N >= 256)
+    return launch<128, 256, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
+  if (HICGAT_GEMM_TALL_TILE == 3 && M > 1024 && N >= 128)
+    return launch<256, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
     return launch<128, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   if (N >= 128) return launch<64, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);

@@ -69,6 +69,7 @@ def main():
             S = kernels.HipKernels.__new__(kernels.HipKernels)
             S.lib, S.slice_width = K.lib, sw
             S.gemm_impl = getattr(K, "gemm_impl", 0)
+            S.agg_form = "row"
             sliced[key] = S
         return sliced[key]
     kset = []
@@ -81,6 +82,7 @@ def main():
         K.lib = lib
         K.slice_width = 0            # the row-per-wave kernels; "@sw" jobs time the strip kernels
         K.gemm_impl = 0              # GEMMs: auto (x3 where supported); "#f32" / "#x3" jobs force one
+        K.agg_form = "row"           # "!block" jobs time the row-block form
         kset.append((os.path.basename(path), K))
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
