@@ -331,9 +331,12 @@ def ln_relu_res(y, norm, res=None):
 
 
 def _adjacent(a, b):
-    """``b`` starts right where ``a`` ends in memory (two flat-buffer parameter views): the pair
-    is then one [a; b] tensor without a copy."""
+    """``b`` starts right where ``a`` ends in the SAME storage (two views into FlatAdam's flat
+    buffer): the pair is then one [a; b] tensor without a copy.  Two separate allocations that
+    merely happen to sit back to back (the caching allocator packs small blocks into one segment)
+    do not qualify: a view cannot span two storages."""
     return (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
             and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size())
 
 

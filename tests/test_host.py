@@ -106,3 +106,20 @@ def test_adj_host_sage_weights_match_oracle():
     assert diag.sum().item() == n and torch.all(adj.value32[diag] == 0)
     assert torch.equal(adj.value32[~diag], v.float())
     assert np.array_equal(adj.inv_deg.numpy(), sage.degree_inverse(g["rowptr"], g["col"], g["value"], n))
+
+
+def test_adjacent_requires_one_storage():
+    """ops._adjacent / _joined: views into one flat buffer join without a copy; two storages that
+    merely sit back to back in memory (the caching allocator packs small blocks) do not."""
+    import numpy as np
+    from hicgat.ops import _adjacent, _joined
+    flat = torch.arange(16, dtype=torch.float32)
+    a, b = flat[:8].view(2, 4), flat[8:].view(2, 4)
+    assert _adjacent(a, b)
+    j = _joined(a, b)
+    assert j.data_ptr() == a.data_ptr() and torch.equal(j, flat.view(4, 4))
+    arr = np.arange(16, dtype=np.float32)
+    x, y = torch.from_numpy(arr[:8]).view(2, 4), torch.from_numpy(arr[8:]).view(2, 4)
+    assert y.data_ptr() == x.data_ptr() + 32 and x.untyped_storage().data_ptr() != y.untyped_storage().data_ptr()
+    assert not _adjacent(x, y)
+    assert torch.equal(_joined(x, y), torch.from_numpy(arr).view(4, 4))
