@@ -253,13 +253,18 @@ def main():
     cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "sage_agg",
                          "pairdist_mse_fused") if k in kern]
     dom = max(cands, key=lambda k: kern[k]["total_ms"])
+
+    def per_launch(k, b):
+        """A pass split into row chunks (the source pass, ops._src_chunks) is several launches per
+        step over near-equal row ranges: each launch's algorithmic bytes are the pass's share."""
+        return b / max(1.0, kern[k]["launches"] / args.steps)
     if dom == "pairdist_mse_fused":
         alg = agg_bytes(dom, n, nnz) / (world if world > 1 else 1)
     else:
-        alg = agg_bytes(dom, n_loc, nnz)
+        alg = per_launch(dom, agg_bytes(dom, n_loc, nnz))
     achieved = alg / (kern[dom]["avg_ms"] * 1e-3) / 1e9
     for k in cands:
-        b = agg_bytes(k, n if k == "pairdist_mse_fused" else n_loc, nnz)
+        b = per_launch(k, agg_bytes(k, n if k == "pairdist_mse_fused" else n_loc, nnz))
         kern[k]["alg_GBps"] = b / (kern[k]["avg_ms"] * 1e-3) / 1e9
 
     traffic = pmc_traffic(dom, args.workload) if world == 1 else None
@@ -288,6 +293,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
                      "alg_bytes_per_launch": alg, "avg_launch_ms": kern[dom]["avg_ms"],
+                     "launches_per_step": kern[dom]["launches"] / args.steps,
                      # the HBM bytes the kernel really moves (PMC) over the same launch time: frac > 1
                      # above because the gathered rows are largely L2 / Infinity-Cache hits
                      "traffic_GBps": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 if traffic else None,

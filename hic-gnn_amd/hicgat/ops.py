@@ -95,6 +95,17 @@ def _dev_check(*ts):
 _ACTS = {None: 0, "relu": 1}
 
 
+# row chunks of the GAT source pass (see _GATConvFn.backward); 1 = one launch over all rows
+SRC_CHUNKS = int(os.environ.get("HICGAT_SRC_CHUNKS", "2"))
+
+
+def _src_chunks(n, chunks=None):
+    """[(r0, r1)] -- ``chunks`` near-equal row ranges (fewer when a chunk would be under 1024 rows)."""
+    c = max(1, min(SRC_CHUNKS if chunks is None else chunks, n // 1024))
+    b = [n * i // c for i in range(c + 1)]
+    return [(b[i], b[i + 1]) for i in range(c) if b[i + 1] > b[i]] or [(0, n)]
+
+
 class _GATConvFn(torch.autograd.Function):
     """PyG 1.7.2 GATConv (+ an optional fused relu epilogue, act=1).  With gradients enabled the
     aggregation also emits out2 / S3 (include/hicgat.h), so the destination half of the backward
@@ -141,21 +152,37 @@ class _GATConvFn(torch.autograd.Function):
             K.agg_bwd_rows(0, N, 0, dout, out, b, out2, None, row_stats)
         dh = torch.empty_like(h)
         da_src = torch.empty_like(a_src)
-        K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
         pW, pl, pr, pb = ctx.params
         sinks = (_sink(pl), _sink(pr), _sink(pb) if ctx.has_bias else None)
-        if all(t is not None for t in sinks):
-            with _side(h, dout, da_src, row_stats):
-                K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
-                             accumulate=True)
-            datt_l = datt_r = dbias = None
-        else:
-            datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
+        use_sinks = all(t is not None for t in sinks)
+        gW = _sink(pW) if ctx.needs_input_grad[1] else None
+        # The source pass runs in row chunks; each chunk's parameter-gradient share (param_grad
+        # partial column sums, dW += dh_c^T x_c) is issued right after it -- on the side stream
+        # when overlapping -- so only the last chunk's share is left after the gathers (the
+        # backward's tail).  The sink and autograd paths add the same partials in the same order.
+        datt_l = datt_r = dbias = dW = None
+        for c, (r0, r1) in enumerate(_src_chunks(N)):
+            K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+            rows = slice(r0, r1)
+            if use_sinks:
+                with _side(h, dout, da_src, row_stats):
+                    K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
+                                 out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
+            else:
+                datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
+                                                     out=None if c == 0 else (datt_l, datt_r, dbias),
+                                                     accumulate=c > 0)
+            if ctx.needs_input_grad[1]:
+                if gW is not None:
+                    with _side(dh, x):
+                        weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True)
+                else:
+                    dW = weight_grad(K, dh[rows], x[rows], out=dW, accumulate=dW is not None)
+        if not use_sinks:
             datt_l, datt_r = datt_l.view(al.shape), datt_r.view(ar.shape)
             dbias = dbias if ctx.has_bias else None
-        dW = None
-        if ctx.needs_input_grad[1]:
-            dW = _weight_grad_to(K, pW, dh, x)
+        else:
+            datt_l = datt_r = dbias = None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
