@@ -271,23 +271,28 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
   }
 }
 
-// block = 64 output columns x 4 groups; group g adds partials b = g, g+4, ...; groups combined
-// in order through LDS (fixed order: bitwise reproducible).
-__global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict__ part, int nblk,
-                                                         int D, float *__restrict__ datt_s,
-                                                         float *__restrict__ datt_d,
-                                                         float *__restrict__ dbias, int accumulate) {
-  __shared__ float red[4][64];
+// block = 64 output columns x 16 groups (1024 threads); group g adds partials b = g, g+16, ...;
+// the groups are combined in order through LDS (fixed order: bitwise reproducible).  Only
+// 3D / 64 = 24 blocks exist, so the partial range is cut 16 ways to keep each thread's chain of
+// dependent loads short (32 partials at nblk = 512).
+constexpr int kPG2Groups = 16;
+__global__ __launch_bounds__(1024) void param_grad_stage2(const float *__restrict__ part, int nblk,
+                                                          int D, float *__restrict__ datt_s,
+                                                          float *__restrict__ datt_d,
+                                                          float *__restrict__ dbias, int accumulate) {
+  __shared__ float red[kPG2Groups][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
   if (c < 3 * D) {
-    for (int b = grp; b < nblk; b += 4) s += part[(size_t)b * 3 * D + c];
+    for (int b = grp; b < nblk; b += kPG2Groups) s += part[(size_t)b * 3 * D + c];
   }
   red[grp][cl] = s;
   __syncthreads();
   if (grp == 0 && c < 3 * D) {
-    const float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    float t = red[0][cl];
+#pragma unroll
+    for (int g = 1; g < kPG2Groups; ++g) t += red[g][cl];
     const int which = c / D, cc = c % D;
     float *o = (which == 0 ? datt_s : which == 1 ? datt_d : dbias) + cc;
     *o = t + (accumulate ? *o : 0.f);
@@ -391,7 +396,7 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
                        da_src, row_stats, N, H, C, rpb, part);
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 63) / 64), dim3(64 * kPG2Groups), 0,
                      (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias, accumulate);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;

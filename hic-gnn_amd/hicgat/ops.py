@@ -96,7 +96,7 @@ _ACTS = {None: 0, "relu": 1}
 
 
 # row chunks of the GAT source pass (see _GATConvFn.backward); 1 = one launch over all rows
-SRC_CHUNKS = int(os.environ.get("HICGAT_SRC_CHUNKS", "2"))
+SRC_CHUNKS = int(os.environ.get("HICGAT_SRC_CHUNKS", "1"))
 
 
 def _src_chunks(n, chunks=None):
