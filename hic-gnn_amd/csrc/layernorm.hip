@@ -125,13 +125,18 @@ extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W) {
   return (size_t)kLnWaves * 2 * W * sizeof(float) + colsum_workspace_bytes(kLnWaves, 2 * W);
 }
 
+extern "C" int hicgat_ln_relu_res_bwd_params(int W, float *dgamma, float *dbeta, int accumulate,
+                                             void *workspace, size_t workspace_bytes,
+                                             hicgat_stream_t stream);
+
 extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, int W,
                                       const float *row_stats, const float *gamma, const float *beta, float *dy,
                                       int64_t lddy, float *dres, int64_t lddres, float *dgamma, float *dbeta,
                                       int accumulate, void *workspace, size_t workspace_bytes,
                                       hicgat_stream_t stream) {
   if (M < 0 || (W != 64 && W != 128 && W != 256)) return M < 0 ? HICGAT_EINVAL : HICGAT_EUNSUPPORTED;
-  if (!dz || !y || !row_stats || !gamma || !beta || !dy || !dgamma || !dbeta || !workspace) return HICGAT_EINVAL;
+  if (!dz || !y || !row_stats || !gamma || !beta || !dy || !workspace) return HICGAT_EINVAL;
+  if ((dgamma == nullptr) != (dbeta == nullptr)) return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_ln_relu_res_workspace_bytes(W)) return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   float *part = static_cast<float *>(workspace);
@@ -144,7 +149,20 @@ extern "C" int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t l
   else
     hipLaunchKernelGGL(ln_relu_res_bwd_kernel<256>, grid, dim3(256), 0, s, dz, y, ldy, M, st, gamma, beta, dy, lddy, dres, lddres, part);
   HICGAT_CHECK_LAUNCH();
-  // dgamma / dbeta = column sums of the per-wave partials [kLnWaves, 2W] (fixed order)
+  if (!dgamma) return HICGAT_OK;   // partials stay in the workspace for hicgat_ln_relu_res_bwd_params
+  return hicgat_ln_relu_res_bwd_params(W, dgamma, dbeta, accumulate, workspace, workspace_bytes, stream);
+}
+
+// dgamma / dbeta = column sums of the per-wave partials [kLnWaves, 2W] (fixed order) that a
+// hicgat_ln_relu_res_bwd call left in `workspace` -- e.g. on another stream, after an event.
+extern "C" int hicgat_ln_relu_res_bwd_params(int W, float *dgamma, float *dbeta, int accumulate,
+                                             void *workspace, size_t workspace_bytes,
+                                             hicgat_stream_t stream) {
+  if (W != 64 && W != 128 && W != 256) return HICGAT_EUNSUPPORTED;
+  if (!dgamma || !dbeta || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_ln_relu_res_workspace_bytes(W)) return HICGAT_EINVAL;
+  float *part = static_cast<float *>(workspace);
   const ColOut o{dgamma, 0, W, dbeta, nullptr, accumulate};
-  return colsum_launch(part, 2 * W, kLnWaves, 2 * W, o, part + (size_t)kLnWaves * 2 * W, s);
+  return colsum_launch(part, 2 * W, kLnWaves, 2 * W, o, part + (size_t)kLnWaves * 2 * W,
+                       (hipStream_t)stream);
 }

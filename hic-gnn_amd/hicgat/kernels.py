@@ -280,13 +280,24 @@ class HipKernels:
                                                    0 if res is None else res.stride(0), P(z), P(row_stats),
                                                    _lib.stream(z.device)), "hicgat_ln_relu_res_fwd")
 
-    def ln_relu_res_bwd(self, dz, y, row_stats, gamma, beta, dy, dgamma, dbeta, accumulate=False, dres=None):
+    def ln_relu_res_bwd(self, dz, y, row_stats, gamma, beta, dy, dgamma, dbeta, accumulate=False, dres=None,
+                        ws=None):
+        """dgamma = dbeta = None: dy / dres only, the partials stay in ``ws`` (pass it, then
+        ``ln_relu_res_bwd_params(W, dgamma, dbeta, ws)`` -- on another stream if wanted)."""
         M, W = dz.shape
-        ws = _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), dz.device)
+        if ws is None:
+            ws = self.ln_workspace(W, dz.device)
         _lib.check(self.lib.hicgat_ln_relu_res_bwd(P(dz), P(y), y.stride(0), M, W, P(row_stats), P(gamma), P(beta),
                                                    P(dy), dy.stride(0), P(dres), 0 if dres is None else dres.stride(0),
                                                    P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
                                                    _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
+
+    def ln_workspace(self, W, device):
+        return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)
+
+    def ln_relu_res_bwd_params(self, W, dgamma, dbeta, ws, accumulate=False):
+        _lib.check(self.lib.hicgat_ln_relu_res_bwd_params(W, P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
+                                                          _lib.stream(ws.device)), "hicgat_ln_relu_res_bwd_params")
 
     # -- a10 --------------------------------------------------------------------------------------
     def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):

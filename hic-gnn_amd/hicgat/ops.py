@@ -338,7 +338,10 @@ class _LnReluResFn(torch.autograd.Function):
         dy = torch.empty(y.shape, dtype=torch.float32, device=y.device)
         sg, sb = _sink(ctx.params[0]), _sink(ctx.params[1])
         if sg is not None and sb is not None:
-            K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, sg, sb, accumulate=True)
+            ws = K.ln_workspace(y.shape[1], y.device)
+            K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, None, None, ws=ws)
+            with _side(ws):
+                K.ln_relu_res_bwd_params(y.shape[1], sg, sb, ws, accumulate=True)
             dgamma = dbeta = None
         else:
             dgamma = torch.empty_like(gamma)
@@ -408,7 +411,10 @@ class _DualLnReluResFn(torch.autograd.Function):
         sg, sb = _sink(pg), _sink(pb)
         dgamma = dbeta = None
         if sg is not None and sb is not None:
-            K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], sg, sb, accumulate=True, dres=dY[:, w:])
+            ws = K.ln_workspace(w, dz.device)
+            K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], None, None, dres=dY[:, w:], ws=ws)
+            with _side(ws):
+                K.ln_relu_res_bwd_params(w, sg, sb, ws, accumulate=True)
         else:
             dgamma, dbeta = torch.empty_like(gamma), torch.empty_like(beta)
             K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], dgamma, dbeta, dres=dY[:, w:])

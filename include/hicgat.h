@@ -251,6 +251,12 @@ int hicgat_ln_relu_res_bwd(const float *dz, const float *y, int64_t ldy, int M, 
                            int64_t lddres, float *dgamma, float *dbeta, int accumulate, void *workspace,
                            size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_ln_relu_res_workspace_bytes(int W);
+/* dgamma = dbeta = NULL in hicgat_ln_relu_res_bwd: only dy (and dres) are written and the per-wave
+ * partials stay in the workspace; this call then reduces them into dgamma / dbeta (fixed order, the
+ * same bits as the one-call form) -- on another stream after an event, so the parameter
+ * reduction leaves the backward's critical path. */
+int hicgat_ln_relu_res_bwd_params(int W, float *dgamma, float *dbeta, int accumulate, void *workspace,
+                                  size_t workspace_bytes, hicgat_stream_t stream);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --
