@@ -35,6 +35,10 @@ def _sink(p):
 _SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": []}
 _SIDE_LOCK = threading.Lock()
 OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
+# LayerNorm dgamma/dbeta reductions on the side stream too (else inside the row-pass call)
+LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "0") != "0"     # measured slower
+# bias column sums / GAT param_grad on the side stream (else on the backward's stream)
+SMALL_SIDE = os.environ.get("HICGAT_SMALL_SIDE", "1") != "0"
 
 
 def side_begin():
@@ -65,6 +69,11 @@ def overlapped_param_grads(enabled=None):
         yield
     finally:
         side_join()
+
+
+def _side_small(*keep):
+    """``_side`` for the small parameter reductions (column sums), unless SMALL_SIDE is off."""
+    return _side(*keep) if SMALL_SIDE else contextlib.nullcontext()
 
 
 def _side(*keep):
@@ -165,7 +174,7 @@ class _GATConvFn(torch.autograd.Function):
             K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
             rows = slice(r0, r1)
             if use_sinks:
-                with _side(h, dout, da_src, row_stats):
+                with _side_small(h, dout, da_src, row_stats):
                     K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
                                  out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
             else:
@@ -227,7 +236,7 @@ def _bias_grad_to(K, p, dy):
     """db = column sums of dy into the parameter's sink (returns None) or a new tensor."""
     g = _sink(p)
     if g is not None:
-        with _side(dy):
+        with _side_small(dy):
             K.colsum(dy, g, accumulate=True)
         return None
     return K.colsum(dy, torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device))
@@ -337,7 +346,10 @@ class _LnReluResFn(torch.autograd.Function):
         dz = dz.contiguous()
         dy = torch.empty(y.shape, dtype=torch.float32, device=y.device)
         sg, sb = _sink(ctx.params[0]), _sink(ctx.params[1])
-        if sg is not None and sb is not None:
+        if sg is not None and sb is not None and not (LN_SIDE and _SIDE["on"]):
+            K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, sg, sb, accumulate=True)
+            dgamma = dbeta = None
+        elif sg is not None and sb is not None:
             ws = K.ln_workspace(y.shape[1], y.device)
             K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, None, None, ws=ws)
             with _side(ws):
@@ -410,7 +422,9 @@ class _DualLnReluResFn(torch.autograd.Function):
         dY = torch.empty((M, 2 * w), dtype=torch.float32, device=dz.device)
         sg, sb = _sink(pg), _sink(pb)
         dgamma = dbeta = None
-        if sg is not None and sb is not None:
+        if sg is not None and sb is not None and not (LN_SIDE and _SIDE["on"]):
+            K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], sg, sb, accumulate=True, dres=dY[:, w:])
+        elif sg is not None and sb is not None:
             ws = K.ln_workspace(w, dz.device)
             K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], None, None, dres=dY[:, w:], ws=ws)
             with _side(ws):
@@ -431,7 +445,7 @@ class _DualLnReluResFn(torch.autograd.Function):
             dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
             dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
         if sb1 is not None and sb2 is not None and _adjacent(sb1, sb2):
-            with _side(dY):
+            with _side_small(dY):
                 K.colsum(dY, _joined(sb1, sb2), accumulate=True)
         else:
             db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
