@@ -187,3 +187,32 @@ def test_linear_att_x3_matches_fused_fp32_kernel():
     assert _rel(s2.cpu(), (hv * al.double()).sum(-1).cpu()) < 1e-5
     assert _rel(d2.cpu(), (hv * ar.double()).sum(-1).cpu()) < 1e-5
     assert hicgat  # silence
+
+
+@pytest.mark.parametrize("W", [64, 128, 256])
+def test_ln_bwd_split_params_same_bits(W):
+    """hicgat_ln_relu_res_bwd with dgamma = dbeta = NULL + hicgat_ln_relu_res_bwd_params on a
+    second stream (the HICGAT_LN_SIDE form) == the one-call backward, bit for bit."""
+    from hicgat import kernels
+    K = kernels.default()
+    M = 3001
+    g = torch.Generator().manual_seed(W)
+    y = torch.randn(M, W, generator=g).to(DEV)
+    dz = torch.randn(M, W, generator=g).to(DEV)
+    gamma = (1 + 0.1 * torch.randn(W, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(W, generator=g)).to(DEV)
+    z = torch.empty_like(y)
+    stats = torch.empty(M, 2, device=DEV)
+    K.ln_relu_res_fwd(y, gamma, beta, 1e-5, None, z, stats)
+    dy1, dg1, db1 = torch.empty_like(y), torch.full((W,), 0.5, device=DEV), torch.full((W,), -0.5, device=DEV)
+    K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy1, dg1, db1, accumulate=True)
+    dy2, dg2, db2 = torch.empty_like(y), torch.full((W,), 0.5, device=DEV), torch.full((W,), -0.5, device=DEV)
+    ws = K.ln_workspace(W, y.device)
+    K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy2, None, None, ws=ws)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        K.ln_relu_res_bwd_params(W, dg2, db2, ws, accumulate=True)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(dy1, dy2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
