@@ -422,6 +422,9 @@ __global__ void colsum_zero_kernel(float *out, int N, int accumulate) {
   if (n < N && !accumulate) out[n] = 0.f;
 }
 
+#ifndef HICGAT_GEMM_DB_ALL
+#define HICGAT_GEMM_DB_ALL 0   // 1: double-buffered LDS for every layout (A/B build; default: dX layout only)
+#endif
 template <int BM, int BN, bool AK, bool BK_>
 static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
                   int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
@@ -432,7 +435,7 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
   const bool b_ok = BK_ ? (N % 4 == 0 && ldb % 4 == 0) : (K % 4 == 0 && ldb % 4 == 0);
   const bool al = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
   if (a_ok && b_ok && al)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true, !AK && BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true, HICGAT_GEMM_DB_ALL ? true : (!AK && BK_)>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
                        K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
   else
     hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, false, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M,
