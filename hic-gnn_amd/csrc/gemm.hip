@@ -28,7 +28,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int GK = HICGAT_GK;  // K-step of the fp32 kernel
 
 template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB>
-__global__ __launch_bounds__(256) void gemm_kernel(const float *__restrict__ A, int64_t lda,
+#ifndef HICGAT_GEMM_OCC64
+// min blocks per CU of the 64 x 128 fp32 kernel: 6 makes the compiler keep the accumulators in
+// VGPRs (74 in all, 6 waves per SIMD instead of 4): fwd 512x512 0.104 vs 0.115 ms, dX 0.057 vs
+// 0.060 (profiles/r01_kbench_gemm_tiles.txt).  The 128 x 128 kernel keeps 1: squeezed the same
+// way its split-K weight gradients ran 2x slower.
+#define HICGAT_GEMM_OCC64 6
+#endif
+__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
                                                    int K, int kchunk, const float *__restrict__ bias,
