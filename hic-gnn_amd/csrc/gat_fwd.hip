@@ -61,8 +61,11 @@ __global__ __launch_bounds__(256) void att_logits_kernel(const float *__restrict
 //   da_dst_i = sum_j alpha_ij lrelu'(e_ij) (<dout_i, h_j> - delta_i) = <dout_i, out2_i> - delta_i S3_i
 // (agg_bwd_rows_kernel, gat_bwd.hip).  ACT = 1 applies the relu that follows the GATConv in
 // GATNetSelectiveResidualsUpdated (models.py:637) in the epilogue: out = relu(acc + bias).
+#ifndef HICGAT_FWD_OCC
+#define HICGAT_FWD_OCC 1   // __launch_bounds__ min blocks per CU of the training form (A/B builds)
+#endif
 template <bool TRAIN, int ACT>
-__global__ __launch_bounds__(256) void agg_fwd_h2c256_kernel(
+__global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ bias, float ns, float *__restrict__ out, float *__restrict__ out2,

@@ -72,6 +72,12 @@ def main():
             S.agg_form = "row"
             sliced[key] = S
         return sliced[key]
+    def _with_impl(K, impl, fn):
+        saved, K.gemm_impl = K.gemm_impl, impl
+        try:
+            return fn()
+        finally:
+            K.gemm_impl = saved
     kset = []
     for path in libs:
         lib = ctypes.CDLL(path)
@@ -86,6 +92,7 @@ def main():
         kset.append((os.path.basename(path), K))
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
+        "gat_linear_att#f32": lambda K: _with_impl(K, 1, lambda: K.linear_att(x, W, al, ar)),
         "gat_agg_fwd": lambda K: K.agg_fwd(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, out, rs),
         "gat_agg_fwd_train": lambda K: K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out,
                                                      out2, rs),
