@@ -35,7 +35,11 @@ template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB>
 // way its split-K weight gradients ran 2x slower.
 #define HICGAT_GEMM_OCC64 6
 #endif
-__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
+#ifndef HICGAT_GEMM_OCC128
+#define HICGAT_GEMM_OCC128 1   // the same for the 128 x 128 tile (A/B builds)
+#endif
+__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64
+                                  : (BM == 128 && BN == 128 && VEC) ? HICGAT_GEMM_OCC128 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
                                                    int K, int kchunk, const float *__restrict__ bias,
