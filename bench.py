@@ -1,20 +1,40 @@
 """Benchmark: GAT-HiC training steps/sec on MI355X (BASELINE.json metric).
 
   python bench.py [--gpus N --steps K --warmup W] [--workload synth-20000|synth-2000]
+                  [--dist-mode allgather|replicate]
 
 One step = zero_grad + GATConv (MFMA lin_l + fused logits, edge-softmax aggregation) + MLP tail
 + fused distance/MSE loss + backward + Adam, over the whole synthetic Hi-C graph, inputs resident
-in HBM.  N > 1 (torch.distributed.run, one rank per GPU, RCCL): destination rows are sharded
-across ranks with RCCL all-gathers of the 512-d node embeddings (strong scaling: the same
-N = 20000 graph is split, so ``value`` = whole-model steps per second).
+in HBM, replayed as one captured hipGraph (``--eager``: kernel by kernel).
 
-Rank 0 prints ONE JSON line.  ``roofline`` is computed from HIP events recorded around every
-launch of the dominant kernel inside the timed region; ``cpu_baseline`` times the CPU oracle (a
-plain-torch restatement of the reference path) on a bounded sample of the same workload.
+N > 1: one rank per GPU over RCCL (hicgat.dist: destination rows sharded by an nnz prefix sum,
+RCCL all-gathers of the 512-d node embeddings; strong scaling -- the same N = 20000 graph is
+split, so ``value`` = whole-model steps per second).  Launched by the driver through
+``torch.distributed.run`` (RANK / WORLD_SIZE in the environment), or directly as
+``python bench.py --gpus N``: then this script starts ``torch.distributed.run`` itself as a child
+process (before any GPU call) and exits with its code; it exits non-zero if fewer than N GPUs are
+visible.
+
+Rank 0 prints ONE JSON line.  ``value`` = K / (max over ranks of the barrier-bracketed wall time of
+the K timed steps).  Per-kernel times (``kernels``, ``roofline.avg_launch_ms``) come from HIP
+events around every launch in an EAGER pass of K steps run right after the timed region (a graph
+replay hides kernel boundaries); rocprofv3's per-kernel averages of the same command are committed
+under profiles/ to cross-check them.  ``roofline.frac`` = HBM bytes the dominant kernel really
+moves (PMC FETCH_SIZE x 2 + WRITE_SIZE, rocprofv3 --pmc passes recorded in profiles/*pmc_traffic*,
+command and commit named in ``traffic_source``) / its average launch time / 8 TB/s;
+``l2_frac`` = its SURVEY 8(d) no-reuse algorithmic bytes / time / the 34.5 TB/s L2 peak (the
+gathered rows are L2 / Infinity-Cache hits).  ``cpu_baseline`` times the CPU
+oracle (a plain-torch restatement of the reference path) on the same workload.
+
+``--selftest-cpu`` (tests only): gloo ranks on the CPU with the torch stand-in kernels of
+tests/cpu_kernels.py on a 400-node graph -- exercises the launcher and the sharded step; it is
+not a measurement.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,6 +47,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6290
+L2_PEAK_GBS = 34500.0   # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)")
 D_FEAT = 512
 HEADS = 2
 
@@ -36,7 +57,7 @@ def log(*a):
 
 
 def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
-    """Algorithmic HBM bytes per launch (DESIGN.md 'Roofline')."""
+    """Algorithmic (no-reuse) bytes per launch."""
     if kind == "gat_agg_fwd":      # gather h_j + col per edge, write out + out2 (training form), rowptr, stats
         return nnz * (4 * d + 4) + 2 * n * 4 * d + (n + 1) * 4 + 2 * n * h * 4 + nnz * 4 * h + n * 16
     if kind == "gat_agg_bwd_rows":  # stream g, y, out2 in and dout out; S3 in, (delta, da_dst) out
@@ -56,36 +77,38 @@ def agg_bytes(kind, n, nnz, d=D_FEAT, h=HEADS):
 
 # timer name (kernels.py) -> HIP kernels launched inside that timed region
 PMC_KERNELS = {
-    "gat_agg_fwd": ["agg_fwd_h2c256_kernel", "agg_edge_rec_kernel", "agg_fwd_strip_kernel"],
+    "gat_agg_fwd": ["agg_fwd_h2c256_kernel"],
     "gat_agg_bwd_dst": ["agg_bwd_dst_h2c256_kernel"],
     "gat_agg_bwd_rows": ["agg_bwd_rows_kernel"],
     "sage_agg": ["sage_agg_f512_kernel", "sage_agg_generic_kernel"],
-    "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel", "agg_src_rec_kernel", "agg_bwd_src_strip_kernel",
-                        "agg_src_finalize_kernel"],
-    "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_reduce_kernel", "moments_reduce_kernel"],
+    "gat_agg_bwd_src": ["agg_bwd_src_h2c256_kernel"],
+    "pairdist_mse_fused": ["pairdist_tile_kernel<0", "pairdist_persist_kernel", "pairdist_reduce_kernel",
+                           "moments_partial_kernel", "moments_final_kernel"],
 }
 
 
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of ``kernel`` from the newest committed PMC summary for ``workload``
     (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py from two rocprofv3 --pmc passes
-    of this bench: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if not collected."""
+    of this bench: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  (bytes, source) or (None, None)."""
     import glob
-    best = None
+    best, src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         with open(f) as fh:
             d = json.load(fh)
         if d.get("workload") == workload:
-            best = d
+            best, src = d, f
     if best is None:
-        return None
+        return None, None
     tot, seen = 0.0, False
     for pat in PMC_KERNELS[kernel]:
         for name, v in best["kernels"].items():
             if pat in name:
                 tot += v["bytes"]
                 seen = True
-    return tot if seen else None
+    if not seen:
+        return None, None
+    return tot, {"file": os.path.relpath(src, ROOT), "command": best.get("command"), "commit": best.get("commit")}
 
 
 def build_workload(name, seed, device):
@@ -105,12 +128,45 @@ def build_workload(name, seed, device):
     return dict(n=n, pairs=(i, j, c), adj=adj, truth=truth, x=x)
 
 
-def cpu_baseline(wl, seed, steps=2, warmup=1):
-    """The oracle (plain-torch restatement of the reference CPU path) on the same workload."""
+def build_selftest_workload(seed, n=400):
+    """A small CPU workload for --selftest-cpu (no GPU, no oracle: T is any symmetric target)."""
+    import hicgat
+    from hicgat import synth
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=seed)
+    adj = hicgat.Adj(torch.tensor(i), torch.tensor(j), None, (n, n)).to_symmetric().to("cpu")
+    A = np.zeros((n, n))
+    A[i, j] = c
+    A[j, i] = c
+    with np.errstate(divide="ignore"):
+        t = np.where(A > 0, A ** -0.5, 0.0)
+    t[A == 0] = t.max()
+    np.fill_diagonal(t, 0.0)
+    truth = hicgat.Truth(torch.tensor(t / t.max(), dtype=torch.float32))
+    x = torch.tensor(synth.features(n, seed=seed))
+    return dict(n=n, pairs=(i, j, c), adj=adj, truth=truth, x=x)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(wl, seed, steps=5, warmup=2):
+    """The oracle (plain-torch restatement of the reference CPU path) on the same workload:
+    ``steps`` timed steps after ``warmup``, median step time (SURVEY 8(d) 'CPU baseline')."""
     from oracle import gat as og
     from oracle import graph as ogr
     from oracle import loop as ol
     from hicgat import synth
+    # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool) or the affinity mask
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
     n = wl["n"]
     i, j, c = wl["pairs"]
     rows = np.concatenate([i, j])
@@ -128,19 +184,47 @@ def cpu_baseline(wl, seed, steps=2, warmup=1):
     x = torch.tensor(synth.features(n, seed=seed))
     torch.manual_seed(0)
     model = og.GATNetSelectiveResidualsUpdated()
-    times = []
+    marks = [time.perf_counter()]
 
     def on_step(k, lv):
-        times.append(time.perf_counter())
-        log(f"[cpu] step {k} loss {lv:.6g}")
+        marks.append(time.perf_counter())
+        log(f"[cpu] step {k} loss {lv:.6g} ({marks[-1] - marks[-2]:.2f} s)")
 
-    t0 = time.perf_counter()
     ol.train(model, x, adj, truth, steps=warmup + steps, on_step=on_step)
-    dt = times[-1] - times[warmup - 1] if warmup > 0 else times[-1] - t0
-    return dict(value=steps / dt, unit="steps/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{steps} timed steps (after {warmup} warm-up) of the full {n}-node step "
-                       f"(oracle GATNetSelectiveResidualsUpdated, fwd+MSE+bwd+Adam, "
-                       f"{torch.get_num_threads()} threads, {os.cpu_count()} host CPUs visible)")
+    per = np.diff(marks)[warmup:]
+    med = float(np.median(per))
+    return dict(value=1.0 / med, unit="steps/s", cores=threads, kind="port",
+                median_s_per_step=med, step_s=[float(v) for v in per], cpu_model=_cpu_model(),
+                host_cpus_visible=os.cpu_count(),
+                sample=f"median of {steps} timed steps (after {warmup} warm-up) of the full {n}-node step "
+                       f"(oracle GATNetSelectiveResidualsUpdated, fwd+MSE+bwd+Adam, torch CPU, "
+                       f"{threads} threads = the box's CPU share (OMP_NUM_THREADS), {os.cpu_count()} host CPUs "
+                       f"visible, {_cpu_model()})")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """``python bench.py --gpus N`` without a torch.distributed.run environment: start one as a
+    child process (no GPU call has happened in this process) and return its exit code."""
+    if not args.selftest_cpu:
+        have = torch.cuda.device_count()      # does not initialise the GPU on this image
+        if have < args.gpus:
+            log(f"[bench] --gpus {args.gpus} but only {have} GPU(s) visible")
+            print(json.dumps({"error": f"--gpus {args.gpus} needs {args.gpus} GPUs, {have} visible",
+                              "n_gpus": args.gpus}), flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -154,38 +238,66 @@ def main():
                     choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
                     help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
                          "N > 1 shards the GAT models only")
+    ap.add_argument("--dist-mode", default="allgather", choices=["allgather", "replicate"],
+                    help="N > 1: all-gather h each step (default) or replicate x and recompute h on every rank "
+                         "(the SURVEY 8(e) ablation)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the step as one "
-                         "captured hipGraph (the default; at N > 1 the graph holds the RCCL collectives too; the "
-                         "per-kernel timing then comes from an eager pass of the same length right after the "
-                         "timed region)")
+                         "captured hipGraph (the default; at N > 1 the graph holds the RCCL collectives too)")
     ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
+    ap.add_argument("--selftest-cpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    args.graph = not args.eager
+    args.graph = not args.eager and not args.selftest_cpu
 
-    import hicgat
-    from hicgat import kernels
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    if world != args.gpus:
+        log(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}")
+        sys.exit(2)
 
-    wl = build_workload(args.workload, args.seed, dev)
+    import hicgat
+    from hicgat import kernels
+    if args.selftest_cpu:
+        import torch.distributed as dist
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from cpu_kernels import CpuKernels, torch_tail   # test stand-ins (tests/), never the product
+        torch.set_num_threads(1)
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("gloo")
+        torch_tail(hicgat)
+        dev = torch.device("cpu")
+        wl = build_selftest_workload(args.seed)
+        kern = CpuKernels()
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=dev)
+        wl = build_workload(args.workload, args.seed, dev)
+        kern = None
     torch.manual_seed(0)
     model = hicgat.MODELS[args.model]().to(dev)
     if world > 1 and args.model == "Net":
         raise SystemExit("the sharded step covers the GAT models (Net is the single-GPU f1 baseline)")
-    if world > 1:
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    graph_error = None
+    if world > 1 or args.selftest_cpu:
         from hicgat import dist as hdist
-        runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss)
+        runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss, kern=kern,
+                                      replicate_x=args.dist_mode == "replicate")
+        wl["truth"] = None                      # each rank keeps only its band (runner.tband)
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         step = runner.step
     else:
         opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
@@ -198,9 +310,10 @@ def main():
     if args.graph and world > 1:
         try:
             step = runner.captured(warmup=max(1, args.warmup))   # kernels + RCCL collectives in one graph
-        except RuntimeError as exc:   # keep a number on record: eager RCCL steps instead of the graph
-            log(f"[bench] rank {rank}: graph capture of the sharded step failed ({exc}); timing eager steps")
-            torch.cuda.synchronize()
+        except RuntimeError as exc:   # recorded in the JSON line ("graph": false, "graph_error")
+            graph_error = f"{type(exc).__name__}: {exc}"
+            log(f"[bench] rank {rank}: GRAPH CAPTURE OF THE SHARDED STEP FAILED ({exc}); timing eager steps")
+            sync()
             args.graph = False
             for w in range(args.warmup):
                 step()
@@ -210,64 +323,80 @@ def main():
     else:
         for w in range(args.warmup):
             step()
-    torch.cuda.synchronize()
-    if world > 1:
+    sync()
+    if world > 1 or args.selftest_cpu:
         torch.distributed.barrier()
     log(f"[bench] warmup done ({args.warmup} steps)")
 
-    if not args.graph:
-        kernels.TIMERS = {}
-    torch.cuda.synchronize()
-    if world > 1:
+    kernels.TIMERS = None
+    timed_events = dev.type == "cuda"
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if timed_events else []
+    sync()
+    if world > 1 or args.selftest_cpu:
         torch.distributed.barrier()
     t0 = time.perf_counter()
+    if timed_events:
+        evs[0].record()
     for k in range(args.steps):
         loss = step()[0]
-    torch.cuda.synchronize()
+        if timed_events:
+            evs[k + 1].record()
+    sync()
     t1 = time.perf_counter()
-    if world > 1:
+    if world > 1 or args.selftest_cpu:
         torch.distributed.barrier()
-    if args.graph:
-        kernels.TIMERS = {}
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)] if timed_events else []
+    # per-kernel HIP events: an eager pass of the same length right after the timed region
+    kernels.TIMERS = {} if timed_events else None
+    if timed_events:
         for k in range(args.steps):
             eager_step()
-        torch.cuda.synchronize()
-    timers, kernels.TIMERS = kernels.TIMERS, None
+        sync()
+    timers, kernels.TIMERS = kernels.TIMERS or {}, None
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1 or args.selftest_cpu:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     loss_v = float(loss.item())
 
-    kern = {}
-    for name, evs in timers.items():
-        ms = [a.elapsed_time(b) for a, b in evs]
-        kern[name] = dict(launches=len(ms), avg_ms=float(np.mean(ms)), total_ms=float(np.sum(ms)))
+    kern_t = {}
+    for name, ev in timers.items():
+        ms = [a.elapsed_time(b) for a, b in ev]
+        kern_t[name] = dict(launches=len(ms), avg_ms=float(np.mean(ms)), total_ms=float(np.sum(ms)))
     n, nnz = wl["n"], wl["adj"].device_nnz
-    if world > 1:
-        nnz = runner.local_nnz
-        n_loc = runner.local_rows
-    else:
-        n_loc = n
+    sharded = world > 1 or args.selftest_cpu
+    n_loc = runner.local_rows if sharded else n
+    nnz_loc = runner.local_nnz if sharded else nnz
     cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "sage_agg",
-                         "pairdist_mse_fused") if k in kern]
-    dom = max(cands, key=lambda k: kern[k]["total_ms"])
+                         "pairdist_mse_fused") if k in kern_t]
+    roof = None
+    if cands:
+        dom = max(cands, key=lambda k: kern_t[k]["total_ms"])
 
-    def per_launch(k, b):
-        """A pass split into row chunks (the source pass, ops._src_chunks) is several launches per
-        step over near-equal row ranges: each launch's algorithmic bytes are the pass's share."""
-        return b / max(1.0, kern[k]["launches"] / args.steps)
-    if dom == "pairdist_mse_fused":
-        alg = agg_bytes(dom, n, nnz) / (world if world > 1 else 1)
-    else:
-        alg = per_launch(dom, agg_bytes(dom, n_loc, nnz))
-    achieved = alg / (kern[dom]["avg_ms"] * 1e-3) / 1e9
-    for k in cands:
-        b = per_launch(k, agg_bytes(k, n if k == "pairdist_mse_fused" else n_loc, nnz))
-        kern[k]["alg_GBps"] = b / (kern[k]["avg_ms"] * 1e-3) / 1e9
+        def per_launch(k, b):
+            """A pass split into row chunks (ops._src_chunks) is several launches per step: each
+            launch's algorithmic bytes are its share."""
+            return b / max(1.0, kern_t[k]["launches"] / args.steps)
 
-    traffic = pmc_traffic(dom, args.workload) if world == 1 else None
+        for k in cands:
+            b = agg_bytes(k, n, nnz) / world if k == "pairdist_mse_fused" else per_launch(k, agg_bytes(k, n_loc, nnz_loc))
+            kern_t[k]["alg_bytes"] = b
+            kern_t[k]["alg_GBps"] = b / (kern_t[k]["avg_ms"] * 1e-3) / 1e9
+        avg = kern_t[dom]["avg_ms"]
+        traffic, src = pmc_traffic(dom, args.workload) if world == 1 else (None, None)
+        achieved = traffic / (avg * 1e-3) / 1e9 if traffic else None
+        roof = {"bound": "hbm", "kernel": dom,
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "traffic": traffic, "traffic_source": src,
+                "avg_launch_ms": avg, "launches_per_step": kern_t[dom]["launches"] / args.steps,
+                "alg_bytes_per_launch": kern_t[dom]["alg_bytes"], "alg_GBps": kern_t[dom]["alg_GBps"],
+                "l2_peak": L2_PEAK_GBS, "l2_frac": kern_t[dom]["alg_GBps"] / L2_PEAK_GBS,
+                "note": "achieved/frac: PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) per launch "
+                        "/ avg launch time vs 8 TB/s; alg_GBps: SURVEY 8(d) no-reuse bytes (every edge reads a "
+                        "whole neighbour row) / time, bounded by the L2 (l2_frac), not HBM"}
+
     result = {
         "metric": f"training steps/sec ({args.model}, fwd+loss+bwd+Adam)",
         "value": args.steps / elapsed,
@@ -276,36 +405,37 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
+        "median_ms_per_step": float(np.median(step_ms)) if step_ms else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
+        "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)"
+                if not args.selftest_cpu else "SELFTEST: CPU gloo ranks + torch stand-in kernels, 400 nodes -- not a measurement",
         "graph": bool(args.graph),
-        "config": {"workload": args.workload, "model": args.model,
-                   "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz, "d": D_FEAT, "heads": HEADS,
-                   "loss": args.loss, "parallelism": f"dst-row shard x{world}" if world > 1 else "single",
-                   "gemm": {0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl],
-                   "aggregation": (f"xcd column strips x{kernels.default().slice_width}"
-                                   if kernels.default().slice_width else "row per wave")},
+        "model": args.model,
+        "config": {"workload": args.workload if not args.selftest_cpu else "selftest-400",
+                   "n_nodes": n, "nnz_with_self_loops": nnz, "d": D_FEAT, "heads": HEADS,
+                   "loss": args.loss,
+                   "parallelism": (f"dst-row shard x{world} (nnz-balanced, {args.dist_mode})" if sharded else "single"),
+                   "gemm": ({0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl]
+                            if not args.selftest_cpu else "cpu stand-in")},
         "final_loss": loss_v,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "alg_bytes_per_launch": alg, "avg_launch_ms": kern[dom]["avg_ms"],
-                     "launches_per_step": kern[dom]["launches"] / args.steps,
-                     # the HBM bytes the kernel really moves (PMC) over the same launch time: frac > 1
-                     # above because the gathered rows are largely L2 / Infinity-Cache hits
-                     "traffic_GBps": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 if traffic else None,
-                     "traffic_frac": traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None},
-        "kernels": kern,
+        "roofline": roof,
+        "kernels": kern_t,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "GATNetSelectiveResidualsUpdated":
+    if sharded:
+        result["shard"] = {"rows_per_rank": [int(v) for v in runner.plan.counts],
+                           "nnz_per_rank": [int(v) for v in runner.plan.nnz]}
+    if graph_error is not None:
+        result["graph_error"] = graph_error
+    if rank == 0 and world == 1 and not args.selftest_cpu and not args.no_cpu_baseline \
+            and args.model == "GATNetSelectiveResidualsUpdated":
         log("[bench] cpu baseline (oracle) ...")
-        result["cpu_baseline"] = cpu_baseline(wl, args.seed, steps=args.cpu_steps)
+        result["cpu_baseline"] = cpu_baseline(wl, args.seed, steps=args.cpu_steps, warmup=args.cpu_warmup)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or args.selftest_cpu:
         torch.distributed.destroy_process_group()
 
 

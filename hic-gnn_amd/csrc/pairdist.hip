@@ -11,6 +11,7 @@
 // w*(c_i - c_j) into row partials (reduced over the 16 tx lanes) and column partials (reduced over
 // ty through LDS).  Partials go to a [tile][2][128] float4 slab and a second kernel adds, per row,
 // the slabs of every tile touching it in a fixed order: bitwise reproducible, no float atomics.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -68,7 +69,8 @@ struct TileAcc {
 // no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
 // w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
 template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1>
-__device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int N, int I, int J,
+__device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int64_t row0, int64_t col0,
+                                          int N, int I, int J,
                                           const float *tile, const float (*sc)[BT][3], int tx, int ty,
                                           const float *cx, const float *cy, const float *cz, const int *gj,
                                           float4 *__restrict__ prow, TileAcc &A) {
@@ -84,7 +86,7 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
       tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
       tv[4] = b.x; tv[5] = b.y; tv[6] = b.z; tv[7] = b.w;
     } else if (gi < N) {
-      const float *trow = T + (size_t)gi * ldt + (size_t)J * BT;
+      const float *trow = T + (size_t)(gi - row0) * ldt + (size_t)((int64_t)J * BT - col0);
 #pragma unroll
       for (int q = 0; q < 8; ++q) tv[q] = gj[q] < N ? trow[tx * 4 + (q & 3) + (q >> 2) * 64] : 0.f;
     } else {
@@ -229,7 +231,8 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
 template <int MODE, bool VEC, bool PEARSON>
 __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
-                                                            int64_t ldt, int nb, int64_t t0,
+                                                            int64_t ldt, int64_t row0, int64_t col0,
+                                                            int nb, int64_t t0,
                                                             float4 *__restrict__ part,
                                                             double *__restrict__ mom) {
   // one dynamic LDS array: [T tile 128x128 fp32 (VEC only)] -- 64 KiB, 16-B aligned
@@ -264,12 +267,13 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
     // tile rows, wave-uniform LDS base + lane*16), each wave only the 32 rows its threads read:
     // rows 16w .. 16w+15 (k = 0..3 of tile_rows) first, then 64+16w .. 64+16w+15 (k = 4..7), so the
     // first half is computed while the second is in flight.  Rows past N are clamped to a valid row
-    // (their values are masked); columns past N lie inside the padded leading dimension.
+    // (their values are masked); columns past N lie inside the padded leading dimension.  T may be
+    // a band of the truth (rows from row0, columns from col0: a rank's share, hicgat.dist).
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int r0 = (q < 8 ? 0 : 64) + wv * 16 + (q & 7) * 2;
       const int gi = min(I * BT + r0 + (lane >> 5), N - 1);
-      const float *src = T + (size_t)gi * ldt + (size_t)J * BT + (lane & 31) * 4;
+      const float *src = T + (size_t)(gi - row0) * ldt + (size_t)((int64_t)J * BT - col0) + (lane & 31) * 4;
       __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
     }
   }
@@ -296,16 +300,16 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   constexpr bool PK = VEC && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
   if (interior) {
     if constexpr (PK) tile_rows_pk<PEARSON, 0, 4>(tile, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
   if (interior) {
     if constexpr (PK) tile_rows_pk<PEARSON, 4, 8>(tile, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 4, 8>(T, ldt, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 4, 8>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   }
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
@@ -477,16 +481,27 @@ using namespace hicgat;
 
 constexpr size_t kTileLds = (size_t)BT * BT * sizeof(float);  // LDS image of one T tile
 
+// mode: HICGAT_PD_TRI (1) = the upper-triangle tiling of the fused loss, HICGAT_PD_SQUARE (0) =
+// the square tiling of the backward -- one convention for both queries (include/hicgat.h).
 extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
   if (N <= 0) return 0;
   const int64_t nb = pd_nb(N);
-  return mode == MODE_SYM ? nb * (nb + 1) / 2 : nb * nb;
+  return mode == HICGAT_PD_TRI ? nb * (nb + 1) / 2 : nb * nb;
 }
 
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
-  // mode 1 (fused, triangular tiles) and mode 0 (backward, square tiles) of the public API.
-  const int64_t tiles = hicgat_pairdist_num_tiles(N, mode == 1 ? MODE_SYM : MODE_FULL);
+  const int64_t tiles = hicgat_pairdist_num_tiles(N, mode);
   return (size_t)tiles * (2 * BT * sizeof(float4) + 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) + 256;
+}
+
+// Host twin of tri_decode (exact integer search): tile-row of upper-triangle tile t.
+static int tri_row_host(int64_t t, int nb) {
+  int lo = 0, hi = nb - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (tri_start(mid, nb) <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 static void carve(void *ws, int64_t tiles, float4 **part, double **mom) {
@@ -512,7 +527,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   if (N < 0 || ldg < N) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !G || !dcoords || !workspace) return HICGAT_EINVAL;
-  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, 0)) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, HICGAT_PD_SQUARE)) return HICGAT_EINVAL;
   const int nb = pd_nb(N);
   const int64_t tiles = (int64_t)nb * nb;
   float4 *part;
@@ -522,10 +537,10 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
                    ldg >= (int64_t)nb * BT;
   if (vec)
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true, false>), dim3(tiles), dim3(256), kTileLds,
-                       (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
+                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom);
   else
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false, false>), dim3(tiles), dim3(256), 0,
-                       (hipStream_t)stream, coords, G, N, ldg, nb, (int64_t)0, part, mom);
+                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
@@ -534,34 +549,43 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   return HICGAT_OK;
 }
 
-extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
-                                         int64_t tile_begin, int64_t tile_end, int loss_kind,
-                                         double *stats, float *loss, float *dcoords,
-                                         void *workspace, size_t workspace_bytes,
-                                         hicgat_stream_t stream) {
-  if (N < 0 || ldt < N || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *T, int N, int64_t ldt,
+                                              int64_t t_row0, int64_t t_rows, int64_t t_col0,
+                                              int64_t tile_begin, int64_t tile_end, int loss_kind,
+                                              double *stats, float *loss, float *dcoords, void *workspace,
+                                              size_t workspace_bytes, hicgat_stream_t stream) {
+  if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !T || !stats || !workspace) return HICGAT_EINVAL;
-  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, 1)) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, HICGAT_PD_TRI)) return HICGAT_EINVAL;
   const int nb = pd_nb(N);
   const int64_t tiles = (int64_t)nb * (nb + 1) / 2;
   if (tile_end < 0 || tile_end > tiles) tile_end = tiles;
   if (tile_begin < 0) tile_begin = 0;
   if (tile_begin > tile_end) return HICGAT_EINVAL;
+  const int64_t nt = tile_end - tile_begin;
+  if (nt > 0) {
+    // the band must hold every row / column the tile range reads: rows of tile-rows I0..I1 and
+    // columns from I0's diagonal tile on (tiles (I, J) have J >= I >= I0)
+    const int64_t I0 = tri_row_host(tile_begin, nb), I1 = tri_row_host(tile_end - 1, nb);
+    const int64_t need_r1 = std::min<int64_t>(N, (I1 + 1) * BT);
+    if (t_row0 < 0 || t_col0 < 0 || t_row0 > I0 * BT || t_col0 > I0 * BT || t_row0 + t_rows < need_r1 ||
+        ldt < (int64_t)N - t_col0)
+      return HICGAT_EINVAL;
+  }
   float4 *part;
   double *mom;
   carve(workspace, tiles, &part, &mom);
-  const int64_t nt = tile_end - tile_begin;
   // HICGAT_PD_NOLDS=1 (A/B measurement only): read T straight into registers instead of the
   // LDS-DMA tile image
   static const bool nolds = getenv("HICGAT_PD_NOLDS") && atoi(getenv("HICGAT_PD_NOLDS")) != 0;
-  const bool vec = !nolds && (ldt % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
-                   ldt >= (int64_t)nb * BT;
+  const bool vec = !nolds && (ldt % 4 == 0) && (t_col0 % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+                   ldt >= (int64_t)nb * BT - t_col0;
   if (nt > 0) {
     // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only
 #define HICGAT_PD_SYM(V, P)                                                                          \
   hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, P>), dim3(nt), dim3(256), V ? kTileLds : 0, \
-                     (hipStream_t)stream, coords, T, N, ldt, nb, tile_begin, part, mom)
+                     (hipStream_t)stream, coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, part, mom)
     if (vec && loss_kind == 1) HICGAT_PD_SYM(true, true);
     else if (vec) HICGAT_PD_SYM(true, false);
     else if (loss_kind == 1) HICGAT_PD_SYM(false, true);
@@ -586,6 +610,16 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
                      stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
+                                         int64_t tile_begin, int64_t tile_end, int loss_kind,
+                                         double *stats, float *loss, float *dcoords,
+                                         void *workspace, size_t workspace_bytes,
+                                         hicgat_stream_t stream) {
+  if (ldt < N) return HICGAT_EINVAL;
+  return hicgat_pairdist_mse_fused_band(coords, T, N, ldt, 0, N, 0, tile_begin, tile_end, loss_kind, stats, loss,
+                                        dcoords, workspace, workspace_bytes, stream);
 }
 
 extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss,

@@ -38,18 +38,6 @@ SIGNATURES = {
                                           c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
-    "hicgat_gat_sliced_workspace_bytes": (c_sz, [c_int, c_int, c_int, c_int]),
-    "hicgat_gat_agg_fwd_sliced": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p,
-                                          c_p, c_f, c_int, c_int, c_p, c_p, c_p, c_p, c_sz, c_p]),
-    "hicgat_gat_agg_bwd_src_sliced": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p,
-                                              c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_int, c_p, c_p, c_p,
-                                              c_sz, c_p]),
-    "hicgat_gat_blk_workspace_bytes": (c_sz, [c_int, c_int]),
-    "hicgat_gat_blk_fwd": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p,
-                                   c_p, c_p, c_f, c_int, c_p, c_p, c_p, c_p, c_sz, c_p]),
-    "hicgat_gat_blk_bwd_src": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
-                                       c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p, c_sz,
-                                       c_p]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),
@@ -57,6 +45,8 @@ SIGNATURES = {
     "hicgat_pairdist_bwd": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_mse_fused": (c_int, [c_p, c_p, c_int, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_p,
                                           c_p, c_sz, c_p]),
+    "hicgat_pairdist_mse_fused_band": (c_int, [c_p, c_p, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int,
+                                               c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_finalize": (c_int, [c_int, c_int, c_p, c_p, c_p]),
     "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
     "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),

@@ -87,8 +87,10 @@ def main(argv=None):
                                             "(HiC_GAT_generalize_directly.py flags).")
     p.add_argument("list_trained")
     p.add_argument("list_untrained")
-    p.add_argument("embeddings_trained", help="N1 x F text file (np.loadtxt)")
-    p.add_argument("embeddings_untrained", help="N2 x F text file (np.loadtxt)")
+    p.add_argument("embeddings_trained", help="N1 x F text file (np.loadtxt), or 'node2vec': generated on the GPU "
+                                              "from the zero-diagonal contact matrix (:148-160)")
+    p.add_argument("embeddings_untrained", help="N2 x F text file, or 'node2vec' (:162-173)")
+    p.add_argument("--seed", type=int, default=42, help="node2vec seed (the reference's Node2Vec(seed=42))")
     p.add_argument("-lr", "--learningrate", type=float, default=0.001)
     p.add_argument("-thresh", "--loss_diff_threshold", type=float, default=1e-8)
     p.add_argument("--conversion", type=float, default=1.0)
@@ -98,12 +100,17 @@ def main(argv=None):
     p.add_argument("--out", default=None, help="prefix for the weights / PDB / log files")
     a = p.parse_args(argv)
     l1, l2 = np.loadtxt(a.list_trained), np.loadtxt(a.list_untrained)
-    e1, e2 = np.loadtxt(a.embeddings_trained), np.loadtxt(a.embeddings_untrained)
-    normed = []
-    for lst in (l1, l2):
+    normed, emb = [], []
+    for lst, src in ((l1, a.embeddings_trained), (l2, a.embeddings_untrained)):
         m = graph.convert_to_matrix(lst)
-        np.fill_diagonal(m, 0)
+        np.fill_diagonal(m, 0)                  # :113-126 (the saved *_matrix.txt)
+        if src == "node2vec":                   # node2vec on that zero-diagonal matrix (:150-173)
+            from .embed import node2vec
+            emb.append(node2vec(m, seed=a.seed).cpu().numpy())
+        else:
+            emb.append(np.loadtxt(src))
         normed.append(kr.KRnorm(m)[0].cpu().numpy())
+    e1, e2 = emb
     model = MODELS[a.model]().cuda()
     if a.weights and os.path.isfile(a.weights):
         model.load_state_dict(torch.load(a.weights, weights_only=True))
@@ -113,7 +120,7 @@ def main(argv=None):
         _, hist = train.train(model, data, truth, a.learningrate, a.loss_diff_threshold, a.steps, "combined")
         print(f"trained {len(hist)} steps, final loss {hist[-1]:.6g}")
         if a.weights:
-            torch.save(model.state_dict(), a.weights)
+            torch.save(train.cpu_state_dict(model), a.weights)
     rho, coords = generalize(model, l1, l2, e1, e2, normed[1], a.conversion)
     print(f"Optimal dSCC for generalized data: {rho}")
     if a.out:

@@ -218,7 +218,19 @@ class Truth:
     """fp32 target for the fused distance/MSE kernel: [N, ld] with ld = ceil(N/128)*128.
 
     ``Truth.from_contacts(y, factor)`` runs cont2dist straight into the padded buffer;
-    ``Truth(t)`` copies an existing [N, N] target (``truth.float()`` of the reference loop)."""
+    ``Truth(t)`` copies an existing [N, N] target (``truth.float()`` of the reference loop).
+
+    The fused kernel reads only the upper-triangle tiles (one T read per pair).  A target that is
+    not exactly symmetric -- R's KR scaling forms (x_i A_ij) x_j and (x_j A_ji) x_i, which can round
+    apart (r_utils.R:74-89), and the reference's MSELoss simply proceeds -- is stored in the
+    equivalent symmetric form: for every pair, with d_ij = d_ji and tbar = (T_ij + T_ji)/2,
+      (d - T_ij)^2 + (d - T_ji)^2 = 2 (d - tbar)^2 + (T_ij - T_ji)^2 / 2,
+    so the off-diagonal becomes tbar (same gradient) and the constant (T_ij - T_ji)^2 / 2 of row i's
+    pairs j > i is folded into the diagonal, whose only role is the (0 - T_ii)^2 term of the MSE
+    (cdist's diagonal is 0 and carries no gradient): T'_ii = sqrt(T_ii^2 + sum_j>i (T_ij - T_ji)^2/2).
+    The MSE value and its gradient are unchanged (to fp32 rounding); ``asymmetric_source`` records it.
+    The combined loss's Pearson term then sees tbar on the upper triangle (a relative change of
+    the order of the asymmetry, 1e-7 for R's rounding)."""
 
     def __init__(self, t=None, *, _buf=None, _n=None):
         if _buf is None:
@@ -230,7 +242,17 @@ class Truth:
             buf, n = _buf, _n
         self.buf, self.n, self.ld = buf, n, buf.shape[1]
         view = buf[:, :n]
-        self.symmetric = bool(torch.equal(view, view.t()))
+        self.asymmetric_source = not bool(torch.equal(view, view.t()))
+        if self.asymmetric_source:
+            self._symmetrise()
+        self.symmetric = True
+
+    def _symmetrise(self):
+        t = self.buf[:, :self.n].double()
+        diff2 = torch.triu((t - t.t()) ** 2, 1).sum(1) * 0.5
+        sym = (t + t.t()) * 0.5
+        sym.diagonal().copy_(torch.sqrt(t.diagonal() ** 2 + diff2))
+        self.buf[:, :self.n] = sym.float()
 
     @classmethod
     def from_contacts(cls, y, factor):
@@ -247,67 +269,3 @@ class Truth:
 
     def dense(self):
         return self.buf[:, :self.n]
-
-
-# ---- row-block structure of the GAT aggregation (csrc/gat_block.hip) ----------------------------
-BLOCK_ROWS = 16
-
-
-def block_csr(rowptr, col, r0, r1, R=BLOCK_ROWS):
-    """Static block structure of CSR rows [r0, r1) for the row-block aggregation kernels.
-
-    Rows are cut into blocks of R consecutive rows (block b = rows r0 + R b ...).  Within a
-    block the edges are ordered by (source j, row); a "run" is one source j of a block with the
-    R-bit mask of the block rows that have the edge (i, j).  Returns numpy arrays:
-      runs    int64 [U]          j | (mask << 32), sorted by (block, j)
-      run_ptr int32 [nblk + 1]   block b's runs are runs[run_ptr[b]:run_ptr[b+1]]
-      pos     int32 [E]          pos[e - rowptr[r0]] = block-order position of CSR edge e,
-                                 relative to rowptr[r0] (a permutation of each block's own range)
-    """
-    rowptr = np.asarray(rowptr, dtype=np.int64)
-    col = np.asarray(col, dtype=np.int64)
-    if not (0 <= r0 <= r1 <= rowptr.shape[0] - 1):
-        raise ValueError("block_csr: bad row range")
-    if R > 32:
-        raise ValueError("block_csr: at most 32 rows per block")
-    e0, e1 = int(rowptr[r0]), int(rowptr[r1])
-    nrow = r1 - r0
-    nblk = -(-nrow // R)
-    deg = np.diff(rowptr[r0:r1 + 1])
-    lrow = np.repeat(np.arange(nrow, dtype=np.int64), deg)
-    blk = lrow // R
-    lr = lrow % R
-    j = col[e0:e1]
-    order = np.lexsort((lr, j, blk))          # primary: block, then j, then row
-    pos = np.empty(e1 - e0, dtype=np.int32)
-    pos[order] = np.arange(e1 - e0, dtype=np.int32)
-    sb, sj, slr = blk[order], j[order], lr[order]
-    if e1 > e0:
-        starts = np.flatnonzero(np.r_[True, (sb[1:] != sb[:-1]) | (sj[1:] != sj[:-1])])
-        mask = np.bitwise_or.reduceat(np.left_shift(np.int64(1), slr), starts)
-        runs = sj[starts] | (mask << 32)
-        run_blk = sb[starts]
-    else:
-        runs = np.zeros(0, dtype=np.int64)
-        run_blk = np.zeros(0, dtype=np.int64)
-    run_ptr = np.searchsorted(run_blk, np.arange(nblk + 1), side="left").astype(np.int32)
-    return runs.astype(np.int64), run_ptr, pos
-
-
-_BLOCK_CACHE = {}
-
-
-def device_block_csr(rowptr, col, r0, r1):
-    """``block_csr`` of the device CSR (rowptr32, col32) for rows [r0, r1), built once on the host
-    and cached on the device.  The cache entry holds the CSR tensors themselves, so their memory
-    (the cache key) cannot be reused by another graph while the entry lives.  The first call for a
-    graph copies the CSR to the host: make it before a hipGraph capture (a warm-up step does)."""
-    key = (rowptr.data_ptr(), rowptr.numel(), col.data_ptr(), col.numel(), int(r0), int(r1), str(rowptr.device))
-    ent = _BLOCK_CACHE.get(key)
-    if ent is None:
-        runs, run_ptr, pos = block_csr(rowptr.cpu().numpy(), col.cpu().numpy(), r0, r1)
-        dev = rowptr.device
-        ent = (rowptr, col, torch.from_numpy(runs).to(dev), torch.from_numpy(run_ptr).to(dev),
-               torch.from_numpy(pos).to(dev))
-        _BLOCK_CACHE[key] = ent
-    return ent[2], ent[3], ent[4]

@@ -13,12 +13,10 @@ from . import _lib
 
 # name -> list of (start, end) torch.cuda.Event pairs recorded around launches (bench.py)
 TIMERS = None
-SLICE_DEFAULT = 0
 GEMM_IMPLS = {"auto": 0, "f32": 1, "x3": 2}
 # the product default is the plain fp32 MFMA GEMM; HICGAT_GEMM=auto opts into the fp32-accurate x3
 # split where it applies (10-25 % faster GEMMs, profiles/r01_kbench_x3_sliced.txt)
 GEMM_DEFAULT = "f32"
-AGG_DEFAULT = "row"
 
 
 class _timed:
@@ -45,23 +43,9 @@ class HipKernels:
 
     def __init__(self):
         self.lib = _lib.lib()
-        # column-strip width of the XCD-sliced aggregation kernels (csrc/gat_sliced.hip); 0 = the
-        # row-per-wave kernels (gat_fwd.hip / gat_bwd.hip)
-        self.slice_width = int(os.environ.get("HICGAT_SLICE", str(SLICE_DEFAULT)))
         # matrix-core arithmetic of the GEMMs (include/hicgat.h HICGAT_GEMM_*): 0 auto (x3 where
         # supported), 1 fp32 MFMA only, 2 x3 only
         self.gemm_impl = GEMM_IMPLS[os.environ.get("HICGAT_GEMM", GEMM_DEFAULT)]
-        # aggregation form: "row" = one wave per row (gat_fwd.hip / gat_bwd.hip), "block" = 16-row
-        # blocks over the union of their neighbour lists (gat_block.hip); the strips above win
-        self.agg_form = os.environ.get("HICGAT_AGG", AGG_DEFAULT)
-        if self.agg_form not in ("row", "block"):
-            raise ValueError(f"HICGAT_AGG must be 'row' or 'block', got {self.agg_form!r}")
-
-    def _blk(self, rowptr, col, r0, r1, N, device):
-        from .graph import device_block_csr
-        runs, run_ptr, pos = device_block_csr(rowptr, col, r0, r1)
-        ws = _lib.workspace(self.lib.hicgat_gat_blk_workspace_bytes(N, col.numel()), device)
-        return runs, run_ptr, pos, ws
 
     # -- a2 ---------------------------------------------------------------------------------------
     def linear_att(self, x, W, att_l, att_r, h=None):
@@ -98,8 +82,6 @@ class HipKernels:
 
     # -- a4 + a5 ----------------------------------------------------------------------------------
     def agg_fwd(self, rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, out, row_stats):
-        if self.slice_width or self.agg_form == "block":
-            return self.agg_fwd_act(rowptr, col, r0, r1, h, a_src, a_dst, bias, ns, 0, out, None, row_stats)
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
@@ -113,23 +95,6 @@ class HipKernels:
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
-        if self.slice_width:
-            nnz = col.numel()
-            ws = _lib.workspace(self.lib.hicgat_gat_sliced_workspace_bytes(N, nnz, H, self.slice_width), h.device)
-            with _timed("gat_agg_fwd"):
-                _lib.check(self.lib.hicgat_gat_agg_fwd_sliced(P(rowptr), P(col), N, nnz, H, C, r0, r1, P(h), P(a_src),
-                                                              P(a_dst), P(bias), float(ns), int(act), self.slice_width,
-                                                              P(out), P(out2), P(row_stats), P(ws), ws.numel(),
-                                                              _lib.stream(h.device)), "hicgat_gat_agg_fwd_sliced")
-            return
-        if self.agg_form == "block":
-            runs, run_ptr, pos, ws = self._blk(rowptr, col, r0, r1, N, h.device)
-            with _timed("gat_agg_fwd"):
-                _lib.check(self.lib.hicgat_gat_blk_fwd(P(rowptr), P(col), P(pos), P(runs), P(run_ptr), N, col.numel(),
-                                                       H, C, r0, r1, P(h), P(a_src), P(a_dst), P(bias), float(ns),
-                                                       int(act), P(out), P(out2), P(row_stats), P(ws), ws.numel(),
-                                                       _lib.stream(h.device)), "hicgat_gat_blk_fwd")
-            return
         with _timed("gat_agg_fwd"):
             _lib.check(self.lib.hicgat_gat_agg_fwd_act(P(rowptr), P(col), N, col.numel(), H, C, r0, r1, P(h),
                                                        P(a_src), P(a_dst), P(bias), float(ns), int(act), P(out),
@@ -163,23 +128,6 @@ class HipKernels:
         C = h.shape[1] // H
         # row_stats / dout may be row-strided views (the packed all-gather buffer of hicgat.dist)
         assert row_stats.stride(1) == 1 and dout.stride(1) == 1
-        if self.slice_width:
-            nnz = col.numel()
-            ws = _lib.workspace(self.lib.hicgat_gat_sliced_workspace_bytes(N, nnz, H, self.slice_width), h.device)
-            with _timed("gat_agg_bwd_src"):
-                _lib.check(self.lib.hicgat_gat_agg_bwd_src_sliced(
-                    P(rowptr), P(col), N, nnz, H, C, r0, r1, P(h), P(a_src), P(a_dst), P(row_stats), row_stats.stride(0),
-                    P(dout), dout.stride(0), P(att_l), P(att_r), float(ns), self.slice_width, P(dh), P(da_src), P(ws),
-                    ws.numel(), _lib.stream(h.device)), "hicgat_gat_agg_bwd_src_sliced")
-            return
-        if self.agg_form == "block":
-            runs, run_ptr, pos, ws = self._blk(rowptr, col, r0, r1, N, h.device)
-            with _timed("gat_agg_bwd_src"):
-                _lib.check(self.lib.hicgat_gat_blk_bwd_src(
-                    P(rowptr), P(col), P(pos), P(runs), P(run_ptr), N, col.numel(), H, C, r0, r1, P(h), P(a_src),
-                    P(a_dst), P(row_stats), row_stats.stride(0), P(dout), dout.stride(0), P(att_l), P(att_r),
-                    float(ns), P(dh), P(da_src), P(ws), ws.numel(), _lib.stream(h.device)), "hicgat_gat_blk_bwd_src")
-            return
         with _timed("gat_agg_bwd_src"):
             _lib.check(self.lib.hicgat_gat_agg_bwd_src_ld(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
                                                           P(a_dst), P(row_stats), row_stats.stride(0), P(dout),
@@ -221,16 +169,20 @@ class HipKernels:
         return z
 
     # -- a7..a9 -----------------------------------------------------------------------------------
-    def num_tiles(self, n):
-        return int(self.lib.hicgat_pairdist_num_tiles(n, 0))
+    PD_SQUARE, PD_TRI = 0, 1   # include/hicgat.h HICGAT_PD_*
 
-    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords):
-        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, 1), coords.device)
+    def num_tiles(self, n):
+        """Upper-triangle 128 x 128 tiles of the fused loss (a rank takes a contiguous range)."""
+        return int(self.lib.hicgat_pairdist_num_tiles(n, self.PD_TRI))
+
+    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords, row0=0, col0=0):
+        """``tbuf`` is the truth or a band of it starting at (row0, col0) (hicgat.dist)."""
+        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, self.PD_TRI), coords.device)
         with _timed("pairdist_mse_fused"):
-            _lib.check(self.lib.hicgat_pairdist_mse_fused(P(coords), P(tbuf), n, tbuf.shape[1], int(t0), int(t1),
-                                                          int(kind), P(stats), P(loss), P(dcoords), P(ws),
-                                                          ws.numel(), _lib.stream(coords.device)),
-                       "hicgat_pairdist_mse_fused")
+            _lib.check(self.lib.hicgat_pairdist_mse_fused_band(
+                P(coords), P(tbuf), n, tbuf.shape[1], int(row0), tbuf.shape[0], int(col0), int(t0), int(t1),
+                int(kind), P(stats), P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
+                "hicgat_pairdist_mse_fused_band")
 
     def loss_finalize(self, n, kind, stats, loss):
         _lib.check(self.lib.hicgat_pairdist_finalize(n, int(kind), P(stats), P(loss), _lib.stream(stats.device)),
@@ -246,7 +198,7 @@ class HipKernels:
     def pairdist_bwd(self, coords, G):
         n = coords.shape[0]
         dc = torch.empty_like(coords)
-        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, 0), coords.device)
+        ws = _lib.workspace(self.lib.hicgat_pairdist_workspace_bytes(n, self.PD_SQUARE), coords.device)
         _lib.check(self.lib.hicgat_pairdist_bwd(P(coords), P(G), n, G.shape[1], P(dc), P(ws), ws.numel(),
                                                 _lib.stream(coords.device)), "hicgat_pairdist_bwd")
         return dc

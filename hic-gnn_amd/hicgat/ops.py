@@ -508,12 +508,11 @@ def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
     MSE + alpha*(1 - pearson) [kind="combined", HiC_GAT_generalize_directly.py:219-225] with the
     gradient of the MSE only (the Pearson term is a detached host value in the reference).
 
-    ``truth`` is a ``graph.Truth`` (symmetric).  ``stats`` (float64 [12], device) receives the
-    moments, mse, r, alpha and total (see include/hicgat.h)."""
+    ``truth`` is a ``graph.Truth`` (stored symmetric; an asymmetric target is folded into the
+    equivalent symmetric form there).  ``stats`` (float64 [12], device) receives the moments, mse,
+    r, alpha and total (see include/hicgat.h)."""
     _lib.lib()
     _dev_check(coords)
-    if not truth.symmetric:
-        raise NotImplementedError("fused loss needs a symmetric truth matrix; use pairwise_dist + MSELoss")
     if stats is None:
         stats = torch.empty(12, dtype=torch.float64, device=coords.device)
     kind_i = {"mse": 0, "combined": 1}[kind]

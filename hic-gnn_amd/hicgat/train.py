@@ -54,14 +54,39 @@ def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_
     return opt, hist
 
 
+def cpu_state_dict(model):
+    """The state_dict as plain CPU tensors (no views into FlatAdam's device buffers), so the saved
+    .pt loads with a bare ``torch.load(path)`` on a CPU-only host, as the reference's evaluate /
+    generalise scripts do (evaluate.py:87, HiC_GAT_generalize_directly.py:313)."""
+    return {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+
+
+def parse_conversions(text):
+    """HiC-GNN_main.py:51-58: '[a, step, b]' -> np.arange(a, b, step), '[f]' -> [f]."""
+    conv = ast.literal_eval(text)
+    if len(conv) == 3:
+        return list(np.arange(conv[0], conv[2], conv[1]))
+    if len(conv) == 1:
+        return [conv[0]]
+    raise ValueError("Invalid conversion input.")
+
+
 def main(argv=None):
+    """HiC-GNN_main.py's pipeline: list -> convert_to_matrix -> zero diagonal -> KRnorm ->
+    embeddings -> load_input -> one model per conversion value -> best dSCC -> weights / PDB / log.
+
+    As in the reference (HiC-GNN_main.py:108-132), EVERY conversion value trains a fresh model
+    against ``cont2dist(y, 0.5)`` and is scored against that same truth: the value only labels the
+    run (the reference never passes it to cont2dist); the models differ by their random init (one
+    seed for the whole sweep, the RNG stream continuing from model to model)."""
     p = argparse.ArgumentParser(description="Train a GAT-HiC model on the MI355X path "
                                             "(HiC-GNN_main.py flags).")
     p.add_argument("matrix", help="Hi-C list (bin_i bin_j count) or dense matrix text file")
     p.add_argument("features", help="N x F embedding text file (np.loadtxt), or 'node2vec' to generate the "
-                                    "embeddings on the GPU from the contact matrix (hicgat.embed, the "
-                                    "HiC_GAT_generalize_directly.py:150-155 call)")
-    p.add_argument("-c", "--conversions", default="[.5]", help="conversion factor list, '[a, step, b]' or '[f]'")
+                                    "embeddings on the GPU from the zero-diagonal contact matrix (hicgat.embed, "
+                                    "the HiC_GAT_generalize_directly.py:150-155 call)")
+    p.add_argument("-c", "--conversions", default="[.1,.1,2]", help="conversion list, '[a, step, b]' or '[f]' "
+                                                                    "(HiC-GNN_main.py:33)")
     p.add_argument("-lr", "--learningrate", type=float, default=1e-3)
     p.add_argument("-th", "--threshold", type=float, default=1e-8)
     p.add_argument("--steps", type=int, default=None, help="fixed step count instead of the threshold rule")
@@ -71,42 +96,46 @@ def main(argv=None):
     p.add_argument("--out", default=None, help="prefix for <out>_weights.pt / _structure.pdb / _log.txt")
     p.add_argument("--no-kr", action="store_true", help="the input is already KR-normalised (skip KRnorm)")
     a = p.parse_args(argv)
-    conv = ast.literal_eval(a.conversions)
-    conv = list(np.arange(conv[0], conv[2], conv[1])) if len(conv) == 3 else [conv[0]]
+    conv = parse_conversions(a.conversions)
     mat = np.loadtxt(a.matrix)
     if mat.shape[1] == 3:                       # HiC-GNN_main.py:75-78
+        print("Converting coordinate list format to matrix.")
         mat = graph.convert_to_matrix(mat)
-    if a.features == "node2vec":                # node2vec on the raw contact graph (:150-155)
+    np.fill_diagonal(mat, 0)                    # :80
+    if a.features == "node2vec":                # node2vec on the zero-diagonal contact graph (:150-155)
         from .embed import node2vec
         feats = node2vec(mat, seed=a.seed if a.seed else 42).cpu().numpy()
     else:
         feats = np.loadtxt(a.features).astype(np.float32)
-    np.fill_diagonal(mat, 0)                    # :80
     if not a.no_kr:                             # :85-89 (Rscript normalize.R -> r_utils.R KRnorm)
         from .kr import KRnorm
         normed, keep = KRnorm(mat)
         mat = normed.cpu().numpy()
         feats = feats[keep.cpu().numpy()] if len(keep) != len(feats) else feats
     data = graph.load_input(mat, feats)
-    best = None
+    truth = graph.Truth.from_contacts(data.y, 0.5)     # :120, the same for every conversion
+    torch.manual_seed(a.seed)
+    runs = []
     for f in conv:
-        torch.manual_seed(a.seed)
+        print(f"Training model using conversion value {f}.")
         model = MODELS[a.model]().to(data.x.device)
-        truth = graph.Truth.from_contacts(data.y, f)
         _, hist = train(model, data, truth, a.learningrate, a.threshold, a.steps, a.loss)
         coords = model.get_model(data.x.float(), data.edge_index).detach()
         rho = metrics.dscc(coords, truth.dense())
         print(f"conversion {f}: steps {len(hist)} loss {hist[-1]:.6g} dSCC {rho:.6f}")
-        if best is None or rho > best[0]:
-            best = (rho, f, hist[-1], model, coords)
-    rho, f, l, model, coords = best
-    print(f"Optimal conversion factor: {f}\nOptimal dSCC: {rho}")
+        runs.append((rho, f, hist[-1], model, coords))
+    k = [r[0] for r in runs].index(max(r[0] for r in runs))     # first maximum, as list.index(max)
+    rho, f, loss, model, coords = runs[k]
+    print(f"Optimal conversion factor: {f}")
+    print(f"Optimal dSCC: {rho}")
     if a.out:
         from .io import write_pdb
-        with open(f"{a.out}_log.txt", "w") as fh:
-            fh.writelines([f"Optimal conversion factor: {f}\n", f"Optimal dSCC: {rho}\n", f"Final MSE loss: {l}\n"])
-        torch.save(model.state_dict(), f"{a.out}_weights.pt")
+        with open(f"{a.out}_log.txt", "w") as fh:        # :155-156
+            fh.writelines([f"Optimal conversion factor: {f}\n", f"Optimal dSCC: {rho}\n", f"Final MSE loss: {loss}\n"])
+        torch.save(cpu_state_dict(model), f"{a.out}_weights.pt")
         write_pdb(coords.cpu().numpy() * 100, f"{a.out}_structure.pdb")
+        print(f"Saved trained model to {a.out}_weights.pt")
+        print(f"Saved optimal structure to {a.out}_structure.pdb")
     return 0
 
 

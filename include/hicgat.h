@@ -129,47 +129,6 @@ int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, 
                               const float *dout, int64_t ld_dout, const float *att_src,
                               const float *att_dst, float neg_slope, float *dh, float *da_src,
                               hicgat_stream_t stream);
-/* Column-sliced forms of hicgat_gat_agg_fwd_act and hicgat_gat_agg_bwd_src_ld: the same outputs
- * (row_stats max / sum / S3 bit-identical, out / out2 / dh / da_src up to fp32 summation order).
- * The H*C = 512 columns are cut into 512/slice_width strips (slice_width 32 or 64) and each of the
- * 8 XCDs aggregates its own strips, so the rows one XCD gathers fit its L2; the per-edge softmax
- * weights are formed once into edge records in the workspace
- * (hicgat_gat_sliced_workspace_bytes(N, nnz, H, slice_width), nnz = the whole CSR). */
-size_t hicgat_gat_sliced_workspace_bytes(int N, int nnz, int H, int slice_width);
-int hicgat_gat_agg_fwd_sliced(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
-                              int row_begin, int row_end, const float *h, const float *a_src,
-                              const float *a_dst, const float *bias, float neg_slope, int act,
-                              int slice_width, float *out, float *out2, float *row_stats, void *workspace,
-                              size_t workspace_bytes, hicgat_stream_t stream);
-int hicgat_gat_agg_bwd_src_sliced(const int32_t *rowptr, const int32_t *col, int N, int nnz, int H, int C,
-                                  int row_begin, int row_end, const float *h, const float *a_src,
-                                  const float *a_dst, const float *row_stats, int64_t ld_stats,
-                                  const float *dout, int64_t ld_dout, const float *att_src,
-                                  const float *att_dst, float neg_slope, int slice_width, float *dh,
-                                  float *da_src, void *workspace, size_t workspace_bytes,
-                                  hicgat_stream_t stream);
-/* Row-block forms of hicgat_gat_agg_fwd_act and hicgat_gat_agg_bwd_src_ld (csrc/gat_block.hip):
- * the same outputs (row_stats bit-identical, out / out2 / dh / da_src up to fp32 summation order).
- * 16 consecutive rows share one workgroup that loads each distinct neighbour row once for all of
- * them.  `runs` / `run_ptr` / `pos` is the static block structure of rows [row_begin, row_end)
- * (hicgat/graph.py block_csr): runs[u] = j | (mask << 32) sorted by (block, j), block b's runs in
- * [run_ptr[b], run_ptr[b+1]), pos[e - rowptr[row_begin]] = edge e's block-order position.  The
- * per-step edge weights go to the workspace (hicgat_gat_blk_workspace_bytes(N, nnz), nnz = the
- * whole CSR).  Replaces the same reference interface as the row forms (PyG GATConv propagate). */
-size_t hicgat_gat_blk_workspace_bytes(int N, int nnz);
-int hicgat_gat_blk_fwd(const int32_t *rowptr, const int32_t *col, const int32_t *pos,
-                       const int64_t *runs, const int32_t *run_ptr, int N, int nnz, int H, int C,
-                       int row_begin, int row_end, const float *h, const float *a_src,
-                       const float *a_dst, const float *bias, float neg_slope, int act, float *out,
-                       float *out2, float *row_stats, void *workspace, size_t workspace_bytes,
-                       hicgat_stream_t stream);
-int hicgat_gat_blk_bwd_src(const int32_t *rowptr, const int32_t *col, const int32_t *pos,
-                           const int64_t *runs, const int32_t *run_ptr, int N, int nnz, int H, int C,
-                           int row_begin, int row_end, const float *h, const float *a_src,
-                           const float *a_dst, const float *row_stats, int64_t ld_stats,
-                           const float *dout, int64_t ld_dout, const float *att_src,
-                           const float *att_dst, float neg_slope, float *dh, float *da_src,
-                           void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;
@@ -183,7 +142,7 @@ size_t hicgat_gat_param_grad_workspace_bytes(int N, int D);
 /* ---- a7: torch.cdist(c, c, p=2) (models.py:661) and its backward -----------------------------
  * D[i,j] = ||c_i - c_j||_2 (exact formula; the diagonal is exactly 0), ld = leading dim of D.
  * Backward: dc_i = sum_j (G_ij + G_ji) (c_i - c_j) / D_ij over D_ij != 0 (torch's
- * _euclidean_dist_backward masks res == 0).  workspace: hicgat_pairdist_workspace_bytes(N, 0). */
+ * _euclidean_dist_backward masks res == 0).  workspace: hicgat_pairdist_workspace_bytes(N, HICGAT_PD_SQUARE). */
 int hicgat_pairdist_fwd(const float *coords, int N, float *D, int64_t ldd, hicgat_stream_t stream);
 int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg, float *dcoords,
                         void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
@@ -201,12 +160,24 @@ int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg,
  *     and 9..10 are not meaningful; loss_kind 1 (combined loss) forms all of them;
  *   loss[1] (float32): mse (loss_kind 0) or total (loss_kind 1);
  *   dcoords [N,3] = d(mse)/dcoords restricted to the tile range (sum over ranks = full gradient).
- * workspace: hicgat_pairdist_workspace_bytes(N, 1). */
+ * workspace: hicgat_pairdist_workspace_bytes(N, HICGAT_PD_TRI). */
 int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
                               int64_t tile_begin, int64_t tile_end, int loss_kind, double *stats,
                               float *loss, float *dcoords, void *workspace, size_t workspace_bytes,
                               hicgat_stream_t stream);
+/* The same over a BAND of the truth (a rank's share, hicgat.dist): T holds rows
+ * [t_row0, t_row0 + t_rows) and columns [t_col0, t_col0 + ldt) of the N x N truth, element (i, j) at
+ * T[(i - t_row0) * ldt + (j - t_col0)].  The band must cover every pair of the tile range: rows of
+ * its tile-rows I0..I1 and columns from I0*128 on (else HICGAT_EINVAL). */
+int hicgat_pairdist_mse_fused_band(const float *coords, const float *T, int N, int64_t ldt,
+                                   int64_t t_row0, int64_t t_rows, int64_t t_col0, int64_t tile_begin,
+                                   int64_t tile_end, int loss_kind, double *stats, float *loss,
+                                   float *dcoords, void *workspace, size_t workspace_bytes,
+                                   hicgat_stream_t stream);
 int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, hicgat_stream_t stream);
+/* Tile count and workspace of the two tilings, mode HICGAT_PD_TRI (the fused loss: upper-triangle
+ * 128x128 tiles, nb(nb+1)/2) or HICGAT_PD_SQUARE (hicgat_pairdist_bwd: nb*nb), nb = ceil(N/128). */
+enum { HICGAT_PD_SQUARE = 0, HICGAT_PD_TRI = 1 };
 int64_t hicgat_pairdist_num_tiles(int N, int mode);
 size_t hicgat_pairdist_workspace_bytes(int N, int mode);
 

@@ -26,6 +26,20 @@ def _tri(I, J, nb):
     return I * nb - I * (I - 1) // 2 + (J - I)
 
 
+def torch_tail(hicgat):
+    """Give the flagship model a plain-torch tail (models.py:637-659) for CPU tensors: the product
+    tail runs on the HIP GEMM / LayerNorm kernels, which need a GPU."""
+    def post_act(self, x):   # after the relu, which the trainer fuses into the aggregation
+        res = self.align_densea(x)
+        x = F.relu(self.norm_a(self.densea(x))) + res
+        res = self.align_dense1(x)
+        x = F.relu(self.norm1(self.dense1(x))) + res
+        x = F.relu(self.norm2(self.dense2(x)))
+        return self.dense3(x)
+    hicgat.GATNetSelectiveResidualsUpdated.post_act = post_act
+    hicgat.GATNetSelectiveResidualsUpdated.tail = lambda self, x: post_act(self, F.relu(x))
+
+
 class CpuKernels:
     def linear_att(self, x, W, att_l, att_r, h=None):
         H, C = att_l.shape[-2], att_l.shape[-1]
@@ -150,9 +164,10 @@ class CpuKernels:
         nb = (n + BT - 1) // BT
         return nb * (nb + 1) // 2
 
-    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords):
+    def fused_loss(self, coords, tbuf, n, kind, t0, t1, stats, loss, dcoords, row0=0, col0=0):
+        """``tbuf`` = the truth or a band of it from (row0, col0) (kernels.HipKernels.fused_loss)."""
         nb = (n + BT - 1) // BT
-        T = tbuf[:, :n].double()
+        Tb = tbuf.double()
         c = coords.double()
         iu = torch.triu_indices(n, n, 1)
         ii, jj = iu[0], iu[1]
@@ -161,7 +176,7 @@ class CpuKernels:
         ii, jj = ii[keep], jj[keep]
         diff = c[ii] - c[jj]
         d = diff.norm(dim=1)
-        t = T[ii, jj]
+        t = Tb[ii - row0, jj - col0]
         r = d - t
         stats[0] = (r * r).sum()
         stats[1] = d.sum()
@@ -172,7 +187,7 @@ class CpuKernels:
         dii = torch.arange(n)
         dtile = _tri(dii // BT, dii // BT, nb)
         dkeep = (dtile >= t0) & (dtile < t1)
-        stats[6] = (T[dii[dkeep], dii[dkeep]] ** 2).sum()
+        stats[6] = (Tb[dii[dkeep] - row0, dii[dkeep] - col0] ** 2).sum()
         w = torch.where(d > 0, r / d, torch.zeros_like(d)) * (4.0 / (n * n))
         g = torch.zeros((n, 3), dtype=torch.float64)
         g.index_add_(0, ii, w.unsqueeze(1) * diff)

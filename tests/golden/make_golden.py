@@ -1,4 +1,5 @@
-"""Generate the golden fixtures under tests/golden/ from the REFERENCE's own code.
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE's own code -- with one
+qualification: the GAT arithmetic in them is NOT the reference's (parity unpinned, see below).
 
 Run in the build container only (the reference tree does not exist on the GPU box):
 
@@ -23,6 +24,20 @@ It imports the reference ``utils.py`` / ``models.py`` (``/root/reference``) with
   rank).
 * ``train_<name>.npz``  -- the ``HiC-GNN_main.py:117-132`` loop run for a fixed K on the same input
   (deterministic algorithms), loss history and final coordinates.
+
+What is pinned by the reference and what is not:
+
+* pinned (reference code ran): convert_to_matrix, load_input's edge construction and cont2dist
+  (``graph_*``), domain_alignment (``align_*``), the SAGE baseline ``Net`` (its SAGEConv is the
+  reference's own ``layers.py``), and the COMPOSITION of the GAT models -- the tail Linear /
+  LayerNorm / residual wiring, parameter registration order and init, cdist, MSE, the combined
+  loss and the training loop of ``models.py`` / ``HiC-GNN_main.py``;
+* NOT pinned: the GATConv values inside ``model_GAT*.npz`` / ``train_GAT*.npz``.  PyG 1.7.2 is
+  absent, so ``models.py``'s ``GATConv`` resolves to the stand-in
+  ``_stubs/torch_geometric/nn.py``, which IS ``oracle.gat.GATConv`` (the restatement of PyG
+  1.7.2's published code path), and the CSR the models see comes through the ``_stubs/torch_sparse``
+  stand-in.  Those fixtures therefore check the oracle's GAT arithmetic against itself: the GAT
+  kernels' parity is "parity unpinned" (DESIGN.md section 4).
 
 Only data is written (inputs and expected outputs); no reference source is copied.
 """

@@ -27,9 +27,15 @@ def _free_port():
     return p
 
 
-def _problem(n=300, seed=0):
+def _problem(n=300, seed=0, skew=False):
+    """Random symmetric contacts; ``skew``: a dense band over the first fifth of the rows plus a
+    sparse tail (equal-ROW shards would give rank 0 most of the edges)."""
     rng = np.random.default_rng(seed)
-    a = (rng.random((n, n)) < 0.08) * rng.integers(1, 50, (n, n)).astype(np.float64)
+    p = np.full((n, n), 0.08)
+    if skew:
+        p[:] = 0.02
+        p[:n // 5, :n // 5] = 0.9
+    a = (rng.random((n, n)) < p) * rng.integers(1, 50, (n, n)).astype(np.float64)
     a = np.triu(a, 1)
     a = a + a.T
     a[17, :] = 0
@@ -38,47 +44,36 @@ def _problem(n=300, seed=0):
     return a, x
 
 
-def _setup(n):
+def _setup(n, skew=False):
     for p in (os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hic-gnn_amd"), HERE):
         if p not in sys.path:
             sys.path.insert(0, p)
     import hicgat
     from oracle import graph as ogr
-    a, x = _problem(n)
+    a, x = _problem(n, skew=skew)
     iu = np.argwhere(np.triu(a != 0, 1))
     adj = hicgat.Adj(torch.tensor(iu[:, 0]), torch.tensor(iu[:, 1]), None, (n, n)).to_symmetric().to("cpu")
     truth = hicgat.Truth(ogr.cont2dist(torch.tensor(a), 0.5))
     return hicgat, adj, truth, torch.tensor(x)
 
 
-def _torch_tail(hicgat):
-    """The flagship tail (models.py:637-659) in plain torch for CPU tensors (the product tail runs
-    on the HIP GEMM / LayerNorm kernels)."""
-    import torch.nn.functional as F
-
-    def post_act(self, x):   # after the relu, which the trainer fuses into the aggregation
-        res = self.align_densea(x)
-        x = F.relu(self.norm_a(self.densea(x))) + res
-        res = self.align_dense1(x)
-        x = F.relu(self.norm1(self.dense1(x))) + res
-        x = F.relu(self.norm2(self.dense2(x)))
-        return self.dense3(x)
-    hicgat.GATNetSelectiveResidualsUpdated.post_act = post_act
-    hicgat.GATNetSelectiveResidualsUpdated.tail = lambda self, x: post_act(self, F.relu(x))
-
-
-def _worker(rank, world, port, n, kind, out):
+def _worker(rank, world, port, n, kind, out, skew=False, replicate_x=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        hicgat, adj, truth, x = _setup(n)
-        from cpu_kernels import CpuKernels
-        _torch_tail(hicgat)
+        hicgat, adj, truth, x = _setup(n, skew)
+        from cpu_kernels import CpuKernels, torch_tail
+        torch_tail(hicgat)
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated()
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels())
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels(),
+                                        replicate_x=replicate_x)
+        # what this rank holds: its edges, its x rows, its truth band (not the whole matrix)
+        held = torch.tensor([tr.local_nnz, tr.local_rows, tr.tband.numel(), tr.x_loc.shape[0]], dtype=torch.long)
+        allheld = [torch.zeros_like(held) for _ in range(world)]
+        dist.all_gather(allheld, held)
         losses, grad1, stats1 = [], None, None
         for _ in range(STEPS):
             loss, stats, _ = tr.step()
@@ -93,14 +88,15 @@ def _worker(rank, world, port, n, kind, out):
             for name, p in model.named_parameters():
                 by_name[name] = grad1[off[id(p)]:off[id(p)] + p.numel()].view_as(p).clone()
             torch.save({"losses": losses, "flat": tr.opt.flat.clone(), "grad1": grad1, "stats": stats1,
-                        "grads": by_name}, out)
+                        "grads": by_name, "held": torch.stack(allheld), "nnz": adj.device_nnz if hasattr(adj, "col32")
+                        and adj.col32 is not None else -1, "truth_numel": truth.dense().numel()}, out)
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, n, kind, tmp_path):
-    out = str(tmp_path / f"w{world}_{kind}.pt")
-    mp.spawn(_worker, args=(world, _free_port(), n, kind, out), nprocs=world, join=True)
+def _run(world, n, kind, tmp_path, skew=False, replicate_x=False):
+    out = str(tmp_path / f"w{world}_{kind}_{int(skew)}{int(replicate_x)}.pt")
+    mp.spawn(_worker, args=(world, _free_port(), n, kind, out, skew, replicate_x), nprocs=world, join=True)
     return torch.load(out, weights_only=True)
 
 
@@ -152,3 +148,50 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
             assert mine.abs().max().item() < 1e-6 * max(1.0, scale)
             continue
         assert (mine - pr.grad).abs().max().item() <= 1e-4 * scale, name
+
+
+@pytest.mark.parametrize("replicate_x", [False, True])
+def test_skewed_graph_shards_balance_nnz_and_match_world1(tmp_path, replicate_x):
+    """destination rows split by an nnz prefix sum.  On a dense band + sparse tail
+    the two shards hold (nearly) equal edge counts -- very unequal row counts -- each rank holds
+    only its edges / x rows / truth band, and the world-2 step equals the world-1 step (also
+    with x replicated and h recomputed on every rank, the 8(e) ablation)."""
+    one = _run(1, 300, "mse", tmp_path, skew=True)
+    two = _run(2, 300, "mse", tmp_path, skew=True, replicate_x=replicate_x)
+    held = two["held"]
+    nnz0, nnz1 = int(held[0, 0]), int(held[1, 0])
+    rows0, rows1 = int(held[0, 1]), int(held[1, 1])
+    assert nnz0 + nnz1 == int(one["held"][0, 0])
+    assert abs(nnz0 - nnz1) <= 0.02 * (nnz0 + nnz1), (nnz0, nnz1)
+    assert rows0 + rows1 == 300 and rows0 < rows1 / 2, (rows0, rows1)     # balance is by edges, not rows
+    assert int(held[0, 2]) < two["truth_numel"] and int(held[1, 2]) < two["truth_numel"]
+    assert abs(two["losses"][0] - one["losses"][0]) <= 1e-6 * abs(one["losses"][0])
+    g1, g2 = one["grad1"], two["grad1"]
+    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
+    np.testing.assert_allclose(two["losses"], one["losses"], rtol=1e-3)
+
+
+def test_partition_rows_prefix_sum():
+    for p in (os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hic-gnn_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from hicgat.dist import ShardPlan, partition_rows, tri_row
+    rp = np.concatenate([[0], np.cumsum([100] * 10 + [1] * 90)])     # 10 heavy rows, 90 light ones
+    b = partition_rows(rp, 2)
+    assert b[0] == 0 and b[2] == 100 and 5 <= b[1] <= 6
+    nb = 157
+    t = 0
+    for I in range(nb):
+        for J in range(I, nb):
+            if J in (I, nb - 1):
+                assert tri_row(t, nb) == I
+            t += 1
+    # local CSR of a plan: edges of own rows only, columns in buffer numbering
+    rowptr = np.array([0, 2, 4, 6, 8])
+    col = np.array([0, 1, 0, 1, 2, 3, 2, 3])
+    plan = ShardPlan(rowptr, col, 2)
+    rp0, c0 = plan.local_csr(0)
+    rp1, c1 = plan.local_csr(1)
+    assert plan.R == 2 and list(plan.gidx) == [0, 1, 2, 3]
+    assert list(rp0) == [0, 2, 4, 4, 4] and list(c0) == [0, 1, 0, 1]
+    assert list(rp1) == [0, 0, 0, 2, 4] and list(c1) == [2, 3, 2, 3]

@@ -81,7 +81,7 @@ def test_sharded_rccl_graph_replay_equals_eager(tmp_path):
     assert torch.equal(r["pe"], r["pg"])
 
 
-def _worker(rank, world, port, backend, n, out):
+def _worker(rank, world, port, backend, n, out, replicate_x=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -95,7 +95,7 @@ def _worker(rank, world, port, backend, n, out):
         hicgat, adj, truth, x = _inputs(n, dev)
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3)
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, replicate_x=replicate_x)
         loss, stats, _ = tr.step()
         grad1 = tr.opt.grad.clone().cpu()
         stats = stats.clone()           # the trainer's stats buffer is reused by the next step
@@ -108,9 +108,9 @@ def _worker(rank, world, port, backend, n, out):
         dist.destroy_process_group()
 
 
-def _run(world, backend, n, tmp_path):
-    out = str(tmp_path / f"{backend}{world}.pt")
-    mp.spawn(_worker, args=(world, _port(), backend, n, out), nprocs=world, join=True)
+def _run(world, backend, n, tmp_path, replicate_x=False):
+    out = str(tmp_path / f"{backend}{world}{int(replicate_x)}.pt")
+    mp.spawn(_worker, args=(world, _port(), backend, n, out, replicate_x), nprocs=world, join=True)
     return torch.load(out, weights_only=True)
 
 
@@ -133,10 +133,13 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path):
     assert (g - res["grad1"]).abs().max().item() <= 1e-5 * g.abs().max().item()
 
 
-def test_sharded_two_ranks_equal_one_rank(tmp_path):
+@pytest.mark.parametrize("replicate_x", [False, True])
+def test_sharded_two_ranks_equal_one_rank(tmp_path, replicate_x):
+    """nnz-balanced shards (padded buffers, remapped local CSR, truth bands) over gloo on the one
+    GPU; replicate_x: the SURVEY 8(e) ablation (h recomputed on every rank, no h all-gather)."""
     n = 777
     one = _run(1, "gloo", n, tmp_path)
-    two = _run(2, "gloo", n, tmp_path)
+    two = _run(2, "gloo", n, tmp_path, replicate_x)
     # the MLP tail runs on 389/388-row shards instead of 777 rows: hipBLASLt may pick another
     # kernel (another k order) for the smaller GEMMs, so coordinates agree to ~1e-7, not bitwise
     assert abs(two["loss"][0] - one["loss"][0]) <= 1e-6 * abs(one["loss"][0])

@@ -101,11 +101,19 @@ def test_cont2dist_bit_exact(case, factor, key):
         assert ulps.max() <= 2 and (ulps > 0).mean() < 0.02
     tr = hicgat.Truth.from_contacts(y, factor)
     d32 = tr.dense().cpu().numpy()
-    assert np.array_equal(d32, ieee.astype(np.float32))
-    assert np.abs(d32.view(np.int32) - g[key].astype(np.float32).view(np.int32)).max() <= 1
     assert tr.ld % 128 == 0
-    # convert_to_matrix's triu + tril(T, 1) is asymmetric when the list has lower-triangle entries
-    assert tr.symmetric == bool(np.array_equal(g[key], g[key].T))
+    # convert_to_matrix's triu + tril(T, 1) is asymmetric when the list has lower-triangle entries;
+    # the fused-loss target then holds the equivalent symmetric form (graph.Truth)
+    asym = not bool(np.array_equal(g[key], g[key].T))
+    assert tr.asymmetric_source == asym
+    if not asym:
+        assert np.array_equal(d32, ieee.astype(np.float32))
+        assert np.abs(d32.view(np.int32) - g[key].astype(np.float32).view(np.int32)).max() <= 1
+    else:
+        t = ieee.astype(np.float32).astype(np.float64)
+        sym = (t + t.T) / 2
+        np.fill_diagonal(sym, np.sqrt(np.diag(t) ** 2 + 0.5 * np.triu((t - t.T) ** 2, 1).sum(1)))
+        np.testing.assert_allclose(d32, sym, rtol=1e-6, atol=1e-7)
 
 
 # ---------------------------------------------------------------- GATConv (a2, a4, a5 + bwd)
@@ -399,7 +407,7 @@ def test_fused_loss_tile_ranges_sum_to_whole():
     np.fill_diagonal(t, 0)
     tr = hicgat.Truth(torch.tensor(t, device=DEV))
     c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32), device=DEV)
-    tiles = _lib.load().hicgat_pairdist_num_tiles(n, 0)
+    tiles = _lib.load().hicgat_pairdist_num_tiles(n, 1)
     full_l, full_s = hicgat.ops.fused_dist_loss(c.clone().requires_grad_(True), tr)
     parts = [(0, tiles // 3), (tiles // 3, tiles // 2), (tiles // 2, tiles)]
     acc = torch.zeros(7, dtype=torch.float64)

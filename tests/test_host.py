@@ -32,8 +32,8 @@ def test_library_exports_every_header_symbol():
 def test_query_functions_need_no_gpu():
     from hicgat import _lib
     lib = _lib.load()
-    assert lib.hicgat_pairdist_num_tiles(20000, 0) == 157 * 158 // 2
-    assert lib.hicgat_pairdist_num_tiles(20000, 1) == 157 * 157
+    assert lib.hicgat_pairdist_num_tiles(20000, 1) == 157 * 158 // 2  # HICGAT_PD_TRI
+    assert lib.hicgat_pairdist_num_tiles(20000, 0) == 157 * 157  # HICGAT_PD_SQUARE
     assert lib.hicgat_pairdist_num_tiles(0, 0) == 0
     assert lib.hicgat_pairdist_workspace_bytes(58, 1) > 0
 

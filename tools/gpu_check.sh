@@ -19,7 +19,6 @@ for s in $STAGES; do
   case $s in
     tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     tfast) run pytest_fast 300 python -u -m pytest tests/test_gpu_fast_paths.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
-    benchs) HICGAT_SLICE=${SLICE:-32} run bench_s${SLICE:-32} 600 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ;;
     benchx3) HICGAT_GEMM=auto run bench_x3 600 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ;;
     dscc) run dscc 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k dscc_chr19 -s -v --timeout 240 --timeout-method thread ;;
     n2v) run n2v 300 python -u -m pytest tests/test_gpu_node2vec.py -m gpu -v -rf --timeout 180 --timeout-method thread ;;

@@ -60,18 +60,6 @@ def main():
     g256, g256b, g256c = torch.randn(256, device=dev), torch.empty(256, device=dev), torch.empty(256, device=dev)
     ya2 = torch.empty(n, 256, device=dev)
     libs = [s for s in a.libs.split(",") if s] or [_lib.LIB_PATH]
-    sliced = {}
-
-    def _sliced(K, sw):
-        """The same library with the XCD column-strip aggregation of width sw."""
-        key = (id(K), sw)
-        if key not in sliced:
-            S = kernels.HipKernels.__new__(kernels.HipKernels)
-            S.lib, S.slice_width = K.lib, sw
-            S.gemm_impl = getattr(K, "gemm_impl", 0)
-            S.agg_form = "row"
-            sliced[key] = S
-        return sliced[key]
     def _with_impl(K, impl, fn):
         saved, K.gemm_impl = K.gemm_impl, impl
         try:
@@ -86,9 +74,7 @@ def main():
             fn.restype, fn.argtypes = res, args
         K = kernels.HipKernels.__new__(kernels.HipKernels)
         K.lib = lib
-        K.slice_width = 0            # the row-per-wave kernels; "@sw" jobs time the strip kernels
         K.gemm_impl = 0              # GEMMs: auto (x3 where supported); "#f32" / "#x3" jobs force one
-        K.agg_form = "row"           # "!block" jobs time the row-block form
         kset.append((os.path.basename(path), K))
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
@@ -101,10 +87,6 @@ def main():
         "gat_agg_bwd_src": lambda K: K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, al, ar,
                                                    0.2, dh, da),
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
-        **{f"gat_agg_fwd_train@{sw}": (lambda K, sw=sw: _sliced(K, sw).agg_fwd_act(
-            adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out, out2, rs)) for sw in (32, 64)},
-        **{f"gat_agg_bwd_src@{sw}": (lambda K, sw=sw: _sliced(K, sw).agg_bwd_src(
-            adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, al, ar, 0.2, dh, da)) for sw in (32, 64)},
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
         "pairdist_combined": lambda K: K.fused_loss(coords, truth.buf, n, 1, 0, -1, stats, loss, dc),
         "colsum_20000x512": lambda K: K.colsum(out, cs),
