@@ -19,6 +19,9 @@
 namespace hicgat {
 
 constexpr int BT = 128;
+#ifndef HICGAT_PD_UNROLL
+#define HICGAT_PD_UNROLL 2   // rows per iteration of the packed interior loop (LDS reads of the next row in flight)
+#endif
 enum { MODE_SYM = 0, MODE_FULL = 1 };
 
 __host__ __device__ inline int pd_nb(int N) { return (N + BT - 1) / BT; }
@@ -31,8 +34,10 @@ __device__ inline void tri_decode(int64_t t, int nb, int &I, int &J) {
   if (Ii > nb - 1) Ii = nb - 1;
   while (Ii > 0 && tri_start(Ii, nb) > t) --Ii;
   while (Ii + 1 < nb && tri_start(Ii + 1, nb) <= t) ++Ii;
-  I = (int)Ii;
-  J = (int)(Ii + (t - tri_start(Ii, nb)));
+  // block-uniform: into SGPRs, so every branch on I / J (interior vs edge tiles) is a scalar
+  // branch, not an if-converted (both paths) VALU select
+  I = __builtin_amdgcn_readfirstlane((int)Ii);
+  J = __builtin_amdgcn_readfirstlane((int)(Ii + (t - tri_start(Ii, nb))));
 }
 
 template <int CTRL>
@@ -171,7 +176,7 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
   }
   const f2 z2 = f2{0.f, 0.f};
   f2 L2 = z2, sd2 = z2, sdd2 = z2, sdt2 = z2, st2 = z2, stt2 = z2;
-#pragma unroll 1
+#pragma unroll HICGAT_PD_UNROLL
   for (int k = K0; k < K1; ++k) {
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
     const f2 rx = f2{sc[0][lr][0], sc[0][lr][0]}, ry = f2{sc[0][lr][1], sc[0][lr][1]},
@@ -183,8 +188,11 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const f2 dx = rx - cx2[h], dy = ry - cy2[h], dz = rz - cz2[h];
-      const f2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-      const f2 inv = f2{fminf(__builtin_amdgcn_rsqf(d2.x), 1e30f), fminf(__builtin_amdgcn_rsqf(d2.y), 1e30f)};
+      // d2 + 2^-100 (below one ulp of any d2 that is not ~0): coincident points give a finite
+      // inv = 2^50, d = 2^-50 and w * (dx, dy, dz) = 0 -- the clamp of the generic path for free
+      const f2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy,
+                                              __builtin_elementwise_fma(dz, dz, f2{0x1.0p-100f, 0x1.0p-100f})));
+      const f2 inv = f2{__builtin_amdgcn_rsqf(d2.x), __builtin_amdgcn_rsqf(d2.y)};
       const f2 d = d2 * inv;
       const f2 r = d - tv[h];
       L2 = __builtin_elementwise_fma(r, r, L2);
@@ -225,287 +233,9 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
   }
 }
 
-#define HICGAT_RING_WAIT 12   // = 4 * (RING - 1): DMA wave-instructions younger than the awaited stage
-// ---- persistent streaming form of the training loss (MODE_SYM, float4-aligned T) ----------------
-// A short-lived block per tile (pairdist_tile_kernel) loads its 64 KiB and then computes: load and
-// math run in series and only ~2 blocks per CU stream at a time.  Here each block stays resident
-// and walks the tile range with a stride of gridDim.x, and every WAVE streams its own rows of T
-// through a private LDS ring of RING stages (LDS-DMA, global_load_lds_dwordx4), RING-1 stages in
-// flight under the math of the current one:
-//   stage = a quarter of a tile for one wave = the 8 rows (4 ty x rows k = 2q, 2q+1) its 64 threads
-//   read = 4 KiB = 4 DMA wave-instructions (lanes 0-31 one 512-B row, 32-63 the next);
-//   a wave consumes only the rows it loaded itself, so the ring needs no barrier -- only a counted
-//   `s_waitcnt vmcnt` (VMEM ops complete in issue order; the count ignores the few stores and
-//   coordinate loads issued in between, which only makes the wait stricter).
-// Per tile the block still syncs twice (coordinates in, column partials out); the coordinates of
-// the NEXT tile are loaded into registers a tile ahead, so no wait for them drains the ring.
-// Thread map, per-tile partial slabs and epilogue are those of pairdist_tile_kernel.
-constexpr int RING = 4;                 // stages per wave ring
-constexpr int STG = 4 * 2 * BT;         // floats per wave-stage (4 KiB)
-constexpr size_t kRingLds = ((size_t)4 * RING * STG + 2 * 2 * BT * 3) * sizeof(float);   // 70 KiB per block
-
-#define HICGAT_STR2(x) #x
-#define HICGAT_STR(x) HICGAT_STR2(x)
-
-// rows k = 2q, 2q+1 of the thread, T from its wave's ring stage (row r of ty at st[ty&3][r][.])
-template <bool PEARSON>
-__device__ __forceinline__ void ring_rows_pk(const float *st, int q, const float (*sc)[BT][3], int tx, int ty,
-                                             const float *cx, const float *cy, const float *cz,
-                                             float4 *__restrict__ prow, TileAcc &A) {
-  f2 cx2[4], cy2[4], cz2[4], ax2[4], ay2[4], az2[4];
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    cx2[h] = f2{cx[2 * h], cx[2 * h + 1]};
-    cy2[h] = f2{cy[2 * h], cy[2 * h + 1]};
-    cz2[h] = f2{cz[2 * h], cz[2 * h + 1]};
-    ax2[h] = f2{A.ax[2 * h], A.ax[2 * h + 1]};
-    ay2[h] = f2{A.ay[2 * h], A.ay[2 * h + 1]};
-    az2[h] = f2{A.az[2 * h], A.az[2 * h + 1]};
-  }
-  const f2 z2 = f2{0.f, 0.f};
-  f2 L2 = z2, sd2 = z2, sdd2 = z2, sdt2 = z2, st2 = z2, stt2 = z2;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int k = 2 * q + r;
-    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
-    const f2 rx = f2{sc[0][lr][0], sc[0][lr][0]}, ry = f2{sc[0][lr][1], sc[0][lr][1]},
-             rz = f2{sc[0][lr][2], sc[0][lr][2]};
-    const float *row = st + ((ty & 3) * 2 + r) * BT;
-    const float4 a = *reinterpret_cast<const float4 *>(&row[tx * 4]);
-    const float4 b = *reinterpret_cast<const float4 *>(&row[64 + tx * 4]);
-    const f2 tv[4] = {f2{a.x, a.y}, f2{a.z, a.w}, f2{b.x, b.y}, f2{b.z, b.w}};
-    f2 px = z2, py = z2, pz = z2;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const f2 dx = rx - cx2[h], dy = ry - cy2[h], dz = rz - cz2[h];
-      const f2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-      const f2 inv = f2{fminf(__builtin_amdgcn_rsqf(d2.x), 1e30f), fminf(__builtin_amdgcn_rsqf(d2.y), 1e30f)};
-      const f2 d = d2 * inv;
-      const f2 rr = d - tv[h];
-      L2 = __builtin_elementwise_fma(rr, rr, L2);
-      if (PEARSON) {
-        sd2 += d;
-        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
-        sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
-        st2 += tv[h];
-        stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
-      }
-      const f2 w = rr * inv;
-      px = __builtin_elementwise_fma(w, dx, px);
-      py = __builtin_elementwise_fma(w, dy, py);
-      pz = __builtin_elementwise_fma(w, dz, pz);
-      ax2[h] = __builtin_elementwise_fma(-w, dx, ax2[h]);
-      ay2[h] = __builtin_elementwise_fma(-w, dy, ay2[h]);
-      az2[h] = __builtin_elementwise_fma(-w, dz, az2[h]);
-    }
-    const float sx = sum16(px.x + px.y), sy = sum16(py.x + py.y), sz = sum16(pz.x + pz.y);
-    if (tx == 0) prow[lr] = make_float4(sx, sy, sz, 0.f);
-  }
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    A.ax[2 * h] = ax2[h].x;
-    A.ax[2 * h + 1] = ax2[h].y;
-    A.ay[2 * h] = ay2[h].x;
-    A.ay[2 * h + 1] = ay2[h].y;
-    A.az[2 * h] = az2[h].x;
-    A.az[2 * h + 1] = az2[h].y;
-  }
-  A.L += L2.x + L2.y;
-  if (PEARSON) {
-    A.sd += sd2.x + sd2.y;
-    A.sdd += sdd2.x + sdd2.y;
-    A.sdt += sdt2.x + sdt2.y;
-    A.st += st2.x + st2.y;
-    A.stt += stt2.x + stt2.y;
-  }
-}
-
-// Edge / diagonal tiles: tile_rows' masked MODE_SYM arithmetic on the ring stage.
-template <bool PEARSON>
-__device__ __forceinline__ void ring_rows_mask(const float *st, int q, int N, int I, int J, const float (*sc)[BT][3],
-                                               int tx, int ty, const float *cx, const float *cy, const float *cz,
-                                               const int *gj, float4 *__restrict__ prow, TileAcc &A) {
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int k = 2 * q + r;
-    const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
-    const int gi = I * BT + lr;
-    const bool rok = gi < N;                          // stale LDS past N (coords_dma)
-    const float rx = rok ? sc[0][lr][0] : 0.f, ry = rok ? sc[0][lr][1] : 0.f, rz = rok ? sc[0][lr][2] : 0.f;
-    const float *row = st + ((ty & 3) * 2 + r) * BT;
-    const float4 a = *reinterpret_cast<const float4 *>(&row[tx * 4]);
-    const float4 b = *reinterpret_cast<const float4 *>(&row[64 + tx * 4]);
-    const float tvv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    float px = 0.f, py = 0.f, pz = 0.f;
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      const float dx = rx - cx[qq], dy = ry - cy[qq], dz = rz - cz[qq];
-      const float d2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-      const float inv = fminf(__builtin_amdgcn_rsqf(d2), 1e30f);
-      const float d = d2 * inv;
-      const float tt = tvv[qq];
-      const float rr = d - tt;
-      bool valid = gi < N && gj[qq] < N;
-      if (valid && gi == gj[qq]) A.dg = fmaf(tt, tt, A.dg);   // (D_ii - T_ii)^2 = T_ii^2
-      valid = valid && (I != J || gi < gj[qq]);
-      if (valid) {
-        A.L = fmaf(rr, rr, A.L);
-        if (PEARSON) {
-          A.sd += d;
-          A.sdd = fmaf(d, d, A.sdd);
-          A.sdt = fmaf(d, tt, A.sdt);
-          A.st += tt;
-          A.stt = fmaf(tt, tt, A.stt);
-        }
-      }
-      const float w = valid ? rr * inv : 0.f;
-      px = fmaf(w, dx, px);
-      py = fmaf(w, dy, py);
-      pz = fmaf(w, dz, pz);
-      A.ax[qq] = fmaf(-w, dx, A.ax[qq]);
-      A.ay[qq] = fmaf(-w, dy, A.ay[qq]);
-      A.az[qq] = fmaf(-w, dz, A.az[qq]);
-    }
-    px = sum16(px);
-    py = sum16(py);
-    pz = sum16(pz);
-    if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
-  }
-}
-
-template <bool PEARSON>
-__global__ __launch_bounds__(256, 2) void pairdist_ring_kernel(
-    const float *__restrict__ coords, const float *__restrict__ T, int N, int64_t ldt, int64_t row0,
-    int64_t col0, int nb, int64_t t0, int64_t t1, float4 *__restrict__ part, double *__restrict__ mom) {
-  // one dynamic LDS array: [4 waves][RING][STG] ring, then the double-buffered coordinates
-  // sc[2][2][BT][3] (both are LDS-DMA targets; the compiler's own waits do not track them, the
-  // counted waits below do)
-  extern __shared__ __attribute__((aligned(16))) float ring[];
-  float (*sc)[2][BT][3] = reinterpret_cast<float (*)[2][BT][3]>(ring + 4 * RING * STG);
-  __shared__ float4 colred[4][BT];
-  __shared__ double mred[4][7];
-  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, lane = tid & 63, wv = tid >> 6;
-  const int64_t tb = t0 + blockIdx.x, G = gridDim.x;
-  if (tb >= t1) return;
-  const int64_t ntiles = (t1 - 1 - tb) / G + 1;        // tiles of this block
-  const int nst = (int)(ntiles * 4);                   // stages of each wave
-  float *myring = ring + (size_t)wv * RING * STG;
-  // DMA of stage g into its ring slot (none past the end: the counted waits then simply wait for
-  // more than they need to, at the last RING - 1 stages)
-  auto issue = [&](int g) {
-    if (g >= nst) return;
-    const int64_t t = tb + (int64_t)(g >> 2) * G;
-    const int q = g & 3;
-    int I, J;
-    tri_decode(t, nb, I, J);
-    float *dst = myring + (g % RING) * STG;
-    const float *base = T + ((int64_t)J * BT - col0) + (lane & 31) * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int lr = (4 * wv + i) * 4 + ((2 * q) & 3) + (q >> 1) * 64 + (lane >> 5);
-      const int gi = min(I * BT + lr, N - 1);
-      __builtin_amdgcn_global_load_lds(base + (int64_t)(gi - row0) * ldt, dst + i * 2 * BT, 16, 0, 0);
-    }
-  };
-  // coordinates of tile t into sc[buf] by LDS-DMA, one float per lane (exact masking at 3N, so
-  // nothing past the coords array is read; rows past N keep stale values, which only edge tiles
-  // see and sanitise): the I rows' 384 floats then the J rows' 384, 12 wave-instructions, 3 per wave
-  auto coords_dma = [&](int64_t t, int buf) {
-    int I, J;
-    tri_decode(t, nb, I, J);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int c = wv * 3 + i;                      // 0..11: 64-float chunk of [I rows | J rows]
-      const int which = c / 6, f = (c % 6) * 64 + lane;
-      const int64_t src = (int64_t)(which ? J : I) * (3 * BT) + f;
-      float *dst = &sc[buf][which][0][0] + (c % 6) * 64;
-      if (src < 3 * (int64_t)N) __builtin_amdgcn_global_load_lds(coords + src, dst, 4, 0, 0);
-    }
-  };
-  coords_dma(tb, 0);
-#pragma unroll
-  for (int g = 0; g < RING - 1; ++g) issue(g);
-  for (int64_t n = 0; n < ntiles; ++n) {
-    const int64_t t = tb + n * G;
-    const int buf = (int)(n & 1);
-    float (*scb)[BT][3] = sc[buf];
-    // this tile's coordinates (DMA'd a tile ago, or in the prologue) have landed: they are older
-    // than the 4 (RING - 1) youngest stage DMAs
-    asm volatile("s_waitcnt vmcnt(" HICGAT_STR(HICGAT_RING_WAIT) ")" ::: "memory");
-    // (A): coordinates visible to every wave; also orders the previous tile's colred / mred reads
-    // before this tile's writes, and every read of sc[buf ^ 1] before its refill below.  A raw
-    // barrier after an LDS drain: __syncthreads' fence would also wait for the whole ring (vmcnt 0)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (n + 1 < ntiles) coords_dma(t + G, buf ^ 1);
-    int I, J;
-    tri_decode(t, nb, I, J);
-    float cx[8], cy[8], cz[8];
-    int gj[8];
-    TileAcc A;
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      const int lc = tx * 4 + (qq & 3) + (qq >> 2) * 64;
-      gj[qq] = J * BT + lc;
-      const bool ok = gj[qq] < N;                     // stale LDS past N (coords_dma)
-      cx[qq] = ok ? scb[1][lc][0] : 0.f;
-      cy[qq] = ok ? scb[1][lc][1] : 0.f;
-      cz[qq] = ok ? scb[1][lc][2] : 0.f;
-      A.ax[qq] = A.ay[qq] = A.az[qq] = 0.f;
-    }
-    float4 *prow = part + (size_t)t * 2 * BT;
-    const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
-#pragma unroll 1
-    for (int q = 0; q < 4; ++q) {
-      const int g = (int)(n * 4) + q;
-      issue(g + RING - 1);
-      // stage g has landed once at most 4 (RING - 1) younger DMAs are outstanding
-      asm volatile("s_waitcnt vmcnt(" HICGAT_STR(HICGAT_RING_WAIT) ")" ::: "memory");
-      const float *st = myring + (g % RING) * STG;
-      if (interior) ring_rows_pk<PEARSON>(st, q, scb, tx, ty, cx, cy, cz, prow, A);
-      else ring_rows_mask<PEARSON>(st, q, N, I, J, scb, tx, ty, cx, cy, cz, gj, prow, A);
-    }
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      A.ax[qq] += __shfl_xor(A.ax[qq], 16);
-      A.ax[qq] += __shfl_xor(A.ax[qq], 32);
-      A.ay[qq] += __shfl_xor(A.ay[qq], 16);
-      A.ay[qq] += __shfl_xor(A.ay[qq], 32);
-      A.az[qq] += __shfl_xor(A.az[qq], 16);
-      A.az[qq] += __shfl_xor(A.az[qq], 32);
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq)
-        colred[wv][tx * 4 + (qq & 3) + (qq >> 2) * 64] = make_float4(A.ax[qq], A.ay[qq], A.az[qq], 0.f);
-    }
-    double m[7] = {A.L, A.sd, A.sdd, A.sdt, A.st, A.stt, A.dg};
-#pragma unroll
-    for (int c = 0; c < 7; ++c) {
-      if (!PEARSON && c >= 1 && c <= 5) continue;
-      for (int o = 32; o > 0; o >>= 1) m[c] += shfl_xor_d(m[c], o);
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int c = 0; c < 7; ++c) mred[wv][c] = m[c];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // (B)
-    if (tid < BT) {
-      float4 sum = colred[0][tid];
-#pragma unroll
-      for (int w2 = 1; w2 < 4; ++w2) {
-        const float4 o = colred[w2][tid];
-        sum.x += o.x;
-        sum.y += o.y;
-        sum.z += o.z;
-      }
-      prow[BT + tid] = sum;
-    }
-    if (tid < 7) mom[(size_t)t * 8 + tid] = ((mred[0][tid] + mred[1][tid]) + mred[2][tid]) + mred[3][tid];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
+#ifndef HICGAT_PD_DBG
+#define HICGAT_PD_DBG 0   // A/B builds only: 1 = skip the T loads (math only), 2 = skip the math (loads only)
+#endif
 
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
@@ -556,7 +286,7 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
       const int r0 = (q < 8 ? 0 : 64) + wv * 16 + (q & 7) * 2;
       const int gi = min(I * BT + r0 + (lane >> 5), N - 1);
       const float *src = T + (size_t)(gi - row0) * ldt + (size_t)((int64_t)J * BT - col0) + (lane & 31) * 4;
-      __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
+      if (HICGAT_PD_DBG != 1) __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
     }
   }
   // sc[] (written above with ds_write) to all waves: LDS drain + raw barrier -- __syncthreads()
@@ -580,14 +310,16 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
   if (VEC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // this wave's first 16 rows landed
   constexpr bool PK = VEC && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
-  if (interior) {
+  if (HICGAT_PD_DBG == 2) {
+  } else if (interior) {
     if constexpr (PK) tile_rows_pk<PEARSON, 0, 4>(tile, sc, tx, ty, cx, cy, cz, prow, A);
     else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
     tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
-  if (interior) {
+  if (HICGAT_PD_DBG == 2) {
+  } else if (interior) {
     if constexpr (PK) tile_rows_pk<PEARSON, 4, 8>(tile, sc, tx, ty, cx, cy, cz, prow, A);
     else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
@@ -638,12 +370,13 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   }
 }
 
-// dcoords[i] = scale * (sum of the row partials of tiles (R, *) + column partials of (*, R)).
+// dcoords[i] = scale * (sum of the row partials of tiles (R, *) + column partials of (*, R));
+// ncol = column slabs per tile (1 here; the slab layout is [row partials | ncol column partials]).
 // Block = 64 rows x 4 groups; group g adds the tiles J = g, g+4, ... of its row, then the 4 group
 // sums are combined in group order (fixed order: bitwise reproducible).
 constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-thread blocks)
 
-__global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part,
+__global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part, int ncol,
                                                                int N, int nb, int mode, int64_t t0,
                                                                int64_t t1, float scale,
                                                                float *__restrict__ dcoords) {
@@ -663,11 +396,17 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
         trow = (int64_t)R * nb + J;
         tcol = (int64_t)J * nb + R;
       }
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if (trow >= t0 && trow < t1) a = part[(size_t)trow * 2 * BT + lr];
-      if (tcol >= t0 && tcol < t1) b = part[(size_t)tcol * 2 * BT + BT + lr];
+      // slab of tile t: [row partials | ncol column-partial rows], (1 + ncol) x BT float4
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+      const size_t st = (size_t)(1 + ncol) * BT;
+      if (trow >= t0 && trow < t1) a = part[(size_t)trow * st + lr];
+      if (tcol >= t0 && tcol < t1) {
+        b = part[(size_t)tcol * st + BT + lr];
+        if (ncol == 2) c = part[(size_t)tcol * st + 2 * BT + lr];
+      }
       sx += a.x; sy += a.y; sz += a.z;
       sx += b.x; sy += b.y; sz += b.z;
+      sx += c.x; sy += c.y; sz += c.z;
     }
   }
   red[grp][lr64] = make_float4(sx, sy, sz, 0.f);
@@ -689,11 +428,13 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
 // each sum a contiguous tile range (tree over 256 threads), one block adds the block sums in order.
 constexpr int kMomBlocks = 64;
 
-__global__ __launch_bounds__(256) void moments_partial_kernel(const double *__restrict__ mom, int64_t t0,
+__global__ __launch_bounds__(256) void moments_partial_kernel(const double *__restrict__ mom, int per, int64_t t0,
                                                               int64_t t1, double *__restrict__ part) {
+  // mom holds `per` 8-double records per tile (1 here), units [t0*per, t1*per)
   __shared__ double red[7][256];
-  const int64_t per = (t1 - t0 + kMomBlocks - 1) / kMomBlocks;
-  const int64_t b0 = t0 + (int64_t)blockIdx.x * per, b1 = min(t1, b0 + per);
+  const int64_t u0 = t0 * per, u1 = t1 * per;
+  const int64_t cnt = (u1 - u0 + kMomBlocks - 1) / kMomBlocks;
+  const int64_t b0 = u0 + (int64_t)blockIdx.x * cnt, b1 = min(u1, b0 + cnt);
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int64_t t = b0 + threadIdx.x; t < b1; t += 256) {
 #pragma unroll
@@ -771,9 +512,15 @@ extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
   return mode == HICGAT_PD_TRI ? nb * (nb + 1) / 2 : nb * nb;
 }
 
+// per tile: a (1 + ncol) x 128 float4 partial slab and ncol x 8 fp64 moments (ncol = 1: one column
+// slab per tile)
+static int pd_ncol(int) { return 1; }
+
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
   const int64_t tiles = hicgat_pairdist_num_tiles(N, mode);
-  return (size_t)tiles * (2 * BT * sizeof(float4) + 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) + 256;
+  const int nc = pd_ncol(mode);
+  return (size_t)tiles * ((1 + nc) * BT * sizeof(float4) + nc * 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) +
+         256;
 }
 
 // Host twin of tri_decode (exact integer search): tile-row of upper-triangle tile t.
@@ -786,10 +533,10 @@ static int tri_row_host(int64_t t, int nb) {
   return lo;
 }
 
-static void carve(void *ws, int64_t tiles, float4 **part, double **mom) {
+static void carve(void *ws, int64_t tiles, int ncol, float4 **part, double **mom) {
   char *p = static_cast<char *>(ws);
   *part = reinterpret_cast<float4 *>(p);
-  *mom = reinterpret_cast<double *>(p + (size_t)tiles * 2 * BT * sizeof(float4));
+  *mom = reinterpret_cast<double *>(p + (size_t)tiles * (1 + ncol) * BT * sizeof(float4));
 }
 
 extern "C" int hicgat_pairdist_fwd(const float *coords, int N, float *D, int64_t ldd,
@@ -814,7 +561,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   const int64_t tiles = (int64_t)nb * nb;
   float4 *part;
   double *mom;
-  carve(workspace, tiles, &part, &mom);
+  carve(workspace, tiles, 1, &part, &mom);
   const bool vec = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) &&
                    ldg >= (int64_t)nb * BT;
   if (vec)
@@ -825,7 +572,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
                        (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
-                     (hipStream_t)stream, part, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
+                     (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
                      dcoords);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
@@ -857,31 +604,13 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   }
   float4 *part;
   double *mom;
-  carve(workspace, tiles, &part, &mom);
+  carve(workspace, tiles, 1, &part, &mom);
   // HICGAT_PD_NOLDS=1 (A/B measurement only): read T straight into registers instead of the
   // LDS-DMA tile image
   static const bool nolds = getenv("HICGAT_PD_NOLDS") && atoi(getenv("HICGAT_PD_NOLDS")) != 0;
   const bool vec = !nolds && (ldt % 4 == 0) && (t_col0 % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                    ldt >= (int64_t)nb * BT - t_col0;
-  // HICGAT_PD_PERSIST=0 (A/B measurement only): one short-lived block per tile (LDS-DMA form)
-  static const bool persist = !(getenv("HICGAT_PD_PERSIST") && atoi(getenv("HICGAT_PD_PERSIST")) == 0);
-  if (nt > 0 && vec && persist) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    // two resident blocks per CU (LDS: 2 x 78 KiB); an equal number of tiles per block
-    const int64_t slots = (int64_t)cus * 2;
-    const int64_t per = (nt + slots - 1) / slots;
-    const int64_t grid = (nt + per - 1) / per;
-    if (loss_kind == 1)
-      hipLaunchKernelGGL(pairdist_ring_kernel<true>, dim3((unsigned)grid), dim3(256), kRingLds, (hipStream_t)stream,
-                         coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, tile_end, part, mom);
-    else
-      hipLaunchKernelGGL(pairdist_ring_kernel<false>, dim3((unsigned)grid), dim3(256), kRingLds, (hipStream_t)stream,
-                         coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, tile_end, part, mom);
-    HICGAT_CHECK_LAUNCH();
-  } else if (nt > 0) {
+  if (nt > 0) {
     // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only
 #define HICGAT_PD_SYM(V, P)                                                                          \
   hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, P>), dim3(nt), dim3(256), V ? kTileLds : 0, \
@@ -893,15 +622,16 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
 #undef HICGAT_PD_SYM
     HICGAT_CHECK_LAUNCH();
   }
+  const int ncol = 1;
   if (dcoords) {
     const float scale = (float)(4.0 / ((double)N * (double)N));
     hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
-                       (hipStream_t)stream, part, N, nb, (int)MODE_SYM, tile_begin, tile_end,
+                       (hipStream_t)stream, part, ncol, N, nb, (int)MODE_SYM, tile_begin, tile_end,
                        scale, dcoords);
     HICGAT_CHECK_LAUNCH();
   }
   double *mpart = mom + (size_t)tiles * 8;
-  hipLaunchKernelGGL(moments_partial_kernel, dim3(kMomBlocks), dim3(256), 0, (hipStream_t)stream, mom,
+  hipLaunchKernelGGL(moments_partial_kernel, dim3(kMomBlocks), dim3(256), 0, (hipStream_t)stream, mom, ncol,
                      tile_begin, tile_end, mpart);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, stats);

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--workload", default="synth-20000")
+    ap.add_argument("--only", default="", help="comma-separated job-name substrings to run")
     a = ap.parse_args()
     import bench
     import hicgat
@@ -109,6 +110,9 @@ def main():
         "torch_dw_densea": lambda K: ya.t().mm(out),
         "torch_fwd_densea": lambda K: torch.nn.functional.linear(out, Wa, ba),
     }
+    if a.only:
+        keys = [k.strip() for k in a.only.split(",") if k.strip()]
+        jobs = {k: v for k, v in jobs.items() if any(x in k for x in keys)}
     res = {}
     for r in range(a.rounds):
         for lname, K in kset:
