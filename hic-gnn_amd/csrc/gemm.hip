@@ -27,7 +27,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 constexpr int GK = HICGAT_GK;  // K-step of the fp32 kernel
 
-template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB>
+// CS (weight gradients, A_KM only): the workgroups of the first column tile also sum their A tile
+// over K, i.e. the bias gradient db[m] = sum_k dY[k][m] of the same Linear comes out of the dW
+// GEMM (its per-split partials go into the slab beside the dW partials, one slab sum for both).
+template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB, bool CS = false>
 #ifndef HICGAT_GEMM_OCC64
 // min blocks per CU of the 64 x 128 fp32 kernel: 6 makes the compiler keep the accumulators in
 // VGPRs (74 in all, 6 waves per SIMD instead of 4): fwd 512x512 0.104 vs 0.115 ms, dX 0.057 vs
@@ -43,7 +46,9 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
                                                    int K, int kchunk, const float *__restrict__ bias,
-                                                   float *__restrict__ slab, int accumulate) {
+                                                   float *__restrict__ slab, int64_t slab_stride, int accumulate,
+                                                   float *__restrict__ csum) {
+  static_assert(!CS || A_KM, "column sums of A need the K-major (weight-gradient) layout");
   constexpr int WM = BM / 2, WN = BN / 2;        // wave tile (4 waves in 2 x 2)
   constexpr int TM = WM / 32, TN = WN / 32;      // 32x32 MFMA tiles per wave
   // staged values per thread: VEC -> float4 pieces, else scalars
@@ -148,6 +153,15 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
     }
   };
+  // CS: thread t < BM adds column t of every staged A tile, k in order (deterministic)
+  const bool cs_on = CS && blockIdx.y == 0 && tid < BM;
+  float cs = 0.f;
+  auto colacc = [&](int cb) {
+    if (cs_on) {
+#pragma unroll
+      for (int kk = 0; kk < GK; ++kk) cs += As[cb][kk][tid];
+    }
+  };
   if (kb < ke) load(kb);
   if (DB) {
     // stage k0 + GK into the other buffer while k0's MFMAs run; one barrier per K-step
@@ -158,6 +172,7 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
       const bool more = k0 + GK < ke;
       if (more) load(k0 + GK);
       mma(cur);
+      colacc(cur);
       if (more) store(cur ^ 1);
       __syncthreads();
       cur ^= 1;
@@ -169,11 +184,20 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
       __syncthreads();
       if (k0 + GK < ke) load(k0 + GK);
       mma(0);
+      colacc(0);
+    }
+  }
+  if (cs_on && m0 + tid < M) {
+    if (slab) {
+      csum[(size_t)blockIdx.z * slab_stride + tid + m0] = cs;      // csum = this launch's slab + M*N
+    } else {
+      float *o = csum + m0 + tid;
+      *o = cs + (accumulate ? *o : 0.f);
     }
   }
 
   // C/D map of a 32x32 f32 tile: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float *out = slab ? slab + (size_t)blockIdx.z * M * N : C;
+  float *out = slab ? slab + (size_t)blockIdx.z * slab_stride : C;
   const int64_t ldo = slab ? N : ldc;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
@@ -436,26 +460,38 @@ __global__ void colsum_zero_kernel(float *out, int N, int accumulate) {
 #ifndef HICGAT_GEMM_DB_ALL
 #define HICGAT_GEMM_DB_ALL 0   // 1: double-buffered LDS for every layout (A/B build; default: dX layout only)
 #endif
+// csum (weight gradients only): also db[m] (+)= sum_k A[k][m] (the CS kernels); the slab of split z
+// is then [M*N dW partials | M db partials].
 template <int BM, int BN, bool AK, bool BK_>
 static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
-                  int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
+                  int K, int splits, const float *bias, float *slab, int acc, hipStream_t s, float *csum = nullptr) {
   const int kchunk = ((K + splits - 1) / splits + GK - 1) / GK * GK;
   const dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
   // float4 staging needs every float4 inside its operand row and 16-B aligned rows
   const bool a_ok = AK ? (M % 4 == 0 && lda % 4 == 0) : (K % 4 == 0 && lda % 4 == 0);
   const bool b_ok = BK_ ? (N % 4 == 0 && ldb % 4 == 0) : (K % 4 == 0 && ldb % 4 == 0);
   const bool al = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
-  if (a_ok && b_ok && al)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, true, HICGAT_GEMM_DB_ALL ? true : (!AK && BK_)>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N,
-                       K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
-  else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, false, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M,
-                       N, K, kchunk, bias, splits > 1 ? slab : nullptr, acc);
+  const bool cs = AK && csum != nullptr;
+  const int64_t stride = (int64_t)M * N + (cs ? M : 0);
+  float *sl = splits > 1 ? slab : nullptr;
+  float *cdst = cs ? (sl ? slab + (int64_t)M * N : csum) : nullptr;
+#define HICGAT_GEMM_GO(V, D, C_)                                                                            \
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, V, D, C_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, \
+                     K, kchunk, bias, sl, stride, acc, cdst)
+  if (a_ok && b_ok && al) {
+    constexpr bool db = HICGAT_GEMM_DB_ALL ? true : (!AK && BK_);
+    if (cs) HICGAT_GEMM_GO(true, db, AK);
+    else HICGAT_GEMM_GO(true, db, false);
+  } else {
+    if (cs) HICGAT_GEMM_GO(false, false, AK);
+    else HICGAT_GEMM_GO(false, false, false);
+  }
+#undef HICGAT_GEMM_GO
   HICGAT_CHECK_LAUNCH();
   if (splits > 1) {
-    // C[m][n] = sum_z slab[z][m][n] (+ bias[n]) (+ C), splits added in order
-    const ColOut o{C, ldc, N, nullptr, bias, acc};
-    return colsum_wide_launch(slab, (int64_t)M * N, splits, (int64_t)M * N, o, s);
+    // C[m][n] = sum_z slab[z][m][n] (+ bias[n]) (+ C), splits added in order; db likewise
+    const ColOut o{C, ldc, N, nullptr, bias, acc, cs ? csum : nullptr, (int64_t)M * N};
+    return colsum_wide_launch(slab, stride, splits, stride, o, s);
   }
   return HICGAT_OK;
 }
@@ -469,7 +505,7 @@ static int launch_x3(const float *A, int64_t lda, const float *B, int64_t ldb, f
                      bias, splits > 1 ? slab : nullptr, acc);
   HICGAT_CHECK_LAUNCH();
   if (splits > 1) {
-    const ColOut o{C, ldc, N, nullptr, bias, acc};
+    const ColOut o{C, ldc, N, nullptr, bias, acc, nullptr, 0};
     return colsum_wide_launch(slab, (int64_t)M * N, splits, (int64_t)M * N, o, s);
   }
   return HICGAT_OK;
@@ -544,6 +580,27 @@ extern "C" int hicgat_gemm_ex(int a_kmajor, int b_kmajor, int M, int N, int K, c
   if (!a_kmajor && b_kmajor) return dispatch<false, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, i, s);
   if (a_kmajor && !b_kmajor) return dispatch<true, false>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, i, s);
   return dispatch<true, true>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, accumulate, i, s);
+}
+
+extern "C" size_t hicgat_gemm_wgrad_workspace_bytes(int M, int N, int splits) {
+  return splits > 1 ? (size_t)splits * ((size_t)M * N + M) * sizeof(float) : 0;
+}
+
+extern "C" int hicgat_gemm_wgrad(int M, int N, int K, const float *dY, int64_t ldy, const float *X, int64_t ldx,
+                                 float *dW, int64_t lddw, float *db, int accumulate, int splits, void *workspace,
+                                 size_t workspace_bytes, hicgat_stream_t stream) {
+  if (M < 0 || N < 0 || K < 0 || splits < 1 || lddw < N) return HICGAT_EINVAL;
+  if (M == 0 || N == 0) return HICGAT_OK;
+  if (!dY || !X || !dW) return HICGAT_EINVAL;
+  if (splits > 1 && (!workspace || workspace_bytes < hicgat_gemm_wgrad_workspace_bytes(M, N, splits)))
+    return HICGAT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  float *slab = static_cast<float *>(workspace);
+  // the dispatch of hicgat_gemm_ex's fp32 path for the (K-major, K-major) layout
+  if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
+    return launch<128, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
+  if (N >= 128) return launch<64, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
+  return launch<64, 64, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
 }
 
 extern "C" size_t hicgat_colsum_workspace_bytes(int K, int N) { return colsum_workspace_bytes(K, N); }

@@ -18,6 +18,11 @@
 namespace hicgat {
 
 __device__ __forceinline__ void colout_write(const ColOut &o, int64_t i, float s) {
+  if (o.tail && i >= o.tail_start) {
+    float *dst = o.tail + (i - o.tail_start);
+    *dst = s + (o.accumulate ? *dst : 0.f);
+    return;
+  }
   const int64_t row = i / o.cols, col = i % o.cols;
   float *dst = (row == 1 && o.out1) ? o.out1 + col : o.out0 + row * o.ld + col;
   if (o.bias) s += o.bias[col];

@@ -12,6 +12,8 @@ struct ColOut {
   float *out1;          // if set, row 1 goes here instead (LayerNorm dbeta)
   const float *bias;    // added per column (split-K GEMM epilogue), may be null
   int accumulate;       // add the previous value of the destination
+  float *tail;          // if set, elements from tail_start on go to tail[i - tail_start] (GEMM: db)
+  int64_t tail_start;
 };
 
 // Sum rows [0, K) of A [K, N] (leading dim lda) into the ColOut target.  ws: colsum_workspace_bytes.

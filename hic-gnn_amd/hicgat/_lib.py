@@ -55,6 +55,9 @@ SIGNATURES = {
     "hicgat_gemm_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
     "hicgat_gemm_ex": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                                c_int, c_int, c_p, c_sz, c_p]),
+    "hicgat_gemm_wgrad": (c_int, [c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_p,
+                                  c_sz, c_p]),
+    "hicgat_gemm_wgrad_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_ln_relu_res_fwd": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_p]),

@@ -246,12 +246,14 @@ class ShardedTrainer:
             self.gbuf[q0:q1].copy_(o.grad)
             # act: writes dout = g * relu'(out) straight into the packed rows; otherwise dout is g
             K.agg_bwd_rows(q0, q1, self.act, self.gbuf, self.out, self.bias.detach(), self.out2, dout, self.rs)
+            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the all-gather + source pass
             if not self.act:
                 dout[q0:q1].copy_(self.gbuf[q0:q1])
             rs_all[q0:q1].copy_(self.rs[q0:q1])
             _all_gather_inplace(self.pack, self._own(self.pack), g)
             K.agg_bwd_src(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, rs_all, dout, al, ar, self.ns,
                           self.dh, self.da_src)
+            ops.side_flush(after=fork)
             dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
             K.param_grad(self.h[q0:q1], dout[q0:q1].contiguous(), self.da_src[q0:q1], self.rs[q0:q1], self.H,
                          out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)

@@ -218,6 +218,21 @@ class HipKernels:
                        "hicgat_gemm_ex")
         return C
 
+    def wgrad(self, dy, x, W_out, b_out=None, accumulate=False, splits=1):
+        """dW = dy^T x and db = column sums of dy (``b_out`` may be None) in one split-K GEMM."""
+        K_, M = dy.shape
+        N = x.shape[1]
+        dev = W_out.device
+        ws = None
+        if splits > 1:
+            ws = _lib.workspace(self.lib.hicgat_gemm_wgrad_workspace_bytes(M, N, splits), dev)
+        with _timed("gemm_dw"):
+            _lib.check(self.lib.hicgat_gemm_wgrad(M, N, K_, P(dy), dy.stride(0), P(x), x.stride(0), P(W_out),
+                                                  W_out.stride(0), P(b_out), int(accumulate), int(splits), P(ws),
+                                                  0 if ws is None else ws.numel(), _lib.stream(dev)),
+                       "hicgat_gemm_wgrad")
+        return W_out, b_out
+
     def colsum(self, A, out, accumulate=False):
         K, N = A.shape
         ws = _lib.workspace(self.lib.hicgat_colsum_workspace_bytes(K, N), A.device)

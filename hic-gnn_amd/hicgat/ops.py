@@ -32,13 +32,20 @@ def _sink(p):
 # L2-bound aggregation backward instead of in series with it; in a captured step the fork and join
 # are graph edges.  Only sink-bound gradients (``_sink``) go to the side stream -- a gradient that
 # is returned to autograd is consumed on the backward's stream and must be produced there.
-_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": []}
+_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": []}
 _SIDE_LOCK = threading.Lock()
 OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
-# LayerNorm dgamma/dbeta reductions on the side stream too (else inside the row-pass call)
-LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "0") != "0"     # measured slower
+# LayerNorm dgamma/dbeta reductions on the side stream too (else inside the row-pass call): measured
+# slower, with and without deferral
+LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "0") != "0"
 # bias column sums / GAT param_grad on the side stream (else on the backward's stream)
 SMALL_SIDE = os.environ.get("HICGAT_SMALL_SIDE", "1") != "0"
+# Deferred side work (HICGAT_DEFER=1): the tail's parameter-gradient launches are queued and issued
+# by ``side_flush`` beside the GAT source-side gather pass (forked after the gather-free row pass).
+# Measured slower than issuing them as they come (2.094 vs 2.082 ms per graph step): the 5000-block
+# gather grid holds every CU slot, so the side kernels wait for slots and run 5-10x longer; beside
+# the tail backward's small kernels they find room.  Off by default; the mechanism stays for A/B.
+DEFER_DEFAULT = os.environ.get("HICGAT_DEFER", "0") != "0"
 
 
 def side_begin():
@@ -47,14 +54,42 @@ def side_begin():
         _SIDE["on"] += 1
 
 
-def side_join():
-    """Make every stream that forked work onto the side stream wait for it; drop the held inputs."""
+def side_mark():
+    """An event on the current stream marking where queued side work may start (``side_flush``)."""
+    if not _SIDE["on"] or not _SIDE["queue"]:
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev
+
+
+def side_flush(after=None):
+    """Issue the queued parameter-gradient launches on the side stream, forked from the current
+    stream at this point, or from the earlier point ``after`` (an event from ``side_mark``): the
+    caller can then enqueue its own next kernel first, so a captured graph lists that kernel
+    ahead of the side branch (they read only tensors produced before the fork point)."""
     with _SIDE_LOCK:
-        _SIDE["on"] = max(0, _SIDE["on"] - 1)
-        for dev, main in _SIDE["mains"].items():
-            main.wait_stream(_SIDE["streams"][dev])
-        _SIDE["mains"].clear()
-        _SIDE["hold"].clear()
+        queue, _SIDE["queue"] = _SIDE["queue"], []
+    if not queue:
+        return
+    with _side(*[t for _, keep in queue for t in keep], after=after):
+        for fn, _ in queue:
+            fn()
+
+
+def side_join():
+    """Flush the queue, make every stream that forked work onto the side stream wait for it, and
+    drop the held inputs.  Always runs the queued launches, even after an exception upstream, so
+    no gradient kernel is left behind for a later step."""
+    try:
+        side_flush()
+    finally:
+        with _SIDE_LOCK:
+            _SIDE["on"] = max(0, _SIDE["on"] - 1)
+            for dev, main in _SIDE["mains"].items():
+                main.wait_stream(_SIDE["streams"][dev])
+            _SIDE["mains"].clear()
+            _SIDE["hold"].clear()
 
 
 @contextlib.contextmanager
@@ -71,16 +106,31 @@ def overlapped_param_grads(enabled=None):
         side_join()
 
 
+def _param_launch(fn, *keep, small=False):
+    """Launch a sink-bound parameter-gradient kernel ``fn()``: now on the current stream when not
+    overlapping; queued for ``side_flush`` when deferring; else now on the side stream.  ``keep``
+    are the tensors ``fn`` reads (held until the join)."""
+    if not _SIDE["on"]:
+        fn()
+    elif DEFER_DEFAULT:
+        with _SIDE_LOCK:
+            _SIDE["queue"].append((fn, keep))
+    else:
+        with (_side_small(*keep) if small else _side(*keep)):
+            fn()
+
+
 def _side_small(*keep):
     """``_side`` for the small parameter reductions (column sums), unless SMALL_SIDE is off."""
     return _side(*keep) if SMALL_SIDE else contextlib.nullcontext()
 
 
-def _side(*keep):
+def _side(*keep, after=None):
     """Stream context for a sink-bound gradient kernel: the side stream (after a fork from the
-    current stream) while overlapping, else a no-op.  ``keep`` are the inputs the side kernels
-    read; they stay referenced until the join so the caching allocator cannot hand their memory
-    to a later backward kernel while the side stream still reads it."""
+    current stream, or from the event ``after``) while overlapping, else a no-op.  ``keep`` are
+    the inputs the side kernels read; they stay referenced until the join so the caching
+    allocator cannot hand their memory to a later backward kernel while the side stream still
+    reads it."""
     if not _SIDE["on"]:
         return contextlib.nullcontext()
     cur = torch.cuda.current_stream()
@@ -91,7 +141,10 @@ def _side(*keep):
             side = _SIDE["streams"][dev] = torch.cuda.Stream(device=dev)
         _SIDE["mains"].setdefault(dev, cur)
         _SIDE["hold"].extend(keep)
-    side.wait_stream(cur)
+    if after is not None:
+        side.wait_event(after)
+    else:
+        side.wait_stream(cur)
     return torch.cuda.stream(side)
 
 
@@ -159,6 +212,7 @@ class _GATConvFn(torch.autograd.Function):
             K.agg_bwd_rows(0, N, ctx.act, g, out, b, out2, dout, row_stats)
         else:
             K.agg_bwd_rows(0, N, 0, dout, out, b, out2, None, row_stats)
+        fork = side_mark()   # the tail's queued dW / db launches run beside the source pass below
         dh = torch.empty_like(h)
         da_src = torch.empty_like(a_src)
         pW, pl, pr, pb = ctx.params
@@ -172,19 +226,21 @@ class _GATConvFn(torch.autograd.Function):
         datt_l = datt_r = dbias = dW = None
         for c, (r0, r1) in enumerate(_src_chunks(N)):
             K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+            if c == 0:
+                side_flush(after=fork)
             rows = slice(r0, r1)
             if use_sinks:
-                with _side_small(h, dout, da_src, row_stats):
-                    K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                                 out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
+                _param_launch(lambda rows=rows: K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
+                                                             out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
+                                                             accumulate=True),
+                              h, dout, da_src, row_stats, small=True)
             else:
                 datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
                                                      out=None if c == 0 else (datt_l, datt_r, dbias),
                                                      accumulate=c > 0)
             if ctx.needs_input_grad[1]:
                 if gW is not None:
-                    with _side(dh, x):
-                        weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True)
+                    _param_launch(lambda rows=rows: weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True), dh, x)
                 else:
                     dW = weight_grad(K, dh[rows], x[rows], out=dW, accumulate=dW is not None)
         if not use_sinks:
@@ -226,18 +282,43 @@ def _weight_grad_to(K, p, dy, x):
     """dW = dy^T x into the parameter's sink (returns None) or a new tensor (returned)."""
     g = _sink(p)
     if g is not None:
-        with _side(dy, x):
-            weight_grad(K, dy, x, out=g, accumulate=True)
+        _param_launch(lambda: weight_grad(K, dy, x, out=g, accumulate=True), dy, x)
         return None
     return weight_grad(K, dy, x)
+
+
+def _wb_grad_to(K, pW, pb, dy, x, need_w=True, need_b=True):
+    """A Linear's dW = dy^T x and db = column sums of dy: ONE fp32 GEMM launch computes both
+    (``hicgat_gemm_wgrad``, db from the staged dY tiles).  Into the parameters' sinks (returns
+    (None, None); on the side stream when overlapping) or new tensors (returned).  Falls back to
+    separate GEMM / column-sum launches when only one of the two is wanted, when the sinks are
+    mixed, or when the x3 GEMM arithmetic was selected (HICGAT_GEMM)."""
+    need_b = need_b and pb is not None
+    if not need_w or K.gemm_impl != 1:
+        dW = _weight_grad_to(K, pW, dy, x) if need_w else None
+        db = _bias_grad_to(K, pb, dy) if need_b else None
+        return dW, db
+    gW = _sink(pW)
+    gb = _sink(pb) if need_b else None
+    rows, m = dy.shape
+    n = x.shape[1]
+    sp = _splits(m, n, rows)
+    if gW is not None and (gb is not None or not need_b):
+        _param_launch(lambda: K.wgrad(dy, x, gW, gb, accumulate=True, splits=sp), dy, x)
+        return None, None
+    if gW is None and (not need_b or _sink(pb) is None):
+        dW = torch.empty((m, n), dtype=torch.float32, device=dy.device)
+        db = torch.empty(m, dtype=torch.float32, device=dy.device) if need_b else None
+        K.wgrad(dy, x, dW, db, splits=sp)
+        return dW, db
+    return _weight_grad_to(K, pW, dy, x), _bias_grad_to(K, pb, dy)
 
 
 def _bias_grad_to(K, p, dy):
     """db = column sums of dy into the parameter's sink (returns None) or a new tensor."""
     g = _sink(p)
     if g is not None:
-        with _side_small(dy):
-            K.colsum(dy, g, accumulate=True)
+        _param_launch(lambda: K.colsum(dy, g, accumulate=True), dy, small=True)
         return None
     return K.colsum(dy, torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device))
 
@@ -268,10 +349,8 @@ class _LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, M, n_in, n_out, dy, W.contiguous(), torch.empty_like(x), name="gemm_dx")
-        if ctx.needs_input_grad[1]:
-            dW = _weight_grad_to(K, ctx.params[0], dy, x)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _bias_grad_to(K, ctx.params[1], dy)
+        dW, db = _wb_grad_to(K, ctx.params[0], ctx.params[1], dy, x, need_w=ctx.needs_input_grad[1],
+                             need_b=ctx.has_bias and ctx.needs_input_grad[2])
         return dx, dW, db
 
 
@@ -312,10 +391,8 @@ class _DualLinearFn(torch.autograd.Function):
             dx = K.gemm(0, 1, M, n_in, W1.shape[0], dy1, W1, torch.empty_like(x), name="gemm_dx")
             K.gemm(0, 1, M, n_in, W2.shape[0], dy2, W2, dx, accumulate=True, name="gemm_dx")
         pW1, pb1, pW2, pb2 = ctx.params
-        dW1 = _weight_grad_to(K, pW1, dy1, x)
-        dW2 = _weight_grad_to(K, pW2, dy2, x)
-        db1 = _bias_grad_to(K, pb1, dy1)
-        db2 = _bias_grad_to(K, pb2, dy2)
+        dW1, db1 = _wb_grad_to(K, pW1, pb1, dy1, x)
+        dW2, db2 = _wb_grad_to(K, pW2, pb2, dy2, x)
         return dx, dW1, db1, dW2, db2
 
 
@@ -352,8 +429,7 @@ class _LnReluResFn(torch.autograd.Function):
         elif sg is not None and sb is not None:
             ws = K.ln_workspace(y.shape[1], y.device)
             K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, None, None, ws=ws)
-            with _side(ws):
-                K.ln_relu_res_bwd_params(y.shape[1], sg, sb, ws, accumulate=True)
+            _param_launch(lambda: K.ln_relu_res_bwd_params(y.shape[1], sg, sb, ws, accumulate=True), ws)
             dgamma = dbeta = None
         else:
             dgamma = torch.empty_like(gamma)
@@ -427,8 +503,7 @@ class _DualLnReluResFn(torch.autograd.Function):
         elif sg is not None and sb is not None:
             ws = K.ln_workspace(w, dz.device)
             K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], None, None, dres=dY[:, w:], ws=ws)
-            with _side(ws):
-                K.ln_relu_res_bwd_params(w, sg, sb, ws, accumulate=True)
+            _param_launch(lambda: K.ln_relu_res_bwd_params(w, sg, sb, ws, accumulate=True), ws)
         else:
             dgamma, dbeta = torch.empty_like(gamma), torch.empty_like(beta)
             K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], dgamma, dbeta, dres=dY[:, w:])
@@ -438,18 +513,23 @@ class _DualLnReluResFn(torch.autograd.Function):
                         name="gemm_dx")
         sW1, sW2, sb1, sb2 = _sink(W1), _sink(W2), _sink(b1), _sink(b2)
         dW1 = dW2 = db1 = db2 = None
-        if sW1 is not None and sW2 is not None and _adjacent(sW1, sW2):
-            with _side(dY, x):
-                weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True)
+        w_pair = sW1 is not None and sW2 is not None and _adjacent(sW1, sW2)
+        b_pair = sb1 is not None and sb2 is not None and _adjacent(sb1, sb2)
+        if w_pair and b_pair and K.gemm_impl == 1:
+            # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
+            gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
+            _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x)
         else:
-            dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
-            dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
-        if sb1 is not None and sb2 is not None and _adjacent(sb1, sb2):
-            with _side_small(dY):
-                K.colsum(dY, _joined(sb1, sb2), accumulate=True)
-        else:
-            db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
-            db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
+            if w_pair:
+                _param_launch(lambda: weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True), dY, x)
+            else:
+                dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
+                dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
+            if b_pair:
+                _param_launch(lambda: K.colsum(dY, _joined(sb1, sb2), accumulate=True), dY, small=True)
+            else:
+                db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
+                db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
         return dx, dW1, db1, dW2, db2, dgamma, dbeta, None
 
 
@@ -549,12 +629,10 @@ class _SageConvFn(torch.autograd.Function):
         dout = dout.contiguous()
         dx = dWl = db = dWr = None
         pWl, pbl, pWr = ctx.params
-        if ctx.needs_input_grad[1]:
-            dWl = _weight_grad_to(K, pWl, dout, z[:, :F])
+        dWl, db = _wb_grad_to(K, pWl, pbl, dout, z[:, :F], need_w=ctx.needs_input_grad[1],
+                              need_b=has_b and ctx.needs_input_grad[2])
         if root and ctx.needs_input_grad[3]:
             dWr = _weight_grad_to(K, pWr, dout, z[:, F:])
-        if has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad_to(K, pbl, dout)
         if ctx.needs_input_grad[0]:
             dagg = K.gemm(0, 1, N, F, dout.shape[1], dout, W_l.contiguous(),
                           torch.empty((N, F), dtype=torch.float32, device=dout.device), name="gemm_dx")

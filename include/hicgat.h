@@ -203,6 +203,18 @@ enum { HICGAT_GEMM_AUTO = 0, HICGAT_GEMM_F32 = 1, HICGAT_GEMM_X3 = 2 };
 int hicgat_gemm_ex(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A, int64_t lda,
                    const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
                    int splits, int impl, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+/* Weight AND bias gradient of a Linear in one GEMM (replaces the dW GEMM + bias column sum of the
+ * Linear backward, torch.nn.Linear via ATen addmm_backward / sum(0), models.py:637-659):
+ *   dW[M,N] (+)= dY^T X  (dY [K,M] and X [K,N] row-major, K = node rows),
+ *   db[M]   (+)= sum_k dY[k][m]  (db may be NULL)
+ * the workgroups of the first column tile sum their staged dY tile over K; with splits > 1 the
+ * per-split db partials sit in the slab beside the dW partials and ONE slab sum (split order,
+ * deterministic) writes both.  fp32 MFMA (HICGAT_GEMM_F32 arithmetic).  Workspace:
+ * hicgat_gemm_wgrad_workspace_bytes(M, N, splits). */
+int hicgat_gemm_wgrad(int M, int N, int K, const float *dY, int64_t ldy, const float *X, int64_t ldx, float *dW,
+                      int64_t lddw, float *db, int accumulate, int splits, void *workspace, size_t workspace_bytes,
+                      hicgat_stream_t stream);
+size_t hicgat_gemm_wgrad_workspace_bytes(int M, int N, int splits);
 /* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
 int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                   size_t workspace_bytes, hicgat_stream_t stream);
