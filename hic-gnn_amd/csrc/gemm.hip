@@ -16,6 +16,8 @@
 // K-step is prefetched into registers under the current step's MFMAs.  K can be split over
 // gridDim.z: each split writes an fp32 partial slab and a second kernel adds the slabs in split
 // order (deterministic, no float atomics; reduce.hip).
+#include <cstdlib>
+
 #include "reduce.hpp"
 
 namespace hicgat {
@@ -520,9 +522,23 @@ static bool x3_ok(const float *A, int64_t lda, const float *B, int64_t ldb, int 
   return a_ok && b_ok && al && N >= 64 && M >= 32;
 }
 
+int gemm_tall_launch(bool b_kmajor, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
+                     int M, int N, int K, const float *bias, int accumulate, hipStream_t s);   // gemm_tall.hip
+
+// HICGAT_GEMM_TALL=0 (A/B measurement only): the 64x128 kernel for the tall problems too
+static bool tall_enabled() {
+  static const bool on = !(getenv("HICGAT_GEMM_TALL") && atoi(getenv("HICGAT_GEMM_TALL")) == 0);
+  return on;
+}
+
 template <bool AK, bool BK_>
 static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
                     int K, int splits, const float *bias, float *slab, int acc, int impl, hipStream_t s) {
+  // tall node-row problems (Linear forward, input gradient): the 160x128 LDS-DMA kernel (gemm_tall.hip)
+  if (!AK && impl == HICGAT_GEMM_F32 && splits == 1 && M >= 1024 && tall_enabled()) {
+    const int rc = gemm_tall_launch(BK_, A, lda, B, ldb, C, ldc, M, N, K, bias, acc, s);
+    if (rc != HICGAT_EUNSUPPORTED) return rc;
+  }
   if (impl != HICGAT_GEMM_F32 && x3_ok<AK, BK_>(A, lda, B, ldb, M, N, K)) {
     // 128-row tiles when they alone give >= 2 blocks per CU, else 64-row tiles
     const int64_t blocks128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;

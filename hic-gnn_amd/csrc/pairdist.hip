@@ -376,10 +376,20 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
 // sums are combined in group order (fixed order: bitwise reproducible).
 constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-thread blocks)
 
+__device__ void moments_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int N, int loss_kind,
+                              double *__restrict__ stats, float *__restrict__ loss);
+
+// mom != NULL: the last block sums the tile moments and finalizes instead (moments_block)
 __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part, int ncol,
                                                                int N, int nb, int mode, int64_t t0,
                                                                int64_t t1, float scale,
-                                                               float *__restrict__ dcoords) {
+                                                               float *__restrict__ dcoords,
+                                                               const double *__restrict__ mom, int loss_kind,
+                                                               double *__restrict__ stats, float *__restrict__ loss) {
+  if (mom && blockIdx.x == gridDim.x - 1) {
+    moments_block(mom, t0, t1, N, loss_kind, stats, loss);
+    return;
+  }
   __shared__ float4 red[kRedGroups][64];
   const int lr64 = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int gi = blockIdx.x * 64 + lr64;
@@ -424,47 +434,8 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
   }
 }
 
-// stats[0..6] = sum over tiles [t0,t1) of the tile moments (fp64, fixed order): kMomBlocks blocks
-// each sum a contiguous tile range (tree over 256 threads), one block adds the block sums in order.
-constexpr int kMomBlocks = 64;
-
-__global__ __launch_bounds__(256) void moments_partial_kernel(const double *__restrict__ mom, int per, int64_t t0,
-                                                              int64_t t1, double *__restrict__ part) {
-  // mom holds `per` 8-double records per tile (1 here), units [t0*per, t1*per)
-  __shared__ double red[7][256];
-  const int64_t u0 = t0 * per, u1 = t1 * per;
-  const int64_t cnt = (u1 - u0 + kMomBlocks - 1) / kMomBlocks;
-  const int64_t b0 = u0 + (int64_t)blockIdx.x * cnt, b1 = min(u1, b0 + cnt);
-  double s[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t t = b0 + threadIdx.x; t < b1; t += 256) {
-#pragma unroll
-    for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
-  }
-#pragma unroll
-  for (int c = 0; c < 7; ++c) red[c][threadIdx.x] = s[c];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-#pragma unroll
-      for (int c = 0; c < 7; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x < 7) part[blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
-}
-
-__global__ __launch_bounds__(64) void moments_final_kernel(const double *__restrict__ part,
-                                                           double *__restrict__ stats) {
-  if (threadIdx.x >= 7) return;
-  double s = 0.0;
-  for (int b = 0; b < kMomBlocks; ++b) s += part[b * 8 + threadIdx.x];
-  stats[threadIdx.x] = s;
-}
-
-// stats[7..10] and loss from the all-reduced moments stats[0..6]: mse, pearson r, alpha, total.
-__global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, double *__restrict__ stats,
-                                                      float *__restrict__ loss) {
-  if (threadIdx.x != 0) return;
+// stats[7..10] and loss from the (all-reduced) moments stats[0..6]: mse, pearson r, alpha, total.
+__device__ void finalize_stats(int N, int loss_kind, double *__restrict__ stats, float *__restrict__ loss) {
   const double n2 = (double)N * (double)N;
   const double mse = (2.0 * stats[0] + stats[6]) / n2;
   const double M = 0.5 * (double)N * (double)(N - 1);
@@ -482,6 +453,43 @@ __global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, doub
   stats[10] = (double)totalf;
   stats[11] = 0.0;
   if (loss) loss[0] = loss_kind == 1 ? totalf : msef;
+}
+
+__global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, double *__restrict__ stats,
+                                                      float *__restrict__ loss) {
+  if (threadIdx.x == 0) finalize_stats(N, loss_kind, stats, loss);
+}
+
+// stats[0..6] = sum over tiles [t0,t1) of the tile moments, then finalize: ONE block of 1024
+// threads, each summing a contiguous tile run, combined by a fixed-shape tree (deterministic).
+// Launched as the extra last block of pairdist_reduce_kernel, so the fused loss ends in one launch
+// after the tile kernel.
+__device__ void moments_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int N, int loss_kind,
+                              double *__restrict__ stats, float *__restrict__ loss) {
+  __shared__ double red[7][256];
+  const int tid = threadIdx.x;
+  double s[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (tid < 256) {
+    const int64_t cnt = (t1 - t0 + 255) / 256;
+    const int64_t b0 = t0 + tid * cnt, b1 = min(t1, b0 + cnt);
+    for (int64_t t = b0; t < b1; ++t) {
+#pragma unroll
+      for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
+    }
+#pragma unroll
+    for (int c = 0; c < 7; ++c) red[c][tid] = s[c];
+  }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+#pragma unroll
+      for (int c = 0; c < 7; ++c) red[c][tid] += red[c][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid < 7) stats[tid] = red[tid][0];
+  __syncthreads();
+  if (tid == 0) finalize_stats(N, loss_kind, stats, loss);
 }
 
 // D[i, j] = ||c_i - c_j||: one thread per element.
@@ -519,8 +527,7 @@ static int pd_ncol(int) { return 1; }
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
   const int64_t tiles = hicgat_pairdist_num_tiles(N, mode);
   const int nc = pd_ncol(mode);
-  return (size_t)tiles * ((1 + nc) * BT * sizeof(float4) + nc * 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) +
-         256;
+  return (size_t)tiles * ((1 + nc) * BT * sizeof(float4) + nc * 8 * sizeof(double)) + 256;
 }
 
 // Host twin of tri_decode (exact integer search): tile-row of upper-triangle tile t.
@@ -573,7 +580,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
-                     dcoords);
+                     dcoords, nullptr, 0, nullptr, nullptr);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -622,22 +629,12 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
 #undef HICGAT_PD_SYM
     HICGAT_CHECK_LAUNCH();
   }
-  const int ncol = 1;
-  if (dcoords) {
-    const float scale = (float)(4.0 / ((double)N * (double)N));
-    hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
-                       (hipStream_t)stream, part, ncol, N, nb, (int)MODE_SYM, tile_begin, tile_end,
-                       scale, dcoords);
-    HICGAT_CHECK_LAUNCH();
-  }
-  double *mpart = mom + (size_t)tiles * 8;
-  hipLaunchKernelGGL(moments_partial_kernel, dim3(kMomBlocks), dim3(256), 0, (hipStream_t)stream, mom, ncol,
-                     tile_begin, tile_end, mpart);
-  HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, stats);
-  HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
-                     stats, loss);
+  // row / column partials -> dcoords (when wanted), and in the same launch the extra last block:
+  // tile moments -> stats[0..6] -> mse / r / alpha / total / loss
+  const float scale = (float)(4.0 / ((double)N * (double)N));
+  const int row_blocks = dcoords ? (N + 63) / 64 : 0;
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + 1), dim3(1024), 0, (hipStream_t)stream, part, 1, N, nb,
+                     (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, loss_kind, stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -17,6 +17,10 @@ GEMM_IMPLS = {"auto": 0, "f32": 1, "x3": 2}
 # the product default is the plain fp32 MFMA GEMM; HICGAT_GEMM=auto opts into the fp32-accurate x3
 # split where it applies (10-25 % faster GEMMs, profiles/r01_kbench_x3_sliced.txt)
 GEMM_DEFAULT = "f32"
+# lin_l + logits (a2): the tall 160x128 GEMM (gemm_tall.hip) and a separate logits pass (default,
+# 2.075 vs 2.095 ms per step) or HICGAT_LINATT=fused: the 64x256-tile kernel with the logits in its
+# epilogue
+LINATT_GEMM = os.environ.get("HICGAT_LINATT", "gemm") == "gemm"
 
 
 class _timed:
@@ -57,8 +61,8 @@ class HipKernels:
         assert h.shape == (N, H * C) and h.is_contiguous()
         a_src = torch.empty((N, H), dtype=torch.float32, device=x.device)
         a_dst = torch.empty_like(a_src)
-        if self.gemm_impl != 1 and N >= 32 and F % 4 == 0 and x.stride(0) % 4 == 0:
-            # x3 GEMM into h, then the logits in one pass over h
+        if (self.gemm_impl != 1 or LINATT_GEMM) and N >= 32 and F % 4 == 0 and x.stride(0) % 4 == 0:
+            # x3 (or, HICGAT_LINATT=gemm, the 160x128 fp32) GEMM into h, then the logits in one pass over h
             st = _lib.stream(x.device)
             with _timed("gat_linear_att"):
                 _lib.check(self.lib.hicgat_gemm_ex(0, 0, N, H * C, F, P(x), x.stride(0), P(W), W.stride(0), None, P(h),

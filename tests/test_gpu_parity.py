@@ -291,6 +291,49 @@ def test_gemm_layouts_match_torch(m, n, k):
     assert _rel(db.cpu(), dy.double().sum(0).cpu()) < 5e-6
 
 
+@pytest.mark.parametrize("m,n,k", [(20001, 512, 512), (1601, 128, 48), (2000, 384, 16)])
+def test_tall_gemm_edges_and_accumulate(m, n, k):
+    """The 160x128 LDS-DMA kernel (gemm_tall.hip) on ragged row counts, both B layouts, bias and
+    accumulate, against fp64."""
+    import hicgat
+    K = hicgat.kernels.default()
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV)
+    w = torch.randn(n, k, device=DEV)
+    b = torch.randn(n, device=DEV)
+    y0 = torch.randn(m, n, device=DEV)
+    y = K.gemm(0, 0, m, n, k, x, w, y0.clone(), bias=b, accumulate=True)
+    assert _rel(y.cpu(), (x.double() @ w.double().t() + b.double() + y0.double()).cpu()) < 5e-6
+    dy = torch.randn(m, n, device=DEV)
+    dx = K.gemm(0, 1, m, k, n, dy, w, torch.empty(m, k, device=DEV))
+    assert _rel(dx.cpu(), (dy.double() @ w.double()).cpu()) < 5e-6
+    if n % 128 == 0 and k % 16 == 0:   # same numbers with the tall kernel's strided-row operands
+        xs = torch.randn(m, k + 4, device=DEV)[:, 2:2 + k]
+        ys = K.gemm(0, 0, m, n, k, xs, w, torch.empty(m, n, device=DEV), bias=b)
+        assert _rel(ys.cpu(), (xs.double() @ w.double().t() + b.double()).cpu()) < 5e-6
+
+
+@pytest.mark.parametrize("splits", [1, 7, 78])
+def test_wgrad_bias_fold_matches_fp64(splits):
+    """hicgat_gemm_wgrad: dW = dY^T X and db = column sums of dY from ONE split-K GEMM launch (the
+    bias partials ride in the slab), accumulate on and off, against fp64."""
+    import hicgat
+    K = hicgat.kernels.default()
+    torch.manual_seed(splits)
+    for (mo, ni) in ((256, 512), (3, 64), (130, 96)):
+        dy = torch.randn(20000, mo, device=DEV)
+        x = torch.randn(20000, ni, device=DEV)
+        dW = torch.randn(mo, ni, device=DEV)
+        db = torch.randn(mo, device=DEV)
+        rW = dy.double().t() @ x.double() + dW.double()
+        rb = dy.double().sum(0) + db.double()
+        K.wgrad(dy, x, dW, db, accumulate=True, splits=splits)
+        tol = 5e-6 * max(1.0, (20000 / splits / 512) ** 0.5)
+        assert _rel(dW.cpu(), rW.cpu()) < tol and _rel(db.cpu(), rb.cpu()) < tol, (mo, ni)
+        K.wgrad(dy, x, dW, None, splits=splits)
+        assert _rel(dW.cpu(), (dy.double().t() @ x.double()).cpu()) < tol
+
+
 def test_linear_autograd_matches_torch():
     import hicgat
     torch.manual_seed(0)

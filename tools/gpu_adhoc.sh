@@ -1,10 +1,9 @@
-# ad-hoc GPU step list for one gpurun call
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 600 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
-for cfg in "HICGAT_DEFER=1 HICGAT_LN_SIDE=1" "HICGAT_DEFER=1 HICGAT_LN_SIDE=0" "HICGAT_DEFER=0 HICGAT_LN_SIDE=0"; do
+for cfg in "HICGAT_GEMM_TALL=1" "HICGAT_GEMM_TALL=0" "HICGAT_LINATT=gemm"; do
   env $cfg timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || exit $?
   echo "$cfg $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench.log)"
 done

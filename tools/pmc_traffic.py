@@ -1,6 +1,7 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-Usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [workload]]
+Usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json [workload
+       [command [commit]]]]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters).  gfx950 correction
 (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE reports exactly half of the bytes of a wide (16 B / lane)
@@ -42,6 +43,8 @@ def summarise(fetch_csv, write_csv):
 if __name__ == "__main__":
     res = summarise(sys.argv[1], sys.argv[2])
     text = json.dumps({"workload": sys.argv[4] if len(sys.argv) > 4 else "synth-20000",
+                       "command": sys.argv[5] if len(sys.argv) > 5 else None,
+                       "commit": sys.argv[6] if len(sys.argv) > 6 else None,
                        "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
                        "kernels": res}, indent=1)
     if len(sys.argv) > 3:
