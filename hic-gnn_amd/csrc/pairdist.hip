@@ -376,18 +376,19 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
 // sums are combined in group order (fixed order: bitwise reproducible).
 constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-thread blocks)
 
-__device__ void moments_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int N, int loss_kind,
-                              double *__restrict__ stats, float *__restrict__ loss);
+__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
+                                      double *__restrict__ part);
 
-// mom != NULL: the last block sums the tile moments and finalizes instead (moments_block)
+// mom != NULL: the last kMomBlocks blocks sum runs of the tile moments into mpart instead
+// (moments_partial_block); blocks [0, row_blocks) reduce the coordinate partials
 __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part, int ncol,
                                                                int N, int nb, int mode, int64_t t0,
                                                                int64_t t1, float scale,
                                                                float *__restrict__ dcoords,
-                                                               const double *__restrict__ mom, int loss_kind,
-                                                               double *__restrict__ stats, float *__restrict__ loss) {
-  if (mom && blockIdx.x == gridDim.x - 1) {
-    moments_block(mom, t0, t1, N, loss_kind, stats, loss);
+                                                               const double *__restrict__ mom, int row_blocks,
+                                                               double *__restrict__ mpart) {
+  if (mom && (int)blockIdx.x >= row_blocks) {
+    moments_partial_block(mom, t0, t1, (int)blockIdx.x - row_blocks, mpart);
     return;
   }
   __shared__ float4 red[kRedGroups][64];
@@ -460,36 +461,47 @@ __global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, doub
   if (threadIdx.x == 0) finalize_stats(N, loss_kind, stats, loss);
 }
 
-// stats[0..6] = sum over tiles [t0,t1) of the tile moments, then finalize: ONE block of 1024
-// threads, each summing a contiguous tile run, combined by a fixed-shape tree (deterministic).
-// Launched as the extra last block of pairdist_reduce_kernel, so the fused loss ends in one launch
-// after the tile kernel.
-__device__ void moments_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int N, int loss_kind,
-                              double *__restrict__ stats, float *__restrict__ loss) {
-  __shared__ double red[7][256];
+// Tile moments over [t0,t1) in two fixed-order stages (deterministic): kMomBlocks extra blocks of
+// pairdist_reduce_kernel each sum a contiguous tile run (256 threads, each a strided subset with
+// its loads in flight, then a fixed tree) into part[b][0..6]; moments_finalize_kernel adds the
+// kMomBlocks partials in block order into stats[0..6] and finalizes.
+constexpr int kMomBlocks = 64;
+
+__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
+                                      double *__restrict__ part) {
+  __shared__ double mred[7][256];
   const int tid = threadIdx.x;
+  const int64_t per = (t1 - t0 + kMomBlocks - 1) / kMomBlocks;
+  const int64_t b0 = t0 + (int64_t)blk * per, b1 = min(t1, b0 + per);
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
   if (tid < 256) {
-    const int64_t cnt = (t1 - t0 + 255) / 256;
-    const int64_t b0 = t0 + tid * cnt, b1 = min(t1, b0 + cnt);
-    for (int64_t t = b0; t < b1; ++t) {
+    for (int64_t t = b0 + tid; t < b1; t += 256) {
 #pragma unroll
       for (int c = 0; c < 7; ++c) s[c] += mom[(size_t)t * 8 + c];
     }
 #pragma unroll
-    for (int c = 0; c < 7; ++c) red[c][tid] = s[c];
+    for (int c = 0; c < 7; ++c) mred[c][tid] = s[c];
   }
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o) {
 #pragma unroll
-      for (int c = 0; c < 7; ++c) red[c][tid] += red[c][tid + o];
+      for (int c = 0; c < 7; ++c) mred[c][tid] += mred[c][tid + o];
     }
     __syncthreads();
   }
-  if (tid < 7) stats[tid] = red[tid][0];
+  if (tid < 7) part[blk * 8 + tid] = mred[tid][0];
+}
+
+__global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__restrict__ part, int N, int loss_kind,
+                                                              double *__restrict__ stats, float *__restrict__ loss) {
+  if (threadIdx.x < 7) {
+    double s = 0.0;
+    for (int b = 0; b < kMomBlocks; ++b) s += part[b * 8 + threadIdx.x];
+    stats[threadIdx.x] = s;
+  }
   __syncthreads();
-  if (tid == 0) finalize_stats(N, loss_kind, stats, loss);
+  if (threadIdx.x == 0) finalize_stats(N, loss_kind, stats, loss);
 }
 
 // D[i, j] = ||c_i - c_j||: one thread per element.
@@ -527,7 +539,8 @@ static int pd_ncol(int) { return 1; }
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
   const int64_t tiles = hicgat_pairdist_num_tiles(N, mode);
   const int nc = pd_ncol(mode);
-  return (size_t)tiles * ((1 + nc) * BT * sizeof(float4) + nc * 8 * sizeof(double)) + 256;
+  return (size_t)tiles * ((1 + nc) * BT * sizeof(float4) + nc * 8 * sizeof(double)) + kMomBlocks * 8 * sizeof(double) +
+         256;
 }
 
 // Host twin of tri_decode (exact integer search): tile-row of upper-triangle tile t.
@@ -580,7 +593,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
-                     dcoords, nullptr, 0, nullptr, nullptr);
+                     dcoords, nullptr, 0, nullptr);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -629,12 +642,16 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
 #undef HICGAT_PD_SYM
     HICGAT_CHECK_LAUNCH();
   }
-  // row / column partials -> dcoords (when wanted), and in the same launch the extra last block:
-  // tile moments -> stats[0..6] -> mse / r / alpha / total / loss
+  // row / column partials -> dcoords (when wanted) and, in the same launch, kMomBlocks blocks of
+  // tile-moment partials; then one small launch: partials -> stats[0..6] -> mse / r / alpha / total
   const float scale = (float)(4.0 / ((double)N * (double)N));
   const int row_blocks = dcoords ? (N + 63) / 64 : 0;
-  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + 1), dim3(1024), 0, (hipStream_t)stream, part, 1, N, nb,
-                     (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, loss_kind, stats, loss);
+  double *mpart = mom + (size_t)tiles * 8;
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, (hipStream_t)stream, part,
+                     1, N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, row_blocks, mpart);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, N, loss_kind, stats,
+                     loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

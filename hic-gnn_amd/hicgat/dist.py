@@ -255,13 +255,16 @@ class ShardedTrainer:
                           self.dh, self.da_src)
             ops.side_flush(after=fork)
             dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
+            with torch.no_grad():
+                # lin_l's dW on the side stream (joined before the gradient all-reduce), param_grad
+                # beside it on this stream
+                with ops._side(self.dh, self.x_loc):
+                    if self.x_loc.is_cuda:
+                        weight_grad(K, self.dh[q0:q1], self.x_loc, out=self.W.grad, accumulate=True)
+                    else:
+                        self.W.grad.addmm_(self.dh[q0:q1].t(), self.x_loc)
             K.param_grad(self.h[q0:q1], dout[q0:q1].contiguous(), self.da_src[q0:q1], self.rs[q0:q1], self.H,
                          out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)
-            with torch.no_grad():
-                if self.x_loc.is_cuda:
-                    weight_grad(K, self.dh[q0:q1], self.x_loc, out=self.W.grad, accumulate=True)
-                else:
-                    self.W.grad.addmm_(self.dh[q0:q1].t(), self.x_loc)
         dist.all_reduce(self.opt.grad, group=g)
         self.opt.step()
         return self.loss, self.stats, coords

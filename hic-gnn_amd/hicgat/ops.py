@@ -40,12 +40,16 @@ OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
 LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "0") != "0"
 # bias column sums / GAT param_grad on the side stream (else on the backward's stream)
 SMALL_SIDE = os.environ.get("HICGAT_SMALL_SIDE", "1") != "0"
-# Deferred side work (HICGAT_DEFER=1): the tail's parameter-gradient launches are queued and issued
-# by ``side_flush`` beside the GAT source-side gather pass (forked after the gather-free row pass).
-# Measured slower than issuing them as they come (2.094 vs 2.082 ms per graph step): the 5000-block
-# gather grid holds every CU slot, so the side kernels wait for slots and run 5-10x longer; beside
-# the tail backward's small kernels they find room.  Off by default; the mechanism stays for A/B.
-DEFER_DEFAULT = os.environ.get("HICGAT_DEFER", "0") != "0"
+# Deferred side work (HICGAT_DEFER=1, the default): the tail's parameter-gradient launches are
+# queued and issued by ``side_flush`` beside the GAT source-side gather pass (forked after the
+# gather-free row pass).  Issued as they come instead (HICGAT_DEFER=0), a captured step's graph
+# places some of them in front of the aggregation backward on its queue: 2.036 vs 2.060 ms per
+# graph step.
+DEFER_DEFAULT = os.environ.get("HICGAT_DEFER", "1") != "0"
+SIDE_PRIO = int(os.environ.get("HICGAT_SIDE_PRIO", "0"))
+# lin_l's dW on the backward's own stream right after the source pass (1, default: 2.011 / 2.014 ms
+# per step) or queued onto the side stream behind the tail's dW work (0: 2.037 / 2.037 ms)
+LINL_MAIN = os.environ.get("HICGAT_LINL_MAIN", "1") != "0"
 
 
 def side_begin():
@@ -86,8 +90,8 @@ def side_join():
     finally:
         with _SIDE_LOCK:
             _SIDE["on"] = max(0, _SIDE["on"] - 1)
-            for dev, main in _SIDE["mains"].items():
-                main.wait_stream(_SIDE["streams"][dev])
+            for key, main in _SIDE["mains"].items():
+                main.wait_stream(_SIDE["streams"][key])
             _SIDE["mains"].clear()
             _SIDE["hold"].clear()
 
@@ -125,21 +129,23 @@ def _side_small(*keep):
     return _side(*keep) if SMALL_SIDE else contextlib.nullcontext()
 
 
-def _side(*keep, after=None):
-    """Stream context for a sink-bound gradient kernel: the side stream (after a fork from the
+def _side(*keep, after=None, lane=0):
+    """Stream context for a sink-bound gradient kernel: side stream ``lane`` (after a fork from the
     current stream, or from the event ``after``) while overlapping, else a no-op.  ``keep`` are
     the inputs the side kernels read; they stay referenced until the join so the caching
     allocator cannot hand their memory to a later backward kernel while the side stream still
-    reads it."""
+    reads it.  HICGAT_SIDE_PRIO sets the side streams' priority (-1 = high: measured no different
+    from the default 0 in graph replay)."""
     if not _SIDE["on"]:
         return contextlib.nullcontext()
     cur = torch.cuda.current_stream()
     dev = cur.device
+    key = (dev, lane)
     with _SIDE_LOCK:
-        side = _SIDE["streams"].get(dev)
+        side = _SIDE["streams"].get(key)
         if side is None:
-            side = _SIDE["streams"][dev] = torch.cuda.Stream(device=dev)
-        _SIDE["mains"].setdefault(dev, cur)
+            side = _SIDE["streams"][key] = torch.cuda.Stream(device=dev, priority=SIDE_PRIO)
+        _SIDE["mains"].setdefault(key, cur)
         _SIDE["hold"].extend(keep)
     if after is not None:
         side.wait_event(after)
@@ -230,17 +236,20 @@ class _GATConvFn(torch.autograd.Function):
                 side_flush(after=fork)
             rows = slice(r0, r1)
             if use_sinks:
-                _param_launch(lambda rows=rows: K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                                                             out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
-                                                             accumulate=True),
-                              h, dout, da_src, row_stats, small=True)
+                # on the backward's own stream (idle after the source pass)
+                K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
+                             out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
             else:
                 datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
                                                      out=None if c == 0 else (datt_l, datt_r, dbias),
                                                      accumulate=c > 0)
             if ctx.needs_input_grad[1]:
                 if gW is not None:
-                    _param_launch(lambda rows=rows: weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True), dh, x)
+                    if LINL_MAIN:   # right behind the source pass on this stream
+                        weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True)
+                    else:           # queued: on the side stream after the tail's dW work
+                        _param_launch(lambda rows=rows: weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True),
+                                      dh, x)
                 else:
                     dW = weight_grad(K, dh[rows], x[rows], out=dW, accumulate=dW is not None)
         if not use_sinks:
