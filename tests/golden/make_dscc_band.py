@@ -1,0 +1,67 @@
+"""Generate ``dscc_band_chr19_1mb.npz``: the oracle's dSCC on GM12878 chr19 1 mb after a fixed
+K = 3000 steps of the HiC-GNN_main.py loop (HiC-GNN_main.py:92-139: KR normalise, load_input,
+cont2dist(y, 0.5), Adam lr 1e-3, get_model, Spearman of the upper-triangle distances), run at 1, 2,
+4 and 8 CPU threads.  The thread count changes torch's summation order and the fixed-K training is
+chaotic, so the spread of these four runs is the oracle's own noise floor; the GPU
+test (tests/test_gpu_parity.py::test_dscc_chr19_1mb_k3000_matches_oracle) compares the device
+result with the 1-thread value and prints that floor beside the difference.
+
+Test infrastructure only (it runs the CPU oracle under oracle/).  Inputs: the committed fixtures
+graph_chr19_1mb.npz (the reference's contact matrix) and model_GATNetSelectiveResidualsUpdated.npz
+(512-d features; node2vec is absent).
+
+    python tests/golden/make_dscc_band.py      # ~5 min on 8 cores
+"""
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import gat as og  # noqa: E402
+from oracle import graph as ogr  # noqa: E402
+from oracle import kr as okr  # noqa: E402
+from oracle import loop as ol  # noqa: E402
+
+K = 3000
+THREADS = (1, 2, 4, 8)
+
+
+def main():
+    with np.load(os.path.join(HERE, "graph_chr19_1mb.npz"), allow_pickle=False) as z:
+        a = np.array(z["matrix"], dtype=np.float64)
+    with np.load(os.path.join(HERE, "model_GATNetSelectiveResidualsUpdated.npz"), allow_pickle=False) as z:
+        x = np.asarray(z["x"], dtype=np.float32)
+    np.fill_diagonal(a, 0)
+    normed, keep = okr.krnorm(a.copy())
+    x = x[np.asarray(keep)] if len(keep) != len(x) else x
+    d = ogr.load_input(normed.copy(), x)
+    truth = ogr.cont2dist(d["y"], 0.5)
+    radj = (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))
+    dscc, loss = [], []
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        for th in THREADS:
+            torch.set_num_threads(th)
+            torch.manual_seed(0)
+            ref = og.GATNetSelectiveResidualsUpdated()
+            t0 = time.time()
+            hist = ol.train(ref, d["x"], radj, truth, steps=K)
+            with torch.no_grad():
+                dscc.append(ol.dscc(ref.get_model(d["x"], radj), truth))
+            loss.append(hist[-1])
+            print(f"threads {th}: dSCC {dscc[-1]:.6f}, loss {loss[-1]:.6e} ({time.time() - t0:.0f} s)", flush=True)
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    np.savez(os.path.join(HERE, "dscc_band_chr19_1mb.npz"), steps=np.int64(K), threads=np.array(THREADS),
+             dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
+             cpu=np.array(platform.processor() or platform.machine()))
+
+
+if __name__ == "__main__":
+    main()
