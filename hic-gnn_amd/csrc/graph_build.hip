@@ -8,6 +8,8 @@
 //   so columns come out sorted with no sort at all.  The count pass and the fill pass walk the
 //   same order, which makes the output bit-exact with the reference pattern.
 // hicgat_cont2dist: utils.cont2dist (utils.py:75-80) in float64, torch's pow special cases kept.
+// hicgat_truth_support: a symmetric target as background value + sorted CSR of the entries that
+//   differ from it (+ its diagonal), for the fused loss's background/support form (pairdist.hip).
 #include "common.hpp"
 
 namespace hicgat {
@@ -75,6 +77,35 @@ __global__ __launch_bounds__(1024) void scan_kernel(int32_t *__restrict__ rowptr
     rowptr[i] = (int32_t)run;
   }
   if (t == 0) rowptr[0] = 0;
+}
+
+// ---- truth in background + support form ------------------------------------------------------
+// One wave per row i: 64 columns per step, ballot of (j != i && T[i][j] != bg), so the support
+// columns come out sorted; the count pass and the fill pass walk the same order.  The fill pass
+// also writes diag[i] = T[i][i].
+template <bool FILL>
+__global__ __launch_bounds__(256) void truth_support_kernel(const float *__restrict__ T, int N, int64_t ldt, float bg,
+                                                            int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
+                                                            float *__restrict__ val, float *__restrict__ diag) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= N) return;   // wave-uniform
+  const float *row = T + (size_t)i * ldt;
+  int at = FILL ? rowptr[i] : 0;
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    const int j = j0 + lane;
+    const float v = j < N ? row[j] : bg;
+    const bool bit = j < N && j != i && v != bg;
+    const unsigned long long mask = __ballot(bit);
+    if (FILL && bit) {
+      const int e = at + __popcll(mask & ((1ull << lane) - 1ull));
+      col[e] = j;
+      val[e] = v;
+    }
+    at += __popcll(mask);
+  }
+  if (FILL && lane == 0) diag[i] = row[i];
+  if (!FILL && lane == 0) rowptr[i + 1] = at;
 }
 
 // ---- cont2dist --------------------------------------------------------------------------------
@@ -172,6 +203,27 @@ extern "C" int hicgat_csr_from_dense(const double *A, int N, int64_t lda, int32_
   } else {
     hipLaunchKernelGGL(csr_strip_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, A, N, lda,
                        rowptr, col);
+    HICGAT_CHECK_LAUNCH();
+  }
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_truth_support(const float *T, int N, int64_t ldt, float background, int32_t *rowptr,
+                                    int32_t *col, float *val, float *diag, hicgat_stream_t stream) {
+  if (N < 0 || ldt < N || !rowptr) return HICGAT_EINVAL;
+  if (N == 0) return hipMemsetAsync(rowptr, 0, sizeof(int32_t), (hipStream_t)stream) == hipSuccess
+                         ? HICGAT_OK : HICGAT_ELAUNCH;
+  if (!T || (col && (!val || !diag))) return HICGAT_EINVAL;
+  const dim3 grid((N + 3) / 4);
+  if (col == nullptr) {
+    hipLaunchKernelGGL(truth_support_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, T, N, ldt, background,
+                       rowptr, nullptr, nullptr, nullptr);
+    HICGAT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rowptr, N);
+    HICGAT_CHECK_LAUNCH();
+  } else {
+    hipLaunchKernelGGL(truth_support_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, T, N, ldt, background,
+                       rowptr, col, val, diag);
     HICGAT_CHECK_LAUNCH();
   }
   return HICGAT_OK;

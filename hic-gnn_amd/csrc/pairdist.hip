@@ -73,9 +73,9 @@ struct TileAcc {
 // bounds, i < j on the diagonal, the diagonal moment); interior tiles take MASK = false and do
 // no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
 // w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
-template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1>
+template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1, bool BG = false>
 __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int64_t row0, int64_t col0,
-                                          int N, int I, int J,
+                                          int N, int I, int J, float bg,
                                           const float *tile, const float (*sc)[BT][3], int tx, int ty,
                                           const float *cx, const float *cy, const float *cz, const int *gj,
                                           float4 *__restrict__ prow, TileAcc &A) {
@@ -85,7 +85,10 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
     const int gi = I * BT + lr;
     const float rx = sc[0][lr][0], ry = sc[0][lr][1], rz = sc[0][lr][2];
     float tv[8];
-    if (VEC) {  // from the LDS image of the tile (conflict-free ds_read_b128: 16 lanes = one row)
+    if (BG) {   // background form: every pair at the background value, the support added later
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tv[q] = bg;
+    } else if (VEC) {  // from the LDS image of the tile (conflict-free ds_read_b128: 16 lanes = one row)
       const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
       const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
       tv[0] = a.x; tv[1] = a.y; tv[2] = a.z; tv[3] = a.w;
@@ -113,7 +116,7 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
         const float r = d - tt;
         if (MASK) {
           bool valid = gi < N && gj[q] < N;
-          if (valid && gi == gj[q]) A.dg = fmaf(tt, tt, A.dg);   // (D_ii - T_ii)^2 = T_ii^2
+          if (!BG && valid && gi == gj[q]) A.dg = fmaf(tt, tt, A.dg);   // (D_ii - T_ii)^2 = T_ii^2
           valid = valid && (I != J || gi < gj[q]);
           if (valid) {
             A.L = fmaf(r, r, A.L);
@@ -160,8 +163,8 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
 // v_pk_{add,mul,fma}_f32 (two pairs per instruction); v_rsq stays scalar.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-template <bool PEARSON, int K0, int K1>
-__device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc)[BT][3], int tx, int ty,
+template <bool PEARSON, int K0, int K1, bool BG = false>
+__device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const float (*sc)[BT][3], int tx, int ty,
                                              const float *cx, const float *cy, const float *cz,
                                              float4 *__restrict__ prow, TileAcc &A) {
   f2 cx2[4], cy2[4], cz2[4], ax2[4], ay2[4], az2[4];
@@ -181,9 +184,18 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
     const f2 rx = f2{sc[0][lr][0], sc[0][lr][0]}, ry = f2{sc[0][lr][1], sc[0][lr][1]},
              rz = f2{sc[0][lr][2], sc[0][lr][2]};
-    const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
-    const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
-    const f2 tv[4] = {f2{a.x, a.y}, f2{a.z, a.w}, f2{b.x, b.y}, f2{b.z, b.w}};
+    f2 tv[4];
+    if constexpr (BG) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) tv[h] = f2{bg, bg};
+    } else {
+      const float4 a = *reinterpret_cast<const float4 *>(&tile[lr * BT + tx * 4]);
+      const float4 b = *reinterpret_cast<const float4 *>(&tile[lr * BT + 64 + tx * 4]);
+      tv[0] = f2{a.x, a.y};
+      tv[1] = f2{a.z, a.w};
+      tv[2] = f2{b.x, b.y};
+      tv[3] = f2{b.z, b.w};
+    }
     f2 px = z2, py = z2, pz = z2;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
@@ -240,13 +252,19 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, const float (*sc
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
 // PEARSON: also the d / t moments of the Pearson term (combined loss only).
-template <int MODE, bool VEC, bool PEARSON>
-__global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restrict__ coords,
+// BG: the background form (T = bg at every pair; no T read, no diagonal term -- the support pass,
+// pairdist_support_kernel, adds the entries that differ and the diagonal).
+#ifndef HICGAT_PD_BG_OCC
+#define HICGAT_PD_BG_OCC 1   // workgroups per CU the background form's register budget is set for
+#endif
+template <int MODE, bool VEC, bool PEARSON, bool BG = false>
+__global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
                                                             int64_t ldt, int64_t row0, int64_t col0,
                                                             int nb, int64_t t0,
                                                             float4 *__restrict__ part,
-                                                            double *__restrict__ mom) {
+                                                            double *__restrict__ mom, float bg) {
+  static_assert(!BG || (MODE == MODE_SYM && !VEC), "the background form is the training loss without a T image");
   // one dynamic LDS array: [T tile 128x128 fp32 (VEC only)] -- 64 KiB, 16-B aligned
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ float sc[2][BT][3];
@@ -309,21 +327,21 @@ __global__ __launch_bounds__(256) void pairdist_tile_kernel(const float *__restr
   float4 *prow = part + (size_t)t * 2 * BT;
   const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
   if (VEC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // this wave's first 16 rows landed
-  constexpr bool PK = VEC && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
+  constexpr bool PK = (VEC || BG) && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4>(tile, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4, BG>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 0, 4>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 0, 4, BG>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8>(tile, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8, BG>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A);
+    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 4, 8>(T, ldt, row0, col0, N, I, J, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 4, 8, BG>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
   }
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
@@ -379,16 +397,18 @@ constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-th
 __device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
                                       double *__restrict__ part);
 
-// mom != NULL: the last kMomBlocks blocks sum runs of the tile moments into mpart instead
-// (moments_partial_block); blocks [0, row_blocks) reduce the coordinate partials
+// mom != NULL: the last kMomBlocks blocks sum runs of the moment records [m0, m1) (tiles, then the
+// support pass's blocks) into mpart instead (moments_partial_block); blocks [0, row_blocks) reduce
+// the coordinate partials, plus the support pass's per-row term corr (background form) last.
 __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part, int ncol,
                                                                int N, int nb, int mode, int64_t t0,
                                                                int64_t t1, float scale,
                                                                float *__restrict__ dcoords,
-                                                               const double *__restrict__ mom, int row_blocks,
-                                                               double *__restrict__ mpart) {
+                                                               const double *__restrict__ mom, int64_t m0, int64_t m1,
+                                                               int row_blocks, double *__restrict__ mpart,
+                                                               const float4 *__restrict__ corr) {
   if (mom && (int)blockIdx.x >= row_blocks) {
-    moments_partial_block(mom, t0, t1, (int)blockIdx.x - row_blocks, mpart);
+    moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
     return;
   }
   __shared__ float4 red[kRedGroups][64];
@@ -427,6 +447,10 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
 #pragma unroll
     for (int g = 1; g < kRedGroups; ++g) {
       const float4 o = red[g][lr64];
+      s0.x += o.x; s0.y += o.y; s0.z += o.z;
+    }
+    if (corr) {
+      const float4 o = corr[gi];
       s0.x += o.x; s0.y += o.y; s0.z += o.z;
     }
     dcoords[3 * (size_t)gi] = s0.x * scale;
@@ -502,6 +526,79 @@ __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__re
   }
   __syncthreads();
   if (threadIdx.x == 0) finalize_stats(N, loss_kind, stats, loss);
+}
+
+// Support pass of the background form: T = bg except at the sorted CSR support (symmetric, no
+// diagonal) and the diagonal.  One wave per row i, lanes over its support entries j:
+//   gradient  corr[i] = sum_j ((d - t) - (d - bg)) / d * (c_i - c_j) = sum_j (bg - t) / d * (c_i - c_j)
+//             (every j: the bulk tiles gave row i the bg term of each pair, as row or column partial);
+//   moments   over j > i only (each pair once, in fp64), the support's change of the bulk's terms:
+//             L += (d - t)^2 - (d - bg)^2, sdt += d (t - bg), st += t - bg, stt += t^2 - bg^2; and the
+//             diagonal's (0 - T_ii)^2 into the dg moment.
+// d is formed exactly as in the bulk's interior path.  Per-block moment records (fixed order).
+template <bool PEARSON>
+__global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__restrict__ coords, int N, float bg,
+                                                               const int32_t *__restrict__ rowptr,
+                                                               const int32_t *__restrict__ col,
+                                                               const float *__restrict__ val,
+                                                               const float *__restrict__ diag,
+                                                               float4 *__restrict__ corr, double *__restrict__ mom) {
+  __shared__ double mred[4][7];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 4 + wv;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  double L = 0.0, sdt = 0.0, st = 0.0, stt = 0.0, dg = 0.0;   // the support's moment changes in fp64
+  if (i < N) {   // wave-uniform
+    const float xi = coords[3 * (size_t)i], yi = coords[3 * (size_t)i + 1], zi = coords[3 * (size_t)i + 2];
+    const int e1 = rowptr[i + 1];
+    for (int e = rowptr[i] + lane; e < e1; e += 64) {
+      const int j = col[e];
+      const float t = val[e];
+      const float dx = xi - coords[3 * (size_t)j], dy = yi - coords[3 * (size_t)j + 1],
+                  dz = zi - coords[3 * (size_t)j + 2];
+      const float d2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, 0x1.0p-100f)));
+      const float inv = __builtin_amdgcn_rsqf(d2);
+      const float d = d2 * inv;
+      const float w = (bg - t) * inv;
+      gx = fmaf(w, dx, gx);
+      gy = fmaf(w, dy, gy);
+      gz = fmaf(w, dz, gz);
+      if (j > i) {
+        const double dd = d, td = t, bd = bg;
+        const double r = dd - td, rb = dd - bd;
+        L += r * r - rb * rb;
+        if (PEARSON) {
+          sdt += dd * (td - bd);
+          st += td - bd;
+          stt += td * td - bd * bd;
+        }
+      }
+    }
+    if (lane == 0) {
+      const float ti = diag[i];
+      dg = (double)ti * (double)ti;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    gx += __shfl_xor(gx, o);
+    gy += __shfl_xor(gy, o);
+    gz += __shfl_xor(gz, o);
+  }
+  if (i < N && lane == 0) corr[i] = make_float4(gx, gy, gz, 0.f);
+  double m[7] = {L, 0.0, 0.0, sdt, st, stt, dg};
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    if (c == 1 || c == 2 || (!PEARSON && c >= 3 && c <= 5)) continue;
+    for (int o = 32; o > 0; o >>= 1) m[c] += shfl_xor_d(m[c], o);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 7; ++c) mred[wv][c] = m[c];
+  }
+  __syncthreads();
+  if (threadIdx.x < 7)
+    mom[(size_t)blockIdx.x * 8 + threadIdx.x] =
+        ((mred[0][threadIdx.x] + mred[1][threadIdx.x]) + mred[2][threadIdx.x]) + mred[3][threadIdx.x];
 }
 
 // D[i, j] = ||c_i - c_j||: one thread per element.
@@ -586,14 +683,14 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
                    ldg >= (int64_t)nb * BT;
   if (vec)
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true, false>), dim3(tiles), dim3(256), kTileLds,
-                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom);
+                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, 0.f);
   else
     hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false, false>), dim3(tiles), dim3(256), 0,
-                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom);
+                       (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, 0.f);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
-                     dcoords, nullptr, 0, nullptr);
+                     dcoords, nullptr, (int64_t)0, (int64_t)0, 0, nullptr, nullptr);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -634,7 +731,7 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
     // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only
 #define HICGAT_PD_SYM(V, P)                                                                          \
   hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, P>), dim3(nt), dim3(256), V ? kTileLds : 0, \
-                     (hipStream_t)stream, coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, part, mom)
+                     (hipStream_t)stream, coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, part, mom, 0.f)
     if (vec && loss_kind == 1) HICGAT_PD_SYM(true, true);
     else if (vec) HICGAT_PD_SYM(true, false);
     else if (loss_kind == 1) HICGAT_PD_SYM(false, true);
@@ -648,7 +745,8 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   const int row_blocks = dcoords ? (N + 63) / 64 : 0;
   double *mpart = mom + (size_t)tiles * 8;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, (hipStream_t)stream, part,
-                     1, N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, row_blocks, mpart);
+                     1, N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end,
+                     row_blocks, mpart, nullptr);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, N, loss_kind, stats,
                      loss);
@@ -671,6 +769,59 @@ extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, flo
   if (N <= 0 || !stats || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
                      stats, loss);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+// ---- background form: T = bg except at a sorted symmetric CSR support + the diagonal -----------
+static int64_t pd_support_blocks(int N) { return (N + 3) / 4; }
+
+extern "C" size_t hicgat_pairdist_support_workspace_bytes(int N) {
+  if (N <= 0) return 256;
+  const int64_t tiles = hicgat_pairdist_num_tiles(N, HICGAT_PD_TRI);
+  return (size_t)tiles * 2 * BT * sizeof(float4) + (size_t)(tiles + pd_support_blocks(N)) * 8 * sizeof(double) +
+         kMomBlocks * 8 * sizeof(double) + (size_t)N * sizeof(float4) + 256;
+}
+
+extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background,
+                                                 const int32_t *rowptr, const int32_t *col, const float *val,
+                                                 const float *diag, int loss_kind, double *stats, float *loss,
+                                                 float *dcoords, void *workspace, size_t workspace_bytes,
+                                                 hicgat_stream_t stream) {
+  if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!coords || !rowptr || !col || !val || !diag || !stats || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_pairdist_support_workspace_bytes(N)) return HICGAT_EINVAL;
+  const int nb = pd_nb(N);
+  const int64_t tiles = (int64_t)nb * (nb + 1) / 2, sblocks = pd_support_blocks(N);
+  char *p = static_cast<char *>(workspace);
+  float4 *part = reinterpret_cast<float4 *>(p);
+  double *mom = reinterpret_cast<double *>(p + (size_t)tiles * 2 * BT * sizeof(float4));
+  double *mpart = mom + (size_t)(tiles + sblocks) * 8;
+  float4 *corr = reinterpret_cast<float4 *>(mpart + kMomBlocks * 8);
+  hipStream_t s = (hipStream_t)stream;
+  // bulk: every pair i < j at the background value (no T read); support: the entries that differ
+  if (loss_kind == 1)
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(tiles), dim3(256), 0, s, coords,
+                       nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, background);
+  else
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true>), dim3(tiles), dim3(256), 0, s, coords,
+                       nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, background);
+  HICGAT_CHECK_LAUNCH();
+  if (loss_kind == 1)
+    hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background, rowptr,
+                       col, val, diag, corr, mom + (size_t)tiles * 8);
+  else
+    hipLaunchKernelGGL(pairdist_support_kernel<false>, dim3(sblocks), dim3(256), 0, s, coords, N, background, rowptr,
+                       col, val, diag, corr, mom + (size_t)tiles * 8);
+  HICGAT_CHECK_LAUNCH();
+  const float scale = (float)(4.0 / ((double)N * (double)N));
+  const int row_blocks = dcoords ? (N + 63) / 64 : 0;
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
+                     (int)MODE_SYM, (int64_t)0, tiles, scale, dcoords, mom, (int64_t)0, tiles + sblocks, row_blocks,
+                     mpart, corr);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

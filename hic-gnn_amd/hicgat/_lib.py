@@ -50,6 +50,10 @@ SIGNATURES = {
     "hicgat_pairdist_finalize": (c_int, [c_int, c_int, c_p, c_p, c_p]),
     "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
     "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),
+    "hicgat_pairdist_mse_fused_support": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_p,
+                                                  c_sz, c_p]),
+    "hicgat_pairdist_support_workspace_bytes": (c_sz, [c_int]),
+    "hicgat_truth_support": (c_int, [c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),
     "hicgat_gemm_workspace_bytes": (c_sz, [c_int, c_int, c_int]),

@@ -10,6 +10,8 @@
 * ``Truth``              -- the fp32 target of the fused distance/MSE kernel: padded leading dim
   (multiple of 128), symmetric.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -214,6 +216,57 @@ def padded_ld(n):
     return ((n + TILE - 1) // TILE) * TILE
 
 
+# The fused loss takes the truth in background + support form when the entries that differ from
+# the background are at most this fraction of the matrix (HICGAT_TRUTH_SUPPORT=0: always dense).
+SUPPORT_BACKGROUND = 1.0 if os.environ.get("HICGAT_TRUTH_SUPPORT", "1") != "0" else None
+SUPPORT_MAX_FRACTION = 0.25
+
+
+class SupportForm:
+    """A symmetric truth as ``background`` off the diagonal except at a sorted CSR support
+    (``rowptr``, ``col``, ``val``: the entries that differ, no diagonal) plus ``diag``.
+    ``cont2dist``'s target (utils.py:75-80) is 1 wherever the contact count is 0 (inf -> max ->
+    /max), so its support is the contact set: the fused loss then streams no truth
+    (hicgat_pairdist_mse_fused_support).  Built on the device by hicgat_truth_support from the
+    stored (symmetrised) truth, so the values are the dense ones, bit for bit."""
+
+    def __init__(self, background, rowptr, col, val, diag, nnz):
+        # col / val hold at least one element (a non-null pointer for an empty support)
+        self.background, self.rowptr, self.col_buf, self.val_buf, self.diag = background, rowptr, col, val, diag
+        self.nnz = nnz
+
+    @property
+    def col(self):
+        return self.col_buf[:self.nnz]
+
+    @property
+    def val(self):
+        return self.val_buf[:self.nnz]
+
+    @classmethod
+    def build(cls, truth, background, max_fraction=SUPPORT_MAX_FRACTION):
+        """The form, or None when the support is denser than ``max_fraction`` of the matrix."""
+        lib = _lib.lib()
+        n, dev = truth.n, truth.buf.device
+        st = _lib.stream(dev)
+        rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        _lib.check(lib.hicgat_truth_support(_lib.ptr(truth.buf), n, truth.ld, float(background), _lib.ptr(rowptr),
+                                            None, None, None, st), "hicgat_truth_support")
+        # int32 counts: a wrap past 2^31 shows as a negative step
+        if bool((rowptr[1:] < rowptr[:-1]).any()):
+            return None
+        nnz = int(rowptr[-1])
+        if nnz > max_fraction * float(n) * float(n):
+            return None
+        col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+        val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+        diag = torch.empty(n, dtype=torch.float32, device=dev)
+        _lib.check(lib.hicgat_truth_support(_lib.ptr(truth.buf), n, truth.ld, float(background), _lib.ptr(rowptr),
+                                            _lib.ptr(col), _lib.ptr(val), _lib.ptr(diag), st),
+                   "hicgat_truth_support")
+        return cls(float(background), rowptr, col, val, diag, nnz)
+
+
 class Truth:
     """fp32 target for the fused distance/MSE kernel: [N, ld] with ld = ceil(N/128)*128.
 
@@ -232,7 +285,7 @@ class Truth:
     The combined loss's Pearson term then sees tbar on the upper triangle (a relative change of
     the order of the asymmetry, 1e-7 for R's rounding)."""
 
-    def __init__(self, t=None, *, _buf=None, _n=None):
+    def __init__(self, t=None, *, _buf=None, _n=None, background=SUPPORT_BACKGROUND):
         if _buf is None:
             t = t.detach()
             n = t.shape[0]
@@ -246,6 +299,9 @@ class Truth:
         if self.asymmetric_source:
             self._symmetrise()
         self.symmetric = True
+        self.support = None
+        if background is not None and buf.is_cuda and n > 1:
+            self.support = SupportForm.build(self, background)
 
     def _symmetrise(self):
         t = self.buf[:, :self.n].double()

@@ -188,6 +188,15 @@ class HipKernels:
                 int(kind), P(stats), P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
                 "hicgat_pairdist_mse_fused_band")
 
+    def fused_loss_support(self, coords, sf, n, kind, stats, loss, dcoords):
+        """The fused loss over a truth in background + support form (``graph.SupportForm``)."""
+        ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
+        with _timed("pairdist_mse_fused"):
+            _lib.check(self.lib.hicgat_pairdist_mse_fused_support(
+                P(coords), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(kind), P(stats),
+                P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
+                "hicgat_pairdist_mse_fused_support")
+
     def loss_finalize(self, n, kind, stats, loss):
         _lib.check(self.lib.hicgat_pairdist_finalize(n, int(kind), P(stats), P(loss), _lib.stream(stats.device)),
                    "hicgat_pairdist_finalize")

@@ -578,18 +578,21 @@ def pairwise_dist(coords):
 
 class _FusedLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, coords, tbuf, n, loss_kind, tile_begin, tile_end, stats):
+    def forward(ctx, coords, tbuf, n, loss_kind, tile_begin, tile_end, stats, support=None):
         c = coords.contiguous().float()
         dc = torch.empty_like(c)
         loss = torch.empty((), dtype=torch.float32, device=c.device)
-        kernels.default().fused_loss(c, tbuf, n, loss_kind, tile_begin, tile_end, stats, loss, dc)
+        if support is not None:
+            kernels.default().fused_loss_support(c, support, n, loss_kind, stats, loss, dc)
+        else:
+            kernels.default().fused_loss(c, tbuf, n, loss_kind, tile_begin, tile_end, stats, loss, dc)
         ctx.save_for_backward(dc)
         return loss
 
     @staticmethod
     def backward(ctx, gl):
         (dc,) = ctx.saved_tensors
-        return dc * gl, None, None, None, None, None, None
+        return dc * gl, None, None, None, None, None, None, None
 
 
 def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
@@ -598,14 +601,19 @@ def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
     gradient of the MSE only (the Pearson term is a detached host value in the reference).
 
     ``truth`` is a ``graph.Truth`` (stored symmetric; an asymmetric target is folded into the
-    equivalent symmetric form there).  ``stats`` (float64 [12], device) receives the moments, mse,
+    equivalent symmetric form there); with a background + support form (``truth.support``, e.g.
+    cont2dist's target) the whole-matrix loss reads no truth in its O(N^2) pass.  ``stats`` (float64 [12], device) receives the moments, mse,
     r, alpha and total (see include/hicgat.h)."""
     _lib.lib()
     _dev_check(coords)
     if stats is None:
         stats = torch.empty(12, dtype=torch.float64, device=coords.device)
     kind_i = {"mse": 0, "combined": 1}[kind]
-    loss = _FusedLossFn.apply(coords, truth.buf, truth.n, kind_i, int(tile_range[0]), int(tile_range[1]), stats)
+    t0, t1 = int(tile_range[0]), int(tile_range[1])
+    # the background + support form (no truth stream) when the truth has one and all tiles are wanted
+    whole = t0 == 0 and t1 in (-1, kernels.default().num_tiles(truth.n))
+    support = getattr(truth, "support", None) if whole else None
+    loss = _FusedLossFn.apply(coords, truth.buf, truth.n, kind_i, t0, t1, stats, support)
     return loss, stats
 
 

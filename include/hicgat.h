@@ -180,6 +180,24 @@ int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, h
 enum { HICGAT_PD_SQUARE = 0, HICGAT_PD_TRI = 1 };
 int64_t hicgat_pairdist_num_tiles(int N, int mode);
 size_t hicgat_pairdist_workspace_bytes(int N, int mode);
+/* The same fused loss (all tiles, stats / loss / dcoords as above) for a truth given in BACKGROUND
+ * form: T[i][j] = background for i != j except at the support -- a symmetric CSR (rowptr [N+1],
+ * sorted col, val = T there, no diagonal entries) -- and T[i][i] = diag[i].  cont2dist's target
+ * (utils.py:75-80) is of this form with background 1 (zero contacts: inf -> max -> 1) and the
+ * support = the contacts, so the O(N^2) pass reads no truth at all: it takes every pair at the
+ * background value and a pass over the support adds the difference (same sums up to fp32 /
+ * fp64 reassociation).  Build the form with hicgat_truth_support.
+ * workspace: hicgat_pairdist_support_workspace_bytes(N). */
+int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background, const int32_t *rowptr,
+                                      const int32_t *col, const float *val, const float *diag, int loss_kind,
+                                      double *stats, float *loss, float *dcoords, void *workspace,
+                                      size_t workspace_bytes, hicgat_stream_t stream);
+size_t hicgat_pairdist_support_workspace_bytes(int N);
+/* The background form of a symmetric N x N fp32 truth T (leading dim ldt): the sorted CSR of the
+ * off-diagonal entries != background, their values, and the diagonal.  Two calls, as
+ * hicgat_csr_from_dense: col == NULL fills rowptr (the counts, scanned); then col / val / diag. */
+int hicgat_truth_support(const float *T, int N, int64_t ldt, float background, int32_t *rowptr, int32_t *col,
+                         float *val, float *diag, hicgat_stream_t stream);
 
 /* ---- a6 / a10: fp32 MFMA GEMM for torch.nn.Linear forward/backward (models.py:637-659) -------
  *   C[M,N] (+)= op(A) op(B) (+ bias[N]);  op(A) = A [M,K] (lda = row stride) or, with a_kmajor,

@@ -198,3 +198,51 @@ def test_synth2000_dense_training_step_matches_oracle():
             continue
         diff = (params[k] - pr.detach()).abs()
         assert float(diff[sig].max()) < 1e-6, k
+
+
+def test_synth20000_support_form_loss_matches_dense():
+    """configs[2] (N = 20000, 1 % contacts): the fused loss over the truth's background + support
+    form (the default for cont2dist's target) against the dense-truth kernel and an fp64
+    evaluation on sampled rows: mse / moments 1e-6 relative, dcoords 1e-5 of their max."""
+    import hicgat
+    from hicgat import synth
+    n = 20000
+    i, j, c = synth.contact_pairs(n, density=0.01, seed=0)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    sf = tr.support
+    assert sf is not None
+    K = hicgat.kernels.default()
+    rng = np.random.default_rng(0)
+    coords = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32), device=DEV)
+    res = {}
+    for kind in (0, 1):
+        for form in ("dense", "support"):
+            stats = torch.empty(12, dtype=torch.float64, device=DEV)
+            loss = torch.empty((), dtype=torch.float32, device=DEV)
+            dc = torch.empty_like(coords)
+            if form == "dense":
+                K.fused_loss(coords, tr.buf, n, kind, 0, -1, stats, loss, dc)
+            else:
+                K.fused_loss_support(coords, sf, n, kind, stats, loss, dc)
+            res[kind, form] = (stats.cpu().numpy(), dc)
+    for kind in (0, 1):
+        sd, gd = res[kind, "dense"]
+        ss, gs = res[kind, "support"]
+        for k in (0, 6, 7) if kind == 0 else (0, 1, 2, 3, 4, 5, 7):
+            assert abs(ss[k] - sd[k]) <= 1e-6 * max(abs(sd[k]), 1e-30), (kind, k, ss[k], sd[k])
+        if kind == 1:
+            assert abs(ss[8] - sd[8]) < 1e-6
+        assert _rel(gs, gd) < 1e-5
+    # fp64 gradient of the MSE on 64 sampled rows: dL/dc_i = 4/N^2 sum_j (d_ij - t_ij)/d_ij (c_i - c_j)
+    cd = coords.double()
+    rows = torch.tensor(rng.choice(n, 64, replace=False), device=DEV)
+    diff = cd[rows, None, :] - cd[None, :, :]
+    d = diff.norm(dim=-1)
+    t = tr.dense()[rows].double()
+    w = torch.where(d > 0, (d - t) / d.clamp_min(1e-300), torch.zeros_like(d))
+    g_ref = 4.0 / n / n * (w[..., None] * diff).sum(1)
+    assert _rel(res[0, "support"][1][rows], g_ref) < 1e-5
+    print(f"support nnz {sf.nnz} ({sf.nnz / n / n:.2%}); mse {res[0, 'support'][0][7]:.9g} vs dense "
+          f"{res[0, 'dense'][0][7]:.9g}")
