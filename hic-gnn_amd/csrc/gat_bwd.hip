@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
 //   da_src[r] = sum_i alpha_ir s_ir (<dout_i, h_r> - delta_i)
 //             = <sum_i alpha_ir s_ir dout_i, h_r> - sum_i alpha_ir s_ir delta_i      (s = lrelu')
 // so the loop only accumulates two vectors (sum alpha dout_i, sum alpha s dout_i) and a scalar.
+// SPLIT (the tiled form, gat_tiles.hip): rowptr/col are the sparse remainder of the row's edges;
+// dh gets the raw sum (no logit terms) and da_src the remainder's share of da_src; the matrix-core
+// pass over the dense tiles adds the rest and finishes both.
+template <bool SPLIT = false>
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
@@ -174,6 +178,13 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   transpose_reduce<4>(v, lane);   // lane 0: v0, 16: v1, 32: v2, 48: v3 (summed over the wave)
   const float ds0 = readlane_f(v[0], 0) - readlane_f(v[0], 32);
   const float ds1 = readlane_f(v[0], 16) - readlane_f(v[0], 48);
+  float4 *o4 = reinterpret_cast<float4 *>(dh);
+  if (SPLIT) {
+    o4[(size_t)r * 128 + lane] = acc0;
+    o4[(size_t)r * 128 + 64 + lane] = acc1;
+    if (lane == 0) *reinterpret_cast<float2 *>(da_src + 2 * (size_t)r) = make_float2(ds0, ds1);
+    return;
+  }
   const float2 dd = *reinterpret_cast<const float2 *>(row_stats + ldr * r + 6);
   const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
   const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
@@ -182,7 +193,6 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   acc0 = f4_fma(dd.x, at0, acc0);
   acc1 = f4_fma(ds1, as1, acc1);
   acc1 = f4_fma(dd.y, at1, acc1);
-  float4 *o4 = reinterpret_cast<float4 *>(dh);
   o4[(size_t)r * 128 + lane] = acc0;
   o4[(size_t)r * 128 + 64 + lane] = acc1;
   if (lane == 0) {
@@ -299,6 +309,17 @@ __global__ __launch_bounds__(1024) void param_grad_stage2(const float *__restric
   }
 }
 
+// The gather half of hicgat_gat_agg_bwd_src_tiled (gat_tiles.hip): the sparse remainder's shares.
+int agg_bwd_src_split_launch(const int *rowptr_s, const int *col_s, int row_begin, int row_end, const float *h,
+                             const float *a_src, const float *a_dst, const float *row_stats, int64_t ldr,
+                             const float *dout, int64_t ldq4, float ns, float *dh, float *da_src, hipStream_t s) {
+  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel<true>, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, s, rowptr_s,
+                     col_s, row_begin, row_end, h, a_src, a_dst, row_stats, ldr, dout, ldq4, nullptr, nullptr, ns, dh,
+                     da_src);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -334,7 +355,7 @@ extern "C" int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *c
       !dh || !da_src)
     return HICGAT_EINVAL;
   const int rows = row_end - row_begin;
-  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
                      row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();

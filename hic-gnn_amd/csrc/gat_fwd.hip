@@ -64,12 +64,18 @@ __global__ __launch_bounds__(256) void att_logits_kernel(const float *__restrict
 #ifndef HICGAT_FWD_OCC
 #define HICGAT_FWD_OCC 1   // __launch_bounds__ min blocks per CU of the training form (A/B builds)
 #endif
-template <bool TRAIN, int ACT>
+//
+// SPLIT (the tiled form, gat_tiles.hip): the softmax statistics still come from the whole row
+// (rowptr/col), but only the edges of the sparse remainder (rowptr_s/col_s) are gathered, and the
+// raw sums (no bias, no activation) go to out/out2 with S3 of those edges; the matrix-core pass over
+// the row's dense 32x32 tiles adds the rest and applies the epilogue.
+template <bool TRAIN, int ACT, bool SPLIT = false>
 __global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ bias, float ns, float *__restrict__ out, float *__restrict__ out2,
-    float *__restrict__ row_stats) {
+    float *__restrict__ row_stats, const int *__restrict__ rowptr_s = nullptr,
+    const int *__restrict__ col_s = nullptr) {
   constexpr int U = HICGAT_FWD_U;  // neighbours in flight per lane
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
@@ -100,12 +106,14 @@ __global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c25
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc0 = z4, acc1 = z4, acs0 = z4, acs1 = z4;
   float t0 = 0.f, t1 = 0.f;
-  for (int base = beg; base < end; base += 64) {
+  const int gbeg = SPLIT ? rowptr_s[i] : beg, gend = SPLIT ? rowptr_s[i + 1] : end;
+  const int *__restrict__ gcol = SPLIT ? col_s : col;
+  for (int base = gbeg; base < gend; base += 64) {
     const int e = base + lane;
     int j = i;  // padded slots gather the (valid) own row with weight 0
     float p0 = 0.f, p1 = 0.f, q0 = 0.f, q1 = 0.f;
-    if (e < end) {
-      j = col[e];
+    if (e < gend) {
+      j = gcol[e];
       const float2 s = as2[j];
       const float e0 = s.x + ad.x, e1 = s.y + ad.y;
       p0 = expf(lrelu(e0, ns) - m0) / den0;
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c25
         t1 += q1;
       }
     }
-    const int cnt = min(64, end - base);
+    const int cnt = min(64, gend - base);
     for (int k = 0; k < cnt; k += U) {
       float4 v0[U], v1[U];
 #pragma unroll
@@ -139,10 +147,10 @@ __global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c25
   }
   const float4 *b4 = reinterpret_cast<const float4 *>(bias);
   float4 *o4 = reinterpret_cast<float4 *>(out);
-  float4 b0 = b4[lane], b1 = b4[64 + lane];
+  float4 b0 = SPLIT ? z4 : b4[lane], b1 = SPLIT ? z4 : b4[64 + lane];
   acc0.x += b0.x; acc0.y += b0.y; acc0.z += b0.z; acc0.w += b0.w;
   acc1.x += b1.x; acc1.y += b1.y; acc1.z += b1.z; acc1.w += b1.w;
-  if (ACT == 1) {
+  if (ACT == 1 && !SPLIT) {
     acc0 = f4_relu(acc0);
     acc1 = f4_relu(acc1);
   }
@@ -158,6 +166,21 @@ __global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c25
     if (lane == 0) rs4[2 * (size_t)i + 1] = make_float4(t0, t1, 0.f, 0.f);
   }
   if (lane == 0) rs4[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
+}
+
+// The gather half of hicgat_gat_agg_fwd_tiled (gat_tiles.hip): raw sums over the sparse remainder.
+int agg_fwd_split_launch(const int *rowptr, const int *col, const int *rowptr_s, const int *col_s, int row_begin,
+                         int row_end, const float *h, const float *a_src, const float *a_dst, float ns, float *out,
+                         float *out2, float *row_stats, hipStream_t s) {
+  const dim3 grid((row_end - row_begin + 3) / 4), block(256);
+  if (out2)
+    hipLaunchKernelGGL((agg_fwd_h2c256_kernel<true, 0, true>), grid, block, 0, s, rowptr, col, row_begin, row_end,
+                       h, a_src, a_dst, nullptr, ns, out, out2, row_stats, rowptr_s, col_s);
+  else
+    hipLaunchKernelGGL((agg_fwd_h2c256_kernel<false, 0, true>), grid, block, 0, s, rowptr, col, row_begin, row_end,
+                       h, a_src, a_dst, nullptr, ns, out, out2, row_stats, rowptr_s, col_s);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
 }
 
 }  // namespace hicgat

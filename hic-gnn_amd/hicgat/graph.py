@@ -175,6 +175,79 @@ class Adj:
         return obj
 
 
+    def tiles(self, min_edges=None):
+        """The dense-tile split of the device CSR (``build_tiles``), built once per CSR and cached;
+        None when tiling is off (HICGAT_TILE_MIN=0)."""
+        m = TILE_MIN if min_edges is None else int(min_edges)
+        if m <= 0:
+            return None
+        key = (self.rowptr32.data_ptr(), self.col32.data_ptr(), m)
+        cache = getattr(self, "_tiles", None)
+        if cache is None or cache[0] != key:
+            self._tiles = cache = (key, build_tiles(self.rowptr32, self.col32, 0, self.n, self.n, m))
+        return cache[1]
+
+
+# A 32x32 tile of the contact graph goes to the matrix cores when it holds at least this many
+# edges (DESIGN.md section 3: a dense tile costs the MFMA time of ~64 gathered edges); 0 = off.
+TILE_MIN = int(os.environ.get("HICGAT_TILE_MIN", "64"))
+TILE_ROWS = 32
+
+
+class Tiles:
+    """Dense-tile split of rows [r0, r1) of a CSR (include/hicgat.h, hicgat_gat_agg_fwd_tiled):
+    ``tptr`` [nrb+1] / ``tcol`` [ntiles] / ``tmask`` [ntiles*32] (int32 bit patterns of uint32
+    words) for the row blocks' dense 32x32 tiles, ``rowptr_s`` / ``col_s`` the CSR of every other
+    edge; ``n_dense`` edges are in tiles."""
+
+    def __init__(self, r0, r1, tptr, tcol, tmask, rowptr_s, col_s, n_dense, min_edges):
+        self.r0, self.r1 = r0, r1
+        self.tptr, self.tcol, self.tmask = tptr, tcol, tmask
+        self.rowptr_s, self.col_s = rowptr_s, col_s
+        self.ntiles = int(tcol.numel())
+        self.n_dense = int(n_dense)
+        self.min_edges = min_edges
+
+
+def build_tiles(rowptr, col, r0, r1, ncols, min_edges=None):
+    """Split the edges of rows [r0, r1) of (rowptr, col) into dense 32x32 tiles (row blocks of 32
+    from r0, column blocks of 32 from 0) holding >= ``min_edges`` edges, and the CSR of the rest
+    (same length as ``rowptr``; rows outside the range empty).  Torch ops on ``col``'s device."""
+    m = TILE_MIN if min_edges is None else int(min_edges)
+    dev = col.device
+    rp = rowptr.long()
+    nrb = (r1 - r0 + TILE_ROWS - 1) // TILE_ROWS
+    ncb = (ncols + TILE_ROWS - 1) // TILE_ROWS
+    beg, end = int(rp[r0]), int(rp[r1])
+    deg = rp[r0 + 1:r1 + 1] - rp[r0:r1]
+    rows = torch.repeat_interleave(torch.arange(r0, r1, device=dev), deg, output_size=end - beg)
+    c = col[beg:end].long()
+    key = ((rows - r0) // TILE_ROWS) * ncb + c // TILE_ROWS
+    cnt = torch.bincount(key, minlength=nrb * ncb)
+    dense = cnt >= max(m, 1)
+    in_tile = dense[key]
+    tkeys = torch.nonzero(dense).flatten()
+    tptr = torch.zeros(nrb + 1, dtype=torch.int64, device=dev)
+    tptr[1:] = torch.cumsum(torch.bincount(tkeys // ncb, minlength=nrb), 0)
+    tcol = (tkeys % ncb).to(torch.int32)
+    tid = torch.searchsorted(tkeys, key[in_tile])
+    word = tid * TILE_ROWS + (rows[in_tile] - r0) % TILE_ROWS
+    bits = torch.bitwise_left_shift(torch.ones_like(word), c[in_tile] % TILE_ROWS)
+    # every (row, col) is one edge: the sum of its distinct bits is their OR
+    mask = torch.zeros(tkeys.numel() * TILE_ROWS, dtype=torch.int64, device=dev).index_add_(0, word, bits)
+    mask = torch.where(mask >= 2 ** 31, mask - 2 ** 32, mask).to(torch.int32)
+    keep = ~in_tile
+    n = rp.numel() - 1
+    rowptr_s = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    rowptr_s[r0 + 1:r1 + 1] = torch.cumsum(torch.bincount(rows[keep] - r0, minlength=r1 - r0), 0)
+    rowptr_s[r1 + 1:] = rowptr_s[r1]
+    col_s = c[keep].to(torch.int32)
+    if col_s.numel() == 0:
+        col_s = torch.zeros(1, dtype=torch.int32, device=dev)   # a valid pointer for an empty remainder
+    return Tiles(r0, r1, tptr.to(torch.int32), tcol, mask, rowptr_s.to(torch.int32), col_s,
+                 int(in_tile.sum()), m)
+
+
 class Data:
     """torch_geometric.data.Data stand-in: x, edge_index (Adj), y."""
 

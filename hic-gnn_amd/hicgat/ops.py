@@ -50,6 +50,9 @@ SIDE_PRIO = int(os.environ.get("HICGAT_SIDE_PRIO", "0"))
 # lin_l's dW on the backward's own stream right after the source pass (1, default: 2.011 / 2.014 ms
 # per step) or queued onto the side stream behind the tail's dW work (0: 2.037 / 2.037 ms)
 LINL_MAIN = os.environ.get("HICGAT_LINL_MAIN", "1") != "0"
+# the GAT param_grad (datt_l, datt_r, dbias column sums) on a second side stream beside lin_l's dW
+# (1, default) or on the backward's stream in front of it (0)
+PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "1") != "0"
 
 
 def side_begin():
@@ -76,8 +79,11 @@ def side_flush(after=None):
         queue, _SIDE["queue"] = _SIDE["queue"], []
     if not queue:
         return
-    with _side(*[t for _, keep in queue for t in keep], after=after):
-        for fn, _ in queue:
+    # largest first: the big weight-gradient GEMMs then get CU slots while the gather pass beside
+    # them still leaves some, and the tiny ones (3 x 64 outputs) trail (stable: equal work keeps order)
+    queue.sort(key=lambda q: -q[2])
+    with _side(*[t for _, keep, _ in queue for t in keep], after=after):
+        for fn, _, _ in queue:
             fn()
 
 
@@ -110,15 +116,15 @@ def overlapped_param_grads(enabled=None):
         side_join()
 
 
-def _param_launch(fn, *keep, small=False):
+def _param_launch(fn, *keep, small=False, work=0):
     """Launch a sink-bound parameter-gradient kernel ``fn()``: now on the current stream when not
-    overlapping; queued for ``side_flush`` when deferring; else now on the side stream.  ``keep``
-    are the tensors ``fn`` reads (held until the join)."""
+    overlapping; queued for ``side_flush`` when deferring (``work``: its size, the issue order);
+    else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join)."""
     if not _SIDE["on"]:
         fn()
     elif DEFER_DEFAULT:
         with _SIDE_LOCK:
-            _SIDE["queue"].append((fn, keep))
+            _SIDE["queue"].append((fn, keep, work))
     else:
         with (_side_small(*keep) if small else _side(*keep)):
             fn()
@@ -180,7 +186,7 @@ class _GATConvFn(torch.autograd.Function):
     is a streaming pass (``agg_bwd_rows``) and only the source half gathers."""
 
     @staticmethod
-    def forward(ctx, x, W, att_l, att_r, bias, rowptr, col, negative_slope, act):
+    def forward(ctx, x, W, att_l, att_r, bias, rowptr, col, negative_slope, act, tiles=None):
         _lib.lib()
         _dev_check(x, W, att_l, att_r, bias, rowptr, col)
         K = kernels.default()
@@ -197,7 +203,11 @@ class _GATConvFn(torch.autograd.Function):
         row_stats = torch.empty((N, 4 * H), dtype=torch.float32, device=x.device)
         train = any(ctx.needs_input_grad[:5])
         out2 = torch.empty((N, D), dtype=torch.float32, device=x.device) if train else None
-        K.agg_fwd_act(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, act, out, out2, row_stats)
+        if tiles is not None:
+            K.agg_fwd_tiled(rowptr, col, tiles, h, a_src, a_dst, b, negative_slope, act, out, out2, row_stats)
+        else:
+            K.agg_fwd_act(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, act, out, out2, row_stats)
+        ctx.tiles = tiles
         if train:
             ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col, out, out2, b)
         ctx.has_bias = bias is not None
@@ -230,15 +240,20 @@ class _GATConvFn(torch.autograd.Function):
         # when overlapping -- so only the last chunk's share is left after the gathers (the
         # backward's tail).  The sink and autograd paths add the same partials in the same order.
         datt_l = datt_r = dbias = dW = None
-        for c, (r0, r1) in enumerate(_src_chunks(N)):
-            K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+        chunks = _src_chunks(N) if ctx.tiles is None else [(0, N)]
+        for c, (r0, r1) in enumerate(chunks):
+            if ctx.tiles is not None:
+                K.agg_bwd_src_tiled(ctx.tiles, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+            else:
+                K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
             if c == 0:
                 side_flush(after=fork)
             rows = slice(r0, r1)
             if use_sinks:
-                # on the backward's own stream (idle after the source pass)
-                K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                             out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
+                # on a second side stream (PG_SIDE, default), beside lin_l's dW GEMM on this one
+                with (_side(h, dout, da_src, row_stats, lane=1) if PG_SIDE else contextlib.nullcontext()):
+                    K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
+                                 out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
             else:
                 datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
                                                      out=None if c == 0 else (datt_l, datt_r, dbias),
@@ -260,7 +275,7 @@ class _GATConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
-        return (dx, dW, datt_l, datt_r, dbias, None, None, None, None)
+        return (dx, dW, datt_l, datt_r, dbias, None, None, None, None, None)
 
 
 # target workgroups of a split-K weight-gradient GEMM (512 measured best at N = 20000: 0.094 vs
@@ -291,7 +306,8 @@ def _weight_grad_to(K, p, dy, x):
     """dW = dy^T x into the parameter's sink (returns None) or a new tensor (returned)."""
     g = _sink(p)
     if g is not None:
-        _param_launch(lambda: weight_grad(K, dy, x, out=g, accumulate=True), dy, x)
+        _param_launch(lambda: weight_grad(K, dy, x, out=g, accumulate=True), dy, x,
+                      work=dy.shape[0] * dy.shape[1] * x.shape[1])
         return None
     return weight_grad(K, dy, x)
 
@@ -313,7 +329,7 @@ def _wb_grad_to(K, pW, pb, dy, x, need_w=True, need_b=True):
     n = x.shape[1]
     sp = _splits(m, n, rows)
     if gW is not None and (gb is not None or not need_b):
-        _param_launch(lambda: K.wgrad(dy, x, gW, gb, accumulate=True, splits=sp), dy, x)
+        _param_launch(lambda: K.wgrad(dy, x, gW, gb, accumulate=True, splits=sp), dy, x, work=rows * m * n)
         return None, None
     if gW is None and (not need_b or _sink(pb) is None):
         dW = torch.empty((m, n), dtype=torch.float32, device=dy.device)
@@ -527,7 +543,8 @@ class _DualLnReluResFn(torch.autograd.Function):
         if w_pair and b_pair and K.gemm_impl == 1:
             # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
             gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
-            _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x)
+            _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x,
+                          work=M * 2 * w * x.shape[1])
         else:
             if w_pair:
                 _param_launch(lambda: weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True), dY, x)
@@ -553,7 +570,8 @@ def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):
     """GATConv forward; ``act="relu"`` returns relu(GATConv(x)) with the relu fused."""
     if adj.rowptr32 is None or adj.rowptr32.device != x.device:
         adj.to(x.device)
-    return _GATConvFn.apply(x, W, att_l, att_r, bias, adj.rowptr32, adj.col32, negative_slope, _ACTS[act])
+    return _GATConvFn.apply(x, W, att_l, att_r, bias, adj.rowptr32, adj.col32, negative_slope, _ACTS[act],
+                            adj.tiles())
 
 
 class _PairDistFn(torch.autograd.Function):

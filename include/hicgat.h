@@ -129,6 +129,31 @@ int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, 
                               const float *dout, int64_t ld_dout, const float *att_src,
                               const float *att_dst, float neg_slope, float *dh, float *da_src,
                               hicgat_stream_t stream);
+/* ---- a4+a5 and the source pass with the dense tiles on the matrix cores (gat_tiles.hip) -------
+ * The same results as hicgat_gat_agg_fwd_act / hicgat_gat_agg_bwd_src_ld (fp32; the tiles' sums are
+ * added in another order), with the edge set split in two:
+ *   tiles: rows [row_begin, row_end) in blocks of 32 (block b = rows row_begin + 32b ..);
+ *     tptr [nrb + 1] (nrb = ceil((row_end - row_begin) / 32)) indexes tcol [ntiles] (a 32-column
+ *     block: columns 32*tcol[t] ..) and tmask [ntiles * 32] (bit c of word 32t + i: the edge
+ *     (row_begin + 32b + i, 32*tcol[t] + c) exists); tiles of a block in any order, each edge in at
+ *     most one tile;
+ *   rowptr_s / col_s: the CSR (N + 1 row pointers, rows of the range) of every OTHER edge.
+ * rowptr / col (the whole rows) give the softmax statistics.  The tiles' products run as dense
+ * 32 x 32 x 32 x 512 blocks on v_mfma_f32_32x32x2_f32 (weights 0 off the edge set).  Built from the
+ * CSR by hicgat.graph.Adj.tiles (a 32x32 tile is dense when it holds >= HICGAT_TILE_MIN edges). */
+int hicgat_gat_agg_fwd_tiled(const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_s,
+                             const int32_t *col_s, const int32_t *tptr, const int32_t *tcol,
+                             const uint32_t *tmask, int ntiles, int N, int H, int C, int row_begin,
+                             int row_end, const float *h, const float *a_src, const float *a_dst,
+                             const float *bias, float neg_slope, int act, float *out, float *out2,
+                             float *row_stats, hicgat_stream_t stream);
+int hicgat_gat_agg_bwd_src_tiled(const int32_t *rowptr_s, const int32_t *col_s, const int32_t *tptr,
+                                 const int32_t *tcol, const uint32_t *tmask, int ntiles, int N, int H,
+                                 int C, int row_begin, int row_end, const float *h, const float *a_src,
+                                 const float *a_dst, const float *row_stats, int64_t ld_stats,
+                                 const float *dout, int64_t ld_dout, const float *att_src,
+                                 const float *att_dst, float neg_slope, float *dh, float *da_src,
+                                 hicgat_stream_t stream);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;

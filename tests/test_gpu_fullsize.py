@@ -87,7 +87,10 @@ def _fp64_gat_train(rowptr, col, h, att_l, att_r, bias, g, mask, ns=0.2, chunk=1
                 datt_l=datt_l, datt_r=datt_r, dbias=dout.sum(0), a_s=a_s, a_d=a_d)
 
 
-def test_synth20000_gat_backward_matches_fp64():
+@pytest.mark.parametrize("tiled", [False, True], ids=["gather", "tiled"])
+def test_synth20000_gat_backward_matches_fp64(tiled):
+    """tiled: the dense 32x32 tiles on the matrix cores (hicgat_gat_agg_fwd_tiled /
+    hicgat_gat_agg_bwd_src_tiled, default HICGAT_TILE_MIN), the rest gathered."""
     import hicgat
     from hicgat import synth
     K = hicgat.kernels.default()
@@ -107,12 +110,20 @@ def test_synth20000_gat_backward_matches_fp64():
     out = torch.empty(n, 512, device=DEV)
     out2 = torch.empty(n, 512, device=DEV)
     rs = torch.empty(n, 8, device=DEV)
-    K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, bias, 0.2, 1, out, out2, rs)
+    tiles = hicgat.graph.build_tiles(adj.rowptr32, adj.col32, 0, n, n, 64) if tiled else None
+    if tiled:
+        assert tiles.n_dense > 0.4 * adj.device_nnz
+        K.agg_fwd_tiled(adj.rowptr32, adj.col32, tiles, h, a_s, a_d, bias, 0.2, 1, out, out2, rs)
+    else:
+        K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, bias, 0.2, 1, out, out2, rs)
     dout = torch.empty(n, 512, device=DEV)
     K.agg_bwd_rows(0, n, 1, g, out, bias, out2, dout, rs)
     dh = torch.empty(n, 512, device=DEV)
     da_src = torch.empty(n, 2, device=DEV)
-    K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, att_l, att_r, 0.2, dh, da_src)
+    if tiled:
+        K.agg_bwd_src_tiled(tiles, h, a_s, a_d, rs, dout, att_l, att_r, 0.2, dh, da_src)
+    else:
+        K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, att_l, att_r, 0.2, dh, da_src)
     datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, rs, 2)
     torch.cuda.synchronize()
     ref = _fp64_gat_train(adj.rowptr32, adj.col32, h, att_l, att_r, bias, g, out > 0)

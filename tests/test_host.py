@@ -123,3 +123,50 @@ def test_adjacent_requires_one_storage():
     assert y.data_ptr() == x.data_ptr() + 32 and x.untyped_storage().data_ptr() != y.untyped_storage().data_ptr()
     assert not _adjacent(x, y)
     assert torch.equal(_joined(x, y), torch.from_numpy(arr).view(4, 4))
+
+
+@pytest.mark.parametrize("r0,r1,tmin", [(0, 150, 1), (0, 150, 20), (0, 150, 2000), (37, 121, 8)])
+def test_build_tiles_partitions_the_edges(r0, r1, tmin):
+    """hicgat.graph.build_tiles: every edge of rows [r0, r1) is in exactly one of a dense tile (bit
+    set in its row's mask word) or the remainder CSR (order kept); every tile holds >= tmin edges
+    and every tile that does is listed; rows outside the range are empty in the remainder."""
+    from hicgat.graph import build_tiles
+    rng = np.random.default_rng(5)
+    n = 150
+    d = np.abs(np.arange(n)[:, None] - np.arange(n)[None, :])
+    A = (rng.random((n, n)) < np.minimum(1.0, 5.0 / np.maximum(d, 1))) | (d == 0)
+    A = np.triu(A) | np.triu(A).T
+    rowptr = np.zeros(n + 1, dtype=np.int32)
+    rowptr[1:] = np.cumsum(A.sum(1))
+    col = np.nonzero(A)[1].astype(np.int32)
+    t = build_tiles(torch.tensor(rowptr), torch.tensor(col), r0, r1, n, tmin)
+    tptr = t.tptr.numpy()
+    tcol = t.tcol.numpy()
+    mask = t.tmask.numpy().view(np.uint32)
+    got = np.zeros((n, n), dtype=int)
+    for b in range(len(tptr) - 1):
+        for k in range(tptr[b], tptr[b + 1]):
+            cnt = 0
+            for i in range(32):
+                for c in range(32):
+                    if (int(mask[32 * k + i]) >> c) & 1:
+                        got[r0 + 32 * b + i, 32 * tcol[k] + c] += 1
+                        cnt += 1
+            assert cnt >= tmin
+    rps, cs = t.rowptr_s.numpy(), t.col_s.numpy()
+    for r in range(n):
+        seg = cs[rps[r]:rps[r + 1]]
+        if not (r0 <= r < r1):
+            assert len(seg) == 0
+        assert np.all(np.diff(seg) > 0)
+        got[r, seg] += 1
+    want = np.zeros((n, n), dtype=int)
+    want[r0:r1] = A[r0:r1]
+    assert np.array_equal(got, want)
+    assert t.n_dense == int(sum(bin(int(w)).count("1") for w in mask))
+    # completeness: no tile left out that holds >= tmin edges
+    for b in range((r1 - r0 + 31) // 32):
+        rows = slice(r0 + 32 * b, min(r1, r0 + 32 * b + 32))
+        for cb in range((n + 31) // 32):
+            listed = cb in set(tcol[tptr[b]:tptr[b + 1]])
+            assert listed == (A[rows, 32 * cb:32 * cb + 32].sum() >= max(tmin, 1))
