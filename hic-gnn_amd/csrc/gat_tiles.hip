@@ -66,8 +66,9 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
     const int *__restrict__ tptr, const int *__restrict__ tcol, const uint32_t *__restrict__ tmask, int row_begin,
     int row_end, int ncols, const float *__restrict__ h, const float *__restrict__ a_src,
     const float *__restrict__ a_dst, const float *__restrict__ bias, float ns, float *__restrict__ out,
-    float *__restrict__ out2, float *__restrict__ row_stats) {
+    float *__restrict__ out2, float *__restrict__ row_stats, int splits, float *__restrict__ ws) {
   const int lane = lane_id(), w = wave_in_block();
+  const int sp = blockIdx.y;   // tile split: this workgroup takes tiles tb + sp, tb + sp + splits, ...
   const int li = lane & 31, lk = lane >> 5;
   const int rb = xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = row_begin + rb * 32;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
   for (int r = 0; r < 16; ++r) {
     const int row = r0 + acc_row(r, lk);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f), u = v;
-    if (row < row_end) {
+    if (splits == 1 && row < row_end) {   // split form: the epilogue kernel adds the gather's sums
       v = o4[(size_t)row * 128 + q0 + li];
       if (TRAIN) u = p4[(size_t)row * 128 + q0 + li];
     }
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
 
   float s3 = 0.f;
   const int tb = tptr[rb], te = tptr[rb + 1];
-  for (int tt = tb; tt < te; ++tt) {
+  for (int tt = tb + sp; tt < te; tt += splits) {
     const int cbase = 32 * tcol[tt];
     const uint32_t mk = tmask[(size_t)tt * 32 + li];
     const int cj = cbase + li;
@@ -138,6 +139,25 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
     }
   }
 
+  if (splits > 1) {   // raw partial sums of this split -> workspace (band_fwd_epilogue adds them)
+    const int64_t R = row_end - row_begin;
+    float4 *wa = reinterpret_cast<float4 *>(ws) + ((int64_t)sp * R - row_begin) * 128;
+    float4 *wq = reinterpret_cast<float4 *>(ws) + ((int64_t)(splits + sp) * R - row_begin) * 128;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = r0 + acc_row(r, lk);
+      if (row < row_end) {
+        wa[(size_t)row * 128 + q0 + li] = make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
+        if (TRAIN) wq[(size_t)row * 128 + q0 + li] = make_float4(acs[0][r], acs[1][r], acs[2][r], acs[3][r]);
+      }
+    }
+    if (TRAIN) {
+      s3 += __shfl_xor(s3, 32);
+      float *w3 = ws + (size_t)2 * splits * R * 512 + ((int64_t)sp * R - row_begin) * 2;
+      if ((w & 1) == 0 && lk == 0 && rvalid) w3[2 * (size_t)ri + hd] = s3;
+    }
+    return;
+  }
   const float4 b = reinterpret_cast<const float4 *>(bias)[q0 + li];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -168,9 +188,10 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
     int row_end, int ncols, const float *__restrict__ h, const float *__restrict__ a_src,
     const float *__restrict__ a_dst, const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout,
     int64_t ldq, const float *__restrict__ att_s, const float *__restrict__ att_d, float ns, float *__restrict__ dh,
-    float *__restrict__ da_src) {
+    float *__restrict__ da_src, int splits, float *__restrict__ ws) {
   __shared__ float red[4][32];
   const int lane = lane_id(), w = wave_in_block();
+  const int sp = blockIdx.y;
   const int li = lane & 31, lk = lane >> 5;
   const int rb = xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = row_begin + rb * 32;
@@ -187,7 +208,7 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
   for (int r = 0; r < 16; ++r) {
     const int row = r0 + acc_row(r, lk);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < row_end) v = o4[(size_t)row * 128 + q0 + li];
+    if (splits == 1 && row < row_end) v = o4[(size_t)row * 128 + q0 + li];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       acc[t][r] = f4_c(v, t);
@@ -197,7 +218,7 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
 
   float sb = 0.f;
   const int tb = tptr[rb], te = tptr[rb + 1];
-  for (int tt = tb; tt < te; ++tt) {
+  for (int tt = tb + sp; tt < te; tt += splits) {
     const int cbase = 32 * tcol[tt];
     const uint32_t mk = tmask[(size_t)tt * 32 + li];
     // constants of destination row (column) cbase + li
@@ -253,6 +274,18 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
   // sb of row li: the two half waves saw the two halves of its k-pairs
   sb += __shfl_xor(sb, 32);
   __syncthreads();
+  if (splits > 1) {   // raw partials of this split -> workspace (band_bwd_epilogue finishes dh, da_src)
+    const int64_t R = row_end - row_begin;
+    float4 *wa = reinterpret_cast<float4 *>(ws) + ((int64_t)sp * R - row_begin) * 128;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = r0 + acc_row(r, lk);
+      if (row < row_end) wa[(size_t)row * 128 + q0 + li] = make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
+    }
+    float *wc = ws + (size_t)splits * R * 512 + ((int64_t)sp * R - row_begin) * 2;
+    if ((w & 1) == 0 && lk == 0 && rvalid) wc[2 * (size_t)ri + hd] = (red[2 * hd][li] + red[2 * hd + 1][li]) - sb;
+    return;
+  }
   // da_src of row li of this head: remainder share + both waves' dot shares - sb
   float ds_row = 0.f;
   if (rvalid) ds_row = (da_src[2 * (size_t)ri + hd] + (red[2 * hd][li] + red[2 * hd + 1][li])) - sb;
@@ -278,6 +311,94 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
   }
 }
 
+// ---- split form (splits > 1: a row block's tiles spread over `splits` workgroups, so a graph with
+// few row blocks -- a dense 2000-node contact map has 63 -- still fills the chip): the tile kernels
+// leave raw partials in the workspace and these one-wave-per-row passes add them to the gather's
+// sums in split order and apply the epilogue (bitwise reproducible).
+template <bool TRAIN, int ACT>
+__global__ __launch_bounds__(256) void band_fwd_epilogue(int row_begin, int row_end, int splits,
+                                                         const float *__restrict__ ws, const float *__restrict__ bias,
+                                                         float *__restrict__ out, float *__restrict__ out2,
+                                                         float *__restrict__ row_stats) {
+  const int lane = lane_id();
+  const int i = row_begin + blockIdx.x * 4 + wave_in_block();
+  if (i >= row_end) return;
+  const int64_t R = row_end - row_begin, lr = i - row_begin;
+  const float4 *w4 = reinterpret_cast<const float4 *>(ws);
+  float4 *o4 = reinterpret_cast<float4 *>(out) + (size_t)i * 128;
+  float4 a0 = o4[lane], a1 = o4[64 + lane];
+  for (int s = 0; s < splits; ++s) {
+    const float4 *p = w4 + ((int64_t)s * R + lr) * 128;
+    const float4 u0 = p[lane], u1 = p[64 + lane];
+    a0.x += u0.x; a0.y += u0.y; a0.z += u0.z; a0.w += u0.w;
+    a1.x += u1.x; a1.y += u1.y; a1.z += u1.z; a1.w += u1.w;
+  }
+  const float4 b0 = reinterpret_cast<const float4 *>(bias)[lane], b1 = reinterpret_cast<const float4 *>(bias)[64 + lane];
+  a0 = make_float4(a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w);
+  a1 = make_float4(a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w);
+  if (ACT == 1) {
+    a0 = f4_relu(a0);
+    a1 = f4_relu(a1);
+  }
+  o4[lane] = a0;
+  o4[64 + lane] = a1;
+  if (TRAIN) {
+    float4 *q4 = reinterpret_cast<float4 *>(out2) + (size_t)i * 128;
+    float4 c0 = q4[lane], c1 = q4[64 + lane];
+    for (int s = 0; s < splits; ++s) {
+      const float4 *p = w4 + ((int64_t)(splits + s) * R + lr) * 128;
+      const float4 u0 = p[lane], u1 = p[64 + lane];
+      c0.x += u0.x; c0.y += u0.y; c0.z += u0.z; c0.w += u0.w;
+      c1.x += u1.x; c1.y += u1.y; c1.z += u1.z; c1.w += u1.w;
+    }
+    q4[lane] = c0;
+    q4[64 + lane] = c1;
+    if (lane < 2) {
+      const float *w3 = ws + (size_t)2 * splits * R * 512;
+      float t = row_stats[8 * (size_t)i + 4 + lane];
+      for (int s = 0; s < splits; ++s) t += w3[((int64_t)s * R + lr) * 2 + lane];
+      row_stats[8 * (size_t)i + 4 + lane] = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void band_bwd_epilogue(int row_begin, int row_end, int splits,
+                                                         const float *__restrict__ ws,
+                                                         const float *__restrict__ row_stats, int64_t ldr,
+                                                         const float *__restrict__ att_s,
+                                                         const float *__restrict__ att_d, float *__restrict__ dh,
+                                                         float *__restrict__ da_src) {
+  const int lane = lane_id();
+  const int r = row_begin + blockIdx.x * 4 + wave_in_block();
+  if (r >= row_end) return;
+  const int64_t R = row_end - row_begin, lr = r - row_begin;
+  const float *wc = ws + (size_t)splits * R * 512;
+  float ds0 = da_src[2 * (size_t)r], ds1 = da_src[2 * (size_t)r + 1];
+  for (int s = 0; s < splits; ++s) {
+    ds0 += wc[((int64_t)s * R + lr) * 2];
+    ds1 += wc[((int64_t)s * R + lr) * 2 + 1];
+  }
+  const float4 *w4 = reinterpret_cast<const float4 *>(ws);
+  float4 *o4 = reinterpret_cast<float4 *>(dh) + (size_t)r * 128;
+  float4 a0 = o4[lane], a1 = o4[64 + lane];
+  for (int s = 0; s < splits; ++s) {
+    const float4 *p = w4 + ((int64_t)s * R + lr) * 128;
+    const float4 u0 = p[lane], u1 = p[64 + lane];
+    a0.x += u0.x; a0.y += u0.y; a0.z += u0.z; a0.w += u0.w;
+    a1.x += u1.x; a1.y += u1.y; a1.z += u1.z; a1.w += u1.w;
+  }
+  const float2 dd = *reinterpret_cast<const float2 *>(row_stats + ldr * r + 6);
+  const float4 *s4 = reinterpret_cast<const float4 *>(att_s);
+  const float4 *t4 = reinterpret_cast<const float4 *>(att_d);
+  a0 = f4_fma(ds0, s4[lane], a0);
+  a0 = f4_fma(dd.x, t4[lane], a0);
+  a1 = f4_fma(ds1, s4[64 + lane], a1);
+  a1 = f4_fma(dd.y, t4[64 + lane], a1);
+  o4[lane] = a0;
+  o4[64 + lane] = a1;
+  if (lane == 0) *reinterpret_cast<float2 *>(da_src + 2 * (size_t)r) = make_float2(ds0, ds1);
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -286,27 +407,46 @@ static bool tiles_args_ok(const int32_t *tptr, const int32_t *tcol, const uint32
   return tptr && (ntiles == 0 || (tcol && tmask));
 }
 
+extern "C" size_t hicgat_gat_tiled_workspace_bytes(int rows, int splits) {
+  if (rows <= 0 || splits <= 1) return 0;
+  return (size_t)splits * rows * (2 * 512 + 2) * sizeof(float);
+}
+
+static int tiled_ws_ok(int rows, int splits, const void *workspace, size_t workspace_bytes) {
+  if (splits < 1 || splits > 64) return 0;
+  const size_t need = hicgat_gat_tiled_workspace_bytes(rows, splits);
+  return need == 0 || (workspace && workspace_bytes >= need && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0);
+}
+
 extern "C" int hicgat_gat_agg_fwd_tiled(const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_s,
                                         const int32_t *col_s, const int32_t *tptr, const int32_t *tcol,
                                         const uint32_t *tmask, int ntiles, int N, int H, int C, int row_begin,
                                         int row_end, const float *h, const float *a_src, const float *a_dst,
                                         const float *bias, float neg_slope, int act, float *out, float *out2,
-                                        float *row_stats, hicgat_stream_t stream) {
+                                        float *row_stats, int splits, void *workspace, size_t workspace_bytes,
+                                        hicgat_stream_t stream) {
   if (N < 0 || ntiles < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (act != 0 && act != 1) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (row_end == row_begin) return HICGAT_OK;
+  const int rows = row_end - row_begin;
   if (!rowptr || !col || !rowptr_s || !col_s || !tiles_args_ok(tptr, tcol, tmask, ntiles) || !h || !a_src ||
-      !a_dst || !bias || !out || !row_stats)
+      !a_dst || !bias || !out || !row_stats || !tiled_ws_ok(rows, splits, workspace, workspace_bytes))
     return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   int rc = agg_fwd_split_launch(rowptr, col, rowptr_s, col_s, row_begin, row_end, h, a_src, a_dst, neg_slope, out,
                                 out2, row_stats, s);
   if (rc != HICGAT_OK) return rc;
-  const dim3 grid((row_end - row_begin + 31) / 32), block(256);
+  const dim3 grid((rows + 31) / 32, splits), block(256), egrid((rows + 3) / 4);
+  float *ws = static_cast<float *>(workspace);
 #define HICGAT_BAND_FWD(TR, AC)                                                                                   \
-  hipLaunchKernelGGL((band_fwd_kernel<TR, AC>), grid, block, 0, s, tptr, tcol, tmask, row_begin, row_end, N, h, \
-                     a_src, a_dst, bias, neg_slope, out, out2, row_stats)
+  do {                                                                                                           \
+    hipLaunchKernelGGL((band_fwd_kernel<TR, AC>), grid, block, 0, s, tptr, tcol, tmask, row_begin, row_end, N, h, \
+                       a_src, a_dst, bias, neg_slope, out, out2, row_stats, splits, ws);                          \
+    if (splits > 1)                                                                                               \
+      hipLaunchKernelGGL((band_fwd_epilogue<TR, AC>), egrid, block, 0, s, row_begin, row_end, splits, ws, bias,   \
+                         out, out2, row_stats);                                                                   \
+  } while (0)
   if (out2) {
     if (act) HICGAT_BAND_FWD(true, 1);
     else HICGAT_BAND_FWD(true, 0);
@@ -325,21 +465,27 @@ extern "C" int hicgat_gat_agg_bwd_src_tiled(const int32_t *rowptr_s, const int32
                                             const float *a_dst, const float *row_stats, int64_t ld_stats,
                                             const float *dout, int64_t ld_dout, const float *att_src,
                                             const float *att_dst, float neg_slope, float *dh, float *da_src,
+                                            int splits, void *workspace, size_t workspace_bytes,
                                             hicgat_stream_t stream) {
   if (N < 0 || ntiles < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (ld_stats < 4 * H || ld_stats % 4 || ld_dout < H * C || ld_dout % 4) return HICGAT_EINVAL;
   if (row_end == row_begin) return HICGAT_OK;
+  const int rows = row_end - row_begin;
   if (!rowptr_s || !col_s || !tiles_args_ok(tptr, tcol, tmask, ntiles) || !h || !a_src || !a_dst || !row_stats ||
-      !dout || !att_src || !att_dst || !dh || !da_src)
+      !dout || !att_src || !att_dst || !dh || !da_src || !tiled_ws_ok(rows, splits, workspace, workspace_bytes))
     return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   int rc = agg_bwd_src_split_launch(rowptr_s, col_s, row_begin, row_end, h, a_src, a_dst, row_stats, ld_stats, dout,
                                     ld_dout / 4, neg_slope, dh, da_src, s);
   if (rc != HICGAT_OK) return rc;
-  hipLaunchKernelGGL(band_bwd_kernel, dim3((row_end - row_begin + 31) / 32), dim3(256), 0, s, tptr, tcol, tmask,
-                     row_begin, row_end, N, h, a_src, a_dst, row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst,
-                     neg_slope, dh, da_src);
+  float *ws = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(band_bwd_kernel, dim3((rows + 31) / 32, splits), dim3(256), 0, s, tptr, tcol, tmask, row_begin,
+                     row_end, N, h, a_src, a_dst, row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope,
+                     dh, da_src, splits, ws);
+  if (splits > 1)
+    hipLaunchKernelGGL(band_bwd_epilogue, dim3((rows + 3) / 4), dim3(256), 0, s, row_begin, row_end, splits, ws,
+                       row_stats, ld_stats, att_src, att_dst, dh, da_src);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

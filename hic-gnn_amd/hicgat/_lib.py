@@ -39,9 +39,12 @@ SIGNATURES = {
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_agg_fwd_tiled": (c_int, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
-                                         c_int, c_p, c_p, c_p, c_p, c_f, c_int, c_p, c_p, c_p, c_p]),
+                                         c_int, c_p, c_p, c_p, c_p, c_f, c_int, c_p, c_p, c_p, c_int, c_p, c_sz,
+                                         c_p]),
     "hicgat_gat_agg_bwd_src_tiled": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                                             c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p]),
+                                             c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_int,
+                                             c_p, c_sz, c_p]),
+    "hicgat_gat_tiled_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_gat_param_grad": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p,
                                       c_sz, c_p]),
     "hicgat_gat_param_grad_workspace_bytes": (c_sz, [c_int, c_int]),

@@ -192,6 +192,7 @@ class Adj:
 # edges (a dense tile costs the MFMA time of ~64 gathered edges); 0 = off.
 TILE_MIN = int(os.environ.get("HICGAT_TILE_MIN", "64"))
 TILE_ROWS = 32
+TILE_SPLITS = int(os.environ.get("HICGAT_TILE_SPLITS", "0"))   # 0 = from the row-block count
 
 
 class Tiles:
@@ -200,13 +201,19 @@ class Tiles:
     words) for the row blocks' dense 32x32 tiles, ``rowptr_s`` / ``col_s`` the CSR of every other
     edge; ``n_dense`` edges are in tiles."""
 
-    def __init__(self, r0, r1, tptr, tcol, tmask, rowptr_s, col_s, n_dense, min_edges):
+    def __init__(self, r0, r1, tptr, tcol, tmask, rowptr_s, col_s, n_dense, min_edges, max_per_block=0,
+                 splits=None):
         self.r0, self.r1 = r0, r1
         self.tptr, self.tcol, self.tmask = tptr, tcol, tmask
         self.rowptr_s, self.col_s = rowptr_s, col_s
         self.ntiles = int(tcol.numel())
         self.n_dense = int(n_dense)
         self.min_edges = min_edges
+        # workgroups per row block: enough for ~2 per CU when the graph has few row blocks
+        nrb = (r1 - r0 + TILE_ROWS - 1) // TILE_ROWS
+        if splits is None:
+            splits = TILE_SPLITS or max(1, min(16, max_per_block, -(-512 // max(nrb, 1))))
+        self.splits = max(1, min(64, int(splits)))
 
 
 def build_tiles(rowptr, col, r0, r1, ncols, min_edges=None):
@@ -244,8 +251,9 @@ def build_tiles(rowptr, col, r0, r1, ncols, min_edges=None):
     col_s = c[keep].to(torch.int32)
     if col_s.numel() == 0:
         col_s = torch.zeros(1, dtype=torch.int32, device=dev)   # a valid pointer for an empty remainder
+    per = tptr[1:] - tptr[:-1]
     return Tiles(r0, r1, tptr.to(torch.int32), tcol, mask, rowptr_s.to(torch.int32), col_s,
-                 int(in_tile.sum()), m)
+                 int(in_tile.sum()), m, int(per.max()) if nrb > 0 else 0)
 
 
 class Data:

@@ -111,11 +111,16 @@ class HipKernels:
         H = a_src.shape[1]
         C = h.shape[1] // H
         t = tiles
+        ws = self.tiled_workspace(t, h.device)
         with _timed("gat_agg_fwd"):
             _lib.check(self.lib.hicgat_gat_agg_fwd_tiled(
                 P(rowptr), P(col), P(t.rowptr_s), P(t.col_s), P(t.tptr), P(t.tcol), P(t.tmask), t.ntiles, N, H, C,
                 t.r0, t.r1, P(h), P(a_src), P(a_dst), P(bias), float(ns), int(act), P(out), P(out2), P(row_stats),
-                _lib.stream(h.device)), "hicgat_gat_agg_fwd_tiled")
+                t.splits, P(ws), 0 if ws is None else ws.numel(), _lib.stream(h.device)), "hicgat_gat_agg_fwd_tiled")
+
+    def tiled_workspace(self, t, device):
+        nb = self.lib.hicgat_gat_tiled_workspace_bytes(t.r1 - t.r0, t.splits)
+        return _lib.workspace(nb, device) if nb else None
 
     def agg_bwd_src_tiled(self, tiles, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src):
         """``agg_bwd_src`` over rows [tiles.r0, tiles.r1) with the dense tiles on the matrix cores."""
@@ -124,11 +129,13 @@ class HipKernels:
         C = h.shape[1] // H
         assert row_stats.stride(1) == 1 and dout.stride(1) == 1
         t = tiles
+        ws = self.tiled_workspace(t, h.device)
         with _timed("gat_agg_bwd_src"):
             _lib.check(self.lib.hicgat_gat_agg_bwd_src_tiled(
                 P(t.rowptr_s), P(t.col_s), P(t.tptr), P(t.tcol), P(t.tmask), t.ntiles, N, H, C, t.r0, t.r1, P(h),
                 P(a_src), P(a_dst), P(row_stats), row_stats.stride(0), P(dout), dout.stride(0), P(att_l), P(att_r),
-                float(ns), P(dh), P(da_src), _lib.stream(h.device)), "hicgat_gat_agg_bwd_src_tiled")
+                float(ns), P(dh), P(da_src), t.splits, P(ws), 0 if ws is None else ws.numel(),
+                _lib.stream(h.device)), "hicgat_gat_agg_bwd_src_tiled")
 
     def agg_bwd_rows(self, r0, r1, act, g, y, bias, out2, dout, row_stats):
         """Destination half of the backward without a gather (after ``agg_fwd_act`` with out2);

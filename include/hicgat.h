@@ -140,20 +140,27 @@ int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, 
  *   rowptr_s / col_s: the CSR (N + 1 row pointers, rows of the range) of every OTHER edge.
  * rowptr / col (the whole rows) give the softmax statistics.  The tiles' products run as dense
  * 32 x 32 x 32 x 512 blocks on v_mfma_f32_32x32x2_f32 (weights 0 off the edge set).  Built from the
- * CSR by hicgat.graph.Adj.tiles (a 32x32 tile is dense when it holds >= HICGAT_TILE_MIN edges). */
+ * CSR by hicgat.graph.build_tiles (a 32x32 tile is dense when it holds >= min_edges edges). */
 int hicgat_gat_agg_fwd_tiled(const int32_t *rowptr, const int32_t *col, const int32_t *rowptr_s,
                              const int32_t *col_s, const int32_t *tptr, const int32_t *tcol,
                              const uint32_t *tmask, int ntiles, int N, int H, int C, int row_begin,
                              int row_end, const float *h, const float *a_src, const float *a_dst,
                              const float *bias, float neg_slope, int act, float *out, float *out2,
-                             float *row_stats, hicgat_stream_t stream);
+                             float *row_stats, int splits, void *workspace, size_t workspace_bytes,
+                             hicgat_stream_t stream);
 int hicgat_gat_agg_bwd_src_tiled(const int32_t *rowptr_s, const int32_t *col_s, const int32_t *tptr,
                                  const int32_t *tcol, const uint32_t *tmask, int ntiles, int N, int H,
                                  int C, int row_begin, int row_end, const float *h, const float *a_src,
                                  const float *a_dst, const float *row_stats, int64_t ld_stats,
                                  const float *dout, int64_t ld_dout, const float *att_src,
                                  const float *att_dst, float neg_slope, float *dh, float *da_src,
+                                 int splits, void *workspace, size_t workspace_bytes,
                                  hicgat_stream_t stream);
+/* splits (1..64): the tiles of a row block are spread over `splits` workgroups (a graph with few
+ * row blocks, e.g. a dense 2000-node map: 63); splits > 1 needs a 16-B aligned workspace of
+ * hicgat_gat_tiled_workspace_bytes(row_end - row_begin, splits) bytes for the partial sums, which
+ * one more pass adds in split order. */
+size_t hicgat_gat_tiled_workspace_bytes(int rows, int splits);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;

@@ -11,6 +11,10 @@ graph_chr19_1mb.npz (the reference's contact matrix) and model_GATNetSelectiveRe
 (512-d features; node2vec is absent).
 
     python tests/golden/make_dscc_band.py      # ~5 min on 8 cores
+
+``--features n2v`` uses the node2vec embedding ``n2v_chr19_1mb.npz`` (tests/golden/make_n2v_chr19.py,
+this repo's GPU node2vec with the reference's parameters) instead of the fixture's random features
+and writes ``dscc_band_chr19_1mb_n2v.npz`` (BASELINE configs[0]: 512-d node2vec).
 """
 import os
 import platform
@@ -35,7 +39,9 @@ THREADS = (1, 2, 4, 8)
 def main():
     with np.load(os.path.join(HERE, "graph_chr19_1mb.npz"), allow_pickle=False) as z:
         a = np.array(z["matrix"], dtype=np.float64)
-    with np.load(os.path.join(HERE, "model_GATNetSelectiveResidualsUpdated.npz"), allow_pickle=False) as z:
+    n2v = "--features" in sys.argv and sys.argv[sys.argv.index("--features") + 1] == "n2v"
+    src = "n2v_chr19_1mb.npz" if n2v else "model_GATNetSelectiveResidualsUpdated.npz"
+    with np.load(os.path.join(HERE, src), allow_pickle=False) as z:
         x = np.asarray(z["x"], dtype=np.float32)
     np.fill_diagonal(a, 0)
     normed, keep = okr.krnorm(a.copy())
@@ -58,7 +64,7 @@ def main():
             print(f"threads {th}: dSCC {dscc[-1]:.6f}, loss {loss[-1]:.6e} ({time.time() - t0:.0f} s)", flush=True)
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
-    np.savez(os.path.join(HERE, "dscc_band_chr19_1mb.npz"), steps=np.int64(K), threads=np.array(THREADS),
+    np.savez(os.path.join(HERE, "dscc_band_chr19_1mb_n2v.npz" if n2v else "dscc_band_chr19_1mb.npz"), steps=np.int64(K), threads=np.array(THREADS),
              dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
              cpu=np.array(platform.processor() or platform.machine()))
 

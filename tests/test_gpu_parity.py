@@ -1107,8 +1107,13 @@ def test_generalize_matches_oracle_pipeline():
 
 
 # ---------------------------------------------------------------- north star: dSCC band
-def test_dscc_chr19_1mb_k3000_matches_oracle():
-    """BASELINE north star: dSCC on GM12878 chr19 1 mb within +-0.005 of the reference.  The
+@pytest.mark.parametrize("feats", ["fixture", "node2vec"])
+def test_dscc_chr19_1mb_k3000_matches_oracle(feats):
+    """feats = "node2vec": BASELINE configs[0]'s 512-d node2vec features -- the embedding this repo's
+    GPU node2vec made with the reference's parameters (tests/golden/make_n2v_chr19.py), fed to both
+    the device pipeline and the oracle band (make_dscc_band.py --features n2v).
+
+    BASELINE north star: dSCC on GM12878 chr19 1 mb within +-0.005 of the reference.  The
     HiC-GNN_main.py pipeline (:92-139) on the device -- hicgat.kr KR normalisation, load_input,
     cont2dist(y, 0.5), the fixture's 512-d features (node2vec is absent), seed-0
     initial weights, a fixed K = 3000 steps (the threshold stop is chaotic), get_model,
@@ -1119,12 +1124,12 @@ def test_dscc_chr19_1mb_k3000_matches_oracle():
     3.8e-2, at K = 3000 it is 3.3e-3."""
     import hicgat
     from oracle import kr as okr
-    band = load_golden("dscc_band_chr19_1mb.npz")
+    band = load_golden("dscc_band_chr19_1mb.npz" if feats == "fixture" else "dscc_band_chr19_1mb_n2v.npz")
     K = int(band["steps"])
     ref1 = float(band["dscc"][list(band["threads"]).index(1)])
     floor = float(band["dscc"].max() - band["dscc"].min())
     g = load_golden("graph_chr19_1mb.npz")
-    mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz")
+    mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz" if feats == "fixture" else "n2v_chr19_1mb.npz")
     a = np.array(g["matrix"], dtype=np.float64)
     np.fill_diagonal(a, 0)
     _, keep = okr.krnorm(a.copy())
@@ -1140,7 +1145,7 @@ def test_dscc_chr19_1mb_k3000_matches_oracle():
     with torch.no_grad():
         coords = model.get_model(data.x.float(), data.edge_index)
     rho = hicgat.metrics.dscc(coords, tr.dense())
-    print(f"dSCC chr19 1mb after {K} steps: device {rho:.6f}; oracle 1 thread {ref1:.6f} "
+    print(f"[{feats}] dSCC chr19 1mb after {K} steps: device {rho:.6f}; oracle 1 thread {ref1:.6f} "
           f"(|diff| {abs(rho - ref1):.2e}); oracle 1/2/4/8 threads {np.round(band['dscc'], 6)} "
           f"(noise floor {floor:.2e})")
     assert abs(rho - ref1) <= 0.005, (rho, ref1)

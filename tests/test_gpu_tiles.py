@@ -78,16 +78,21 @@ def _run(K, adj, n, tiles, seed=1):
     return dict(out=out, out2=out2, rs=rs, dout=dout, dh=dh, da_src=da_src)
 
 
-CASES = [("band", 100, 1), ("band", 100, 64), ("band", 1000, 64), ("band", 1000, 1025), ("dense", 67, 64),
-         ("dense", 300, 64), ("random", 515, 1), ("random", 515, 64), ("isolated", 200, 4)]
+CASES = [("band", 100, 1, 1), ("band", 100, 64, 2), ("band", 1000, 64, 1), ("band", 1000, 64, 5),
+         ("band", 1000, 1025, 1), ("dense", 67, 64, 1), ("dense", 300, 64, 1), ("dense", 300, 64, 4),
+         ("dense", 2000, 64, 8), ("random", 515, 1, 1), ("random", 515, 64, 3), ("isolated", 200, 4, 1),
+         ("isolated", 200, 4, 16)]
 
 
-@pytest.mark.parametrize("kind,n,tmin", CASES, ids=[f"{k}-{n}-t{t}" for k, n, t in CASES])
-def test_tiled_matches_gather(kind, n, tmin):
+@pytest.mark.parametrize("kind,n,tmin,splits", CASES, ids=[f"{k}-{n}-t{t}-s{s}" for k, n, t, s in CASES])
+def test_tiled_matches_gather(kind, n, tmin, splits):
+    """splits > 1: a row block's tiles spread over several workgroups, partials added by the
+    epilogue passes (more splits than a block has tiles leaves some workgroups with none)."""
     import hicgat
     K = hicgat.kernels.default()
     adj = _graph(kind, n)
     tiles = hicgat.graph.build_tiles(adj.rowptr32, adj.col32, 0, n, n, tmin)
+    tiles.splits = splits
     if tmin > 1024:
         assert tiles.ntiles == 0
     else:
@@ -98,7 +103,7 @@ def test_tiled_matches_gather(kind, n, tmin):
     errs = {k: _rel(got[k], ref[k]) for k in ("out", "out2", "dout", "dh", "da_src")}
     errs["delta"] = _rel(got["rs"][:, 4:6], ref["rs"][:, 4:6])
     errs["da_dst"] = _rel(got["rs"][:, 6:8], ref["rs"][:, 6:8])
-    print(kind, n, tmin, f"tiles {tiles.ntiles} dense edges {tiles.n_dense}/{adj.device_nnz}",
+    print(kind, n, tmin, splits, f"tiles {tiles.ntiles} dense edges {tiles.n_dense}/{adj.device_nnz}",
           {k: f"{v:.1e}" for k, v in errs.items()})
     for k, v in errs.items():
         assert v < 1e-5, (k, errs)
@@ -132,11 +137,19 @@ def test_tiled_abi_rejects_bad_arguments():
     z = torch.zeros(16, device=DEV)
     p = _lib.ptr(z)
     s = _lib.stream()
+    fwd = lambda nt, N, H, r0, r1, sp=1, ws=None, wb=0: lib.hicgat_gat_agg_fwd_tiled(  # noqa: E731
+        p, p, p, p, p, p, p, nt, N, H, 256, r0, r1, p, p, p, p, 0.2, 1, p, p, p, sp, ws, wb, s)
     # negative ntiles, row range outside N, unsupported heads
-    assert lib.hicgat_gat_agg_fwd_tiled(p, p, p, p, p, p, p, -1, 4, 2, 256, 0, 4, p, p, p, p, 0.2, 1, p, p, p, s) != 0
-    assert lib.hicgat_gat_agg_fwd_tiled(p, p, p, p, p, p, p, 0, 4, 2, 256, 0, 5, p, p, p, p, 0.2, 1, p, p, p, s) != 0
-    assert lib.hicgat_gat_agg_fwd_tiled(p, p, p, p, p, p, p, 0, 4, 1, 256, 0, 4, p, p, p, p, 0.2, 1, p, p, p, s) != 0
+    assert fwd(-1, 4, 2, 0, 4) != 0
+    assert fwd(0, 4, 2, 0, 5) != 0
+    assert fwd(0, 4, 1, 0, 4) != 0
     assert lib.hicgat_gat_agg_bwd_src_tiled(p, p, p, None, None, 3, 4, 2, 256, 0, 4, p, p, p, p, 8, p, 512, p, p,
-                                            0.2, p, p, s) != 0
+                                            0.2, p, p, 1, None, 0, s) != 0
+    # splits > 1 without (or with too small) a workspace; splits out of range
+    need = lib.hicgat_gat_tiled_workspace_bytes(4, 2)
+    assert need > 0 and lib.hicgat_gat_tiled_workspace_bytes(4, 1) == 0
+    assert fwd(0, 4, 2, 0, 4, 2) != 0
+    assert fwd(0, 4, 2, 0, 4, 2, p, need - 4) != 0
+    assert fwd(0, 4, 2, 0, 4, 0) != 0 and fwd(0, 4, 2, 0, 4, 65) != 0
     # an empty range is a no-op
-    assert lib.hicgat_gat_agg_fwd_tiled(p, p, p, p, p, p, p, 0, 4, 2, 256, 2, 2, p, p, p, p, 0.2, 1, p, p, p, s) == 0
+    assert fwd(0, 4, 2, 2, 2) == 0

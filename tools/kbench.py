@@ -61,6 +61,12 @@ def main():
     g256, g256b, g256c = torch.randn(256, device=dev), torch.empty(256, device=dev), torch.empty(256, device=dev)
     ya2 = torch.empty(n, 256, device=dev)
     libs = [s for s in a.libs.split(",") if s] or [_lib.LIB_PATH]
+    _tiles = {}
+
+    def tiles():   # the dense-tile split at HICGAT_TILE_MIN (64 when tiling is off by default)
+        if not _tiles:
+            _tiles["t"] = hicgat.graph.build_tiles(adj.rowptr32, adj.col32, 0, n, n, hicgat.graph.TILE_MIN or 64)
+        return _tiles["t"]
     def _with_impl(K, impl, fn):
         saved, K.gemm_impl = K.gemm_impl, impl
         try:
@@ -90,6 +96,10 @@ def main():
         "param_grad": lambda K: K.param_grad(h, dout, da, rs, 2),
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
         "pairdist_combined": lambda K: K.fused_loss(coords, truth.buf, n, 1, 0, -1, stats, loss, dc),
+        "pairdist_support": lambda K: K.fused_loss_support(coords, truth.support, n, 0, stats, loss, dc),
+        "gat_agg_fwd_tiled": lambda K: K.agg_fwd_tiled(adj.rowptr32, adj.col32, tiles(), h, a_s, a_d, b, 0.2, 1, out,
+                                                       out2, rs),
+        "gat_agg_bwd_src_tiled": lambda K: K.agg_bwd_src_tiled(tiles(), h, a_s, a_d, rs, dout, al, ar, 0.2, dh, da),
         "colsum_20000x512": lambda K: K.colsum(out, cs),
         "ln_bwd_256": lambda K: K.ln_relu_res_bwd(ya, ya, lns, g256, g256, ya2, g256b, g256c),
         "adam": lambda K: K.adam(flat, g, m, v, flat.numel(), 1e-3, 0.9, 0.999, 1e-8, 1),
