@@ -18,6 +18,9 @@
 // Source side (row r) gathers dout_i of the rows that have r as a neighbour.  The graph is
 // structurally symmetric (to_symmetric, utils.py:71), so row r's own CSR list *is* that set: the
 // transpose needs no permutation array and no atomics.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 
 #ifndef HICGAT_BWD_U
@@ -117,8 +120,42 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
 // dh gets the raw sum (no logit terms) and da_src the remainder's share of da_src; the matrix-core
 // pass over the dense tiles adds the rest and finishes both.
 template <bool SPLIT = false>
+__device__ __forceinline__ void agg_bwd_src_row(
+    int r, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout, int64_t ldq,
+    const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
+    float *__restrict__ dh, float *__restrict__ da_src);
+
+// Persistent when the grid is smaller than the row-block count (HICGAT_SRC_WGS per CU): each
+// workgroup walks row blocks b, b + gridDim.x, ... (the same XCD for all of them), so the CUs keep
+// free slots for the parameter-gradient GEMMs the side stream runs beside this pass.
+template <bool SPLIT = false, bool PERSIST = false>
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
+    const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
+    const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout, int64_t ldq,
+    const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
+    float *__restrict__ dh, float *__restrict__ da_src) {
+  const int nblk = (row_end - row_begin + 3) / 4;
+  if constexpr (!PERSIST) {
+    const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+    if (r < row_end)
+      agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh,
+                             da_src);
+  } else {
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+      const int r = row_begin + xcd_remap(b, nblk) * 4 + wave_in_block();
+      if (r < row_end)
+        agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh,
+                               da_src);
+    }
+  }
+}
+
+template <bool SPLIT>
+__device__ __forceinline__ void agg_bwd_src_row(
+    int r, const int *__restrict__ rowptr, const int *__restrict__ col,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout, int64_t ldq,
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
@@ -127,8 +164,6 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
   // a multi-GPU caller can all-gather [dout | row stats] rows as one packed buffer)
   constexpr int U = HICGAT_SRC_U;
   const int lane = lane_id();
-  const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (r >= row_end) return;
   const int beg = rowptr[r], end = rowptr[r + 1];
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
@@ -309,11 +344,31 @@ __global__ __launch_bounds__(1024) void param_grad_stage2(const float *__restric
   }
 }
 
+// Grid of the source pass: one workgroup per 4 rows, or HICGAT_SRC_WGS workgroups per CU (persistent)
+// when set -- then the gather leaves CU slots to the side stream's GEMMs.
+static int src_grid(int rows) {
+  static const int per_cu = getenv("HICGAT_SRC_WGS") ? atoi(getenv("HICGAT_SRC_WGS")) : 0;
+  const int full = (rows + 3) / 4;
+  if (per_cu <= 0) return full;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return std::max(1, std::min(full, per_cu * cus));
+}
+#define HICGAT_SRC_LAUNCH(SPLIT_, rows_, ...)                                                              \
+  do {                                                                                                     \
+    const int g_ = src_grid(rows_);                                                                        \
+    if (g_ < ((rows_) + 3) / 4)                                                                            \
+      hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, true>), dim3(g_), dim3(256), 0, __VA_ARGS__);  \
+    else                                                                                                   \
+      hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, false>), dim3(g_), dim3(256), 0, __VA_ARGS__); \
+  } while (0)
+
 // The gather half of hicgat_gat_agg_bwd_src_tiled (gat_tiles.hip): the sparse remainder's shares.
 int agg_bwd_src_split_launch(const int *rowptr_s, const int *col_s, int row_begin, int row_end, const float *h,
                              const float *a_src, const float *a_dst, const float *row_stats, int64_t ldr,
                              const float *dout, int64_t ldq4, float ns, float *dh, float *da_src, hipStream_t s) {
-  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel<true>, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, s, rowptr_s,
+  HICGAT_SRC_LAUNCH(true, row_end - row_begin, s, rowptr_s,
                      col_s, row_begin, row_end, h, a_src, a_dst, row_stats, ldr, dout, ldq4, nullptr, nullptr, ns, dh,
                      da_src);
   HICGAT_CHECK_LAUNCH();
@@ -355,7 +410,7 @@ extern "C" int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *c
       !dh || !da_src)
     return HICGAT_EINVAL;
   const int rows = row_end - row_begin;
-  hipLaunchKernelGGL(agg_bwd_src_h2c256_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0,
+  HICGAT_SRC_LAUNCH(false, rows,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
                      row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();

@@ -177,20 +177,31 @@ class Adj:
 
     def tiles(self, min_edges=None):
         """The dense-tile split of the device CSR (``build_tiles``), built once per CSR and cached;
-        None when tiling is off (HICGAT_TILE_MIN=0)."""
+        None when tiling is off (HICGAT_TILE_MIN=0) or, for the default threshold, when the dense
+        tiles hold less than TILE_FRAC of the edges."""
         m = TILE_MIN if min_edges is None else int(min_edges)
         if m <= 0:
             return None
         key = (self.rowptr32.data_ptr(), self.col32.data_ptr(), m)
         cache = getattr(self, "_tiles", None)
         if cache is None or cache[0] != key:
-            self._tiles = cache = (key, build_tiles(self.rowptr32, self.col32, 0, self.n, self.n, m))
+            t = build_tiles(self.rowptr32, self.col32, 0, self.n, self.n, m)
+            # the tiled form pays where the dense tiles hold nearly every edge (a dense contact map:
+            # synth-2000 0.96 vs 1.20 ms per step); on a power-law graph whose tiles hold about half
+            # the edges (synth-20000) the gather alone is faster (2.07 vs 2.39 ms per step)
+            # (and a graph of a few row blocks, e.g. chr19 1 mb with 58 loci, gains nothing either)
+            if min_edges is None and (t.n_dense < TILE_FRAC * self.device_nnz or self.n < TILE_MIN_N):
+                t = None
+            self._tiles = cache = (key, t)
         return cache[1]
 
 
 # A 32x32 tile of the contact graph goes to the matrix cores when it holds at least this many
 # edges (DESIGN.md section 3: a dense tile costs the MFMA time of ~64 gathered edges); 0 = off.
 TILE_MIN = int(os.environ.get("HICGAT_TILE_MIN", "64"))
+# ... and the tiled form is used when the dense tiles hold at least this fraction of the edges
+TILE_FRAC = float(os.environ.get("HICGAT_TILE_FRAC", "0.9"))
+TILE_MIN_N = int(os.environ.get("HICGAT_TILE_MIN_N", "512"))
 TILE_ROWS = 32
 TILE_SPLITS = int(os.environ.get("HICGAT_TILE_SPLITS", "0"))   # 0 = from the row-block count
 

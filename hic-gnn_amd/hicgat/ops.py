@@ -51,8 +51,13 @@ SIDE_PRIO = int(os.environ.get("HICGAT_SIDE_PRIO", "0"))
 # per step) or queued onto the side stream behind the tail's dW work (0: 2.037 / 2.037 ms)
 LINL_MAIN = os.environ.get("HICGAT_LINL_MAIN", "1") != "0"
 # the GAT param_grad (datt_l, datt_r, dbias column sums) on a second side stream beside lin_l's dW
-# (1, default) or on the backward's stream in front of it (0)
-PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "1") != "0"
+# (1: measured 2.06 vs 1.98 ms per step) or on the backward's stream in front of it (0, default)
+PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "0") != "0"
+# issue order of the deferred side work: "fifo" (backward order, default) or "size" (largest first:
+# with the full-grid source pass the big dW GEMMs then wait for it to drain, 2.007 vs 1.978 ms per
+# step; with HICGAT_SRC_WGS=2 they all finish beside it, but the thinner gather takes 611 vs 489 us
+# and the step is the same, 1.953 vs 1.953-1.959 ms median)
+SIDE_ORDER = os.environ.get("HICGAT_SIDE_ORDER", "fifo")
 
 
 def side_begin():
@@ -79,9 +84,8 @@ def side_flush(after=None):
         queue, _SIDE["queue"] = _SIDE["queue"], []
     if not queue:
         return
-    # largest first: the big weight-gradient GEMMs then get CU slots while the gather pass beside
-    # them still leaves some, and the tiny ones (3 x 64 outputs) trail (stable: equal work keeps order)
-    queue.sort(key=lambda q: -q[2])
+    if SIDE_ORDER == "size":
+        queue.sort(key=lambda q: -q[2])
     with _side(*[t for _, keep, _ in queue for t in keep], after=after):
         for fn, _, _ in queue:
             fn()

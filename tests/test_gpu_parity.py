@@ -1111,7 +1111,9 @@ def test_generalize_matches_oracle_pipeline():
 def test_dscc_chr19_1mb_k3000_matches_oracle(feats):
     """feats = "node2vec": BASELINE configs[0]'s 512-d node2vec features -- the embedding this repo's
     GPU node2vec made with the reference's parameters (tests/golden/make_n2v_chr19.py), fed to both
-    the device pipeline and the oracle band (make_dscc_band.py --features n2v).
+    the device pipeline and the oracle band (make_dscc_band.py --features n2v).  With them the
+    flagship collapses to constant coordinates in the oracle (dSCC undefined), so that case checks
+    that the device lands on the same degenerate fixed point (final loss within 1e-3).
 
     BASELINE north star: dSCC on GM12878 chr19 1 mb within +-0.005 of the reference.  The
     HiC-GNN_main.py pipeline (:92-139) on the device -- hicgat.kr KR normalisation, load_input,
@@ -1141,10 +1143,20 @@ def test_dscc_chr19_1mb_k3000_matches_oracle(feats):
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
     tr = hicgat.Truth.from_contacts(data.y, 0.5)
-    hicgat.train.train(model, data, tr, steps=K)
+    _, hist = hicgat.train.train(model, data, tr, steps=K)
     with torch.no_grad():
         coords = model.get_model(data.x.float(), data.edge_index)
     rho = hicgat.metrics.dscc(coords, tr.dense())
+    if feats == "node2vec":
+        # with these node2vec features the oracle itself collapses to (near-)constant coordinates
+        # at 1/2/4/8 threads (final loss 8.5743e-2 at 1, 4 and 8 threads, dSCC undefined / 0.0035):
+        # the device must reach the same degenerate fixed point -- same final loss, no rank signal
+        loss1 = float(band["loss"][list(band["threads"]).index(1)])
+        print(f"[node2vec] device loss {hist[-1]:.6e} dSCC {rho}; oracle 1 thread loss {loss1:.6e}, "
+              f"dSCC 1/2/4/8 threads {band['dscc']}")
+        assert abs(hist[-1] - loss1) <= 1e-3 * loss1, (hist[-1], loss1)
+        assert not (abs(rho) > 0.05), rho
+        return
     print(f"[{feats}] dSCC chr19 1mb after {K} steps: device {rho:.6f}; oracle 1 thread {ref1:.6f} "
           f"(|diff| {abs(rho - ref1):.2e}); oracle 1/2/4/8 threads {np.round(band['dscc'], 6)} "
           f"(noise floor {floor:.2e})")

@@ -119,12 +119,15 @@ def test_tiled_gat_conv_autograd_matches_gather(monkeypatch):
     res = {}
     for tmin in (0, 32):
         monkeypatch.setattr(hicgat.graph, "TILE_MIN", tmin)
+        monkeypatch.setattr(hicgat.graph, "TILE_FRAC", 0.0)
         torch.manual_seed(0)
         conv = hicgat.GATConv(512, 256, heads=2).to(DEV)
         y = conv(x, adj, act="relu")
         (y * torch.linspace(-1, 1, 512, device=DEV)).sum().backward()
         res[tmin] = (y.detach(), {k: p.grad.detach().clone() for k, p in conv.named_parameters()})
     assert adj.tiles(32) is not None and adj.tiles(0) is None
+    res_tiled_used = adj._tiles[1] is not None
+    assert res_tiled_used
     assert _rel(res[32][0], res[0][0]) < 1e-5
     for k in res[0][1]:
         assert _rel(res[32][1][k], res[0][1][k]) < 1e-4, k
@@ -153,3 +156,20 @@ def test_tiled_abi_rejects_bad_arguments():
     assert fwd(0, 4, 2, 0, 4, 0) != 0 and fwd(0, 4, 2, 0, 4, 65) != 0
     # an empty range is a no-op
     assert fwd(0, 4, 2, 2, 2) == 0
+
+
+def test_tile_policy_dense_vs_power_law(monkeypatch):
+    """Adj.tiles(): the tiled form for a (nearly) dense contact map, the gather alone for a
+    power-law graph whose dense tiles hold only part of the edges (HICGAT_TILE_FRAC)."""
+    import hicgat
+    from hicgat import synth
+    dense = _graph("dense", 600)
+    assert dense.tiles() is not None and dense.tiles().n_dense == dense.device_nnz
+    assert _graph("dense", 100).tiles() is None          # a few row blocks: the gather alone
+    n = 3000
+    i, j, c = synth.contact_pairs(n, density=0.01, seed=0)
+    sparse = hicgat.Adj.from_dense_device(synth.dense_contacts(n, i, j, c, device=DEV), keep_host=False)
+    assert sparse.tiles() is None
+    monkeypatch.setattr(hicgat.graph, "TILE_FRAC", 0.0)
+    sparse._tiles = None
+    assert sparse.tiles() is not None
