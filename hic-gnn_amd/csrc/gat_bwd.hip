@@ -282,64 +282,78 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
 }
 
 // ---- GATConv parameter gradients: deterministic two-stage column reductions over N rows. ------
-// stage 1: block b sums rows [b*R, (b+1)*R) into part[b][3][D] (datt_src, datt_dst, dbias);
+// Three parts: datt_src (sum_n da_src[n,h] h[n,:]), datt_dst (sum_n da_dst[n,h] h[n,:]) and dbias
+// (sum_n dout[n,:]); any subset may be asked for (PARTS bit 0 / 1 / 2), so datt_dst and dbias --
+// known after the gather-free row pass -- can be summed beside the source-side gather and only
+// datt_src is left behind it.  Each part's sum runs in the same order whatever subset is asked for
+// (bitwise the all-parts call).
+// stage 1: block b sums rows [b*R, (b+1)*R) into part[b][P][D] (the P asked-for parts in order);
 // stage 2: one thread per output column sums the partials in block order.
 #ifndef HICGAT_PG_BLOCKS
 #define HICGAT_PG_BLOCKS 512    // 1024 measured slower (stage 2 sums twice the partials)
 #endif
 constexpr int kParamBlocks = HICGAT_PG_BLOCKS;   // row blocks of stage 1 (128 left half the CUs idle)
 
+template <int PARTS>
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,
                                                          const float *__restrict__ dout,
                                                          const float *__restrict__ da_src,
                                                          const float *__restrict__ row_stats, int N,
                                                          int H, int C, int rows_per_block,
                                                          float *__restrict__ part) {
+  constexpr bool kS = PARTS & 1, kT = PARTS & 2, kB = PARTS & 4;
+  constexpr int P = (int)kS + (int)kT + (int)kB;
   const int D = H * C, Q = D / 4;
   const int r0 = blockIdx.x * rows_per_block, r1 = min(N, r0 + rows_per_block);
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
   const float4 *g4 = reinterpret_cast<const float4 *>(dout);
-  float4 *p4 = reinterpret_cast<float4 *>(part + (size_t)blockIdx.x * 3 * D);
+  float4 *p4 = reinterpret_cast<float4 *>(part + (size_t)blockIdx.x * P * D);
   for (int q = threadIdx.x; q < Q; q += blockDim.x) {
     const int hd = (4 * q) / C;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f), t = s, b = s;
 #pragma unroll 4   // several rows' loads in flight per thread (one wave per SIMD at this grid size)
     for (int n = r0; n < r1; ++n) {
-      const float4 hv = h4[(size_t)n * Q + q], gv = g4[(size_t)n * Q + q];
-      s = f4_fma(da_src[(size_t)n * H + hd], hv, s);
-      t = f4_fma(row_stats[(size_t)n * 4 * H + 3 * H + hd], hv, t);
-      b.x += gv.x; b.y += gv.y; b.z += gv.z; b.w += gv.w;
+      if (kS || kT) {
+        const float4 hv = h4[(size_t)n * Q + q];
+        if (kS) s = f4_fma(da_src[(size_t)n * H + hd], hv, s);
+        if (kT) t = f4_fma(row_stats[(size_t)n * 4 * H + 3 * H + hd], hv, t);
+      }
+      if (kB) {
+        const float4 gv = g4[(size_t)n * Q + q];
+        b.x += gv.x; b.y += gv.y; b.z += gv.z; b.w += gv.w;
+      }
     }
-    p4[q] = s;
-    p4[Q + q] = t;
-    p4[2 * Q + q] = b;
+    int o = 0;
+    if (kS) p4[(o++) * Q + q] = s;
+    if (kT) p4[(o++) * Q + q] = t;
+    if (kB) p4[o * Q + q] = b;
   }
 }
 
 // block = 64 output columns x 16 groups (1024 threads); group g adds partials b = g, g+16, ...;
 // the groups are combined in order through LDS (fixed order: bitwise reproducible).  Only
-// 3D / 64 = 24 blocks exist, so the partial range is cut 16 ways to keep each thread's chain of
+// P*D / 64 blocks exist, so the partial range is cut 16 ways to keep each thread's chain of
 // dependent loads short (32 partials at nblk = 512).
 constexpr int kPG2Groups = 16;
+struct PGOut {
+  float *o[3];
+};
 __global__ __launch_bounds__(1024) void param_grad_stage2(const float *__restrict__ part, int nblk,
-                                                          int D, float *__restrict__ datt_s,
-                                                          float *__restrict__ datt_d,
-                                                          float *__restrict__ dbias, int accumulate) {
+                                                          int P, int D, PGOut out, int accumulate) {
   __shared__ float red[kPG2Groups][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  if (c < 3 * D) {
-    for (int b = grp; b < nblk; b += kPG2Groups) s += part[(size_t)b * 3 * D + c];
+  if (c < P * D) {
+    for (int b = grp; b < nblk; b += kPG2Groups) s += part[(size_t)b * P * D + c];
   }
   red[grp][cl] = s;
   __syncthreads();
-  if (grp == 0 && c < 3 * D) {
+  if (grp == 0 && c < P * D) {
     float t = red[0][cl];
 #pragma unroll
     for (int g = 1; g < kPG2Groups; ++g) t += red[g][cl];
-    const int which = c / D, cc = c % D;
-    float *o = (which == 0 ? datt_s : which == 1 ? datt_d : dbias) + cc;
+    float *o = out.o[c / D] + c % D;
     *o = t + (accumulate ? *o : 0.f);
   }
 }
@@ -461,19 +475,34 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
                                      size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || H <= 0 || C <= 0 || (C % 4) != 0) return HICGAT_EINVAL;
   const int D = H * C;
-  if (!h || !dout || !da_src || !row_stats || !datt_src || !datt_dst || !dbias || !workspace)
+  const int parts = (datt_src ? 1 : 0) | (datt_dst ? 2 : 0) | (dbias ? 4 : 0);
+  if (!parts || !workspace) return HICGAT_EINVAL;
+  if (((parts & 3) && !h) || ((parts & 1) && !da_src) || ((parts & 2) && !row_stats) || ((parts & 4) && !dout))
     return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_gat_param_grad_workspace_bytes(N, D)) return HICGAT_EINVAL;
   const int rpb = N > 0 ? (N + kParamBlocks - 1) / kParamBlocks : 1;
   const int nblk = N > 0 ? (N + rpb - 1) / rpb : 0;
   float *part = static_cast<float *>(workspace);
+  PGOut out{};
+  int P = 0;
+  if (datt_src) out.o[P++] = datt_src;
+  if (datt_dst) out.o[P++] = datt_dst;
+  if (dbias) out.o[P++] = dbias;
+  hipStream_t s = (hipStream_t)stream;
   if (nblk > 0) {
-    hipLaunchKernelGGL(param_grad_stage1, dim3(nblk), dim3(128), 0, (hipStream_t)stream, h, dout,
-                       da_src, row_stats, N, H, C, rpb, part);
+#define HICGAT_PG1(PARTS_)                                                                                      \
+  case PARTS_:                                                                                                  \
+    hipLaunchKernelGGL(param_grad_stage1<PARTS_>, dim3(nblk), dim3(128), 0, s, h, dout, da_src, row_stats, N, H, \
+                       C, rpb, part);                                                                           \
+    break;
+    switch (parts) {
+      HICGAT_PG1(1) HICGAT_PG1(2) HICGAT_PG1(3) HICGAT_PG1(4) HICGAT_PG1(5) HICGAT_PG1(6) HICGAT_PG1(7)
+    }
+#undef HICGAT_PG1
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(param_grad_stage2, dim3((3 * D + 63) / 64), dim3(64 * kPG2Groups), 0,
-                     (hipStream_t)stream, part, nblk, D, datt_src, datt_dst, dbias, accumulate);
+  hipLaunchKernelGGL(param_grad_stage2, dim3((P * D + 63) / 64), dim3(64 * kPG2Groups), 0, s, part, nblk, P, D,
+                     out, accumulate);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

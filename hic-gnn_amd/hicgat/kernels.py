@@ -173,7 +173,8 @@ class HipKernels:
 
     def param_grad(self, h, dout, da_src, row_stats, H, out=None, accumulate=False):
         """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D]); ``out`` =
-        three destination tensors (e.g. the parameters' own .grad views) to write or add into."""
+        three destination tensors (e.g. the parameters' own .grad views) to write or add into; a
+        None among them skips that part (datt_dst / dbias need no source-pass output)."""
         N, D = h.shape
         C = D // H
         dev = h.device

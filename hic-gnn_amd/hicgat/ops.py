@@ -35,9 +35,9 @@ def _sink(p):
 _SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": []}
 _SIDE_LOCK = threading.Lock()
 OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
-# LayerNorm dgamma/dbeta reductions on the side stream too (else inside the row-pass call): measured
-# slower, with and without deferral
-LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "0") != "0"
+# LayerNorm dgamma/dbeta reductions queued with the deferred side work (1, default: 1.959 / 1.945 vs
+# 1.965 / 1.961 ms per step, two A/B pairs, profiles/r02d_ab_step.txt) or inside the row-pass call (0)
+LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "1") != "0"
 # bias column sums / GAT param_grad on the side stream (else on the backward's stream)
 SMALL_SIDE = os.environ.get("HICGAT_SMALL_SIDE", "1") != "0"
 # Deferred side work (HICGAT_DEFER=1, the default): the tail's parameter-gradient launches are
@@ -58,6 +58,11 @@ PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "0") != "0"
 # step; with HICGAT_SRC_WGS=2 they all finish beside it, but the thinner gather takes 611 vs 489 us
 # and the step is the same, 1.953 vs 1.953-1.959 ms median)
 SIDE_ORDER = os.environ.get("HICGAT_SIDE_ORDER", "fifo")
+# the GAT param_grad split (1): datt_dst / dbias on the second side stream beside the source pass,
+# only datt_src behind it -- measured slower (2.02-2.03 vs 1.95-1.96 ms per step: the 82 MB stream
+# beside the gather slows it more than the 30 us it takes off the tail); 0 (default): all three
+# behind the source pass
+PG_SPLIT = os.environ.get("HICGAT_PG_SPLIT", "0") != "0"
 
 
 def side_begin():
@@ -238,13 +243,19 @@ class _GATConvFn(torch.autograd.Function):
         pW, pl, pr, pb = ctx.params
         sinks = (_sink(pl), _sink(pr), _sink(pb) if ctx.has_bias else None)
         use_sinks = all(t is not None for t in sinks)
+        chunks = _src_chunks(N) if ctx.tiles is None else [(0, N)]
+        pg_split = use_sinks and PG_SPLIT and _SIDE["on"] and len(chunks) == 1
+        if pg_split:
+            # datt_dst and dbias need only the row pass's outputs: summed on the second side stream
+            # beside the source pass; datt_src (da_src) is left behind it
+            with _side(h, dout, row_stats, lane=1):
+                K.param_grad(h, dout, None, row_stats, H, out=(None, sinks[1].view(-1), sinks[2]), accumulate=True)
         gW = _sink(pW) if ctx.needs_input_grad[1] else None
         # The source pass runs in row chunks; each chunk's parameter-gradient share (param_grad
         # partial column sums, dW += dh_c^T x_c) is issued right after it -- on the side stream
         # when overlapping -- so only the last chunk's share is left after the gathers (the
         # backward's tail).  The sink and autograd paths add the same partials in the same order.
         datt_l = datt_r = dbias = dW = None
-        chunks = _src_chunks(N) if ctx.tiles is None else [(0, N)]
         for c, (r0, r1) in enumerate(chunks):
             if ctx.tiles is not None:
                 K.agg_bwd_src_tiled(ctx.tiles, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
@@ -254,10 +265,11 @@ class _GATConvFn(torch.autograd.Function):
                 side_flush(after=fork)
             rows = slice(r0, r1)
             if use_sinks:
-                # on a second side stream (PG_SIDE, default), beside lin_l's dW GEMM on this one
+                # on a second side stream (PG_SIDE), beside lin_l's dW GEMM on this one, or in front of it
                 with (_side(h, dout, da_src, row_stats, lane=1) if PG_SIDE else contextlib.nullcontext()):
                     K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                                 out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]), accumulate=True)
+                                 out=((sinks[0].view(-1), None, None) if pg_split else
+                                      (sinks[0].view(-1), sinks[1].view(-1), sinks[2])), accumulate=True)
             else:
                 datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
                                                      out=None if c == 0 else (datt_l, datt_r, dbias),

@@ -164,7 +164,10 @@ size_t hicgat_gat_tiled_workspace_bytes(int rows, int splits);
 /* Column reductions for the GATConv parameter gradients over N rows (pass pointers offset to a
  * shard's first row for a partial sum; deterministic, two-stage):
  *   datt_src[h,c] = sum_n da_src[n,h] h[n,h,c];  datt_dst likewise with row_stats' da_dst;
- *   dbias[c] = sum_n dout[n,c].  workspace: hicgat_gat_param_grad_workspace_bytes(N, H*C). */
+ *   dbias[c] = sum_n dout[n,c].  workspace: hicgat_gat_param_grad_workspace_bytes(N, H*C).
+ * Any of datt_src / datt_dst / dbias may be NULL (that part is skipped, and the inputs only it
+ * reads may be NULL too): datt_dst and dbias need no source-pass output, so they can be summed
+ * beside that pass; each part is bitwise the same whichever subset is asked for. */
 int hicgat_gat_param_grad(const float *h, const float *dout, const float *da_src,
                           const float *row_stats, int N, int H, int C, float *datt_src,
                           float *datt_dst, float *dbias, int accumulate, void *workspace,

@@ -148,12 +148,14 @@ class CpuKernels:
         n, D = h.shape
         C = D // H
         hv = h.view(n, H, C).double()
-        datt_l = (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
+        datt_l = None if da_src is None else (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
         datt_r = (row_stats[:, 3 * H:4 * H].double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
-        res = (datt_l, datt_r, dout.double().sum(0).float())
+        res = (datt_l, datt_r, None if dout is None else dout.double().sum(0).float())
         if out is None:
             return res
         for o, r in zip(out, res):
+            if o is None:
+                continue
             if accumulate:
                 o.add_(r)
             else:

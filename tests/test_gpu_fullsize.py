@@ -125,7 +125,14 @@ def test_synth20000_gat_backward_matches_fp64(tiled):
     else:
         K.agg_bwd_src(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, rs, dout, att_l, att_r, 0.2, dh, da_src)
     datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, rs, 2)
+    # any subset of the three parts (the split the training backward issues: datt_dst + dbias
+    # beside the source pass, datt_src behind it) is bitwise the all-parts call
+    parts = [torch.full((512,), 7.0, device=DEV) for _ in range(3)]
+    K.param_grad(h, dout, None, rs, 2, out=(None, parts[1], parts[2]))
+    K.param_grad(h, None, da_src, rs, 2, out=(parts[0], None, None))
     torch.cuda.synchronize()
+    for got, want in zip(parts, (datt_l, datt_r, dbias)):
+        assert torch.equal(got, want)
     ref = _fp64_gat_train(adj.rowptr32, adj.col32, h, att_l, att_r, bias, g, out > 0)
     # relu decisions may differ from fp64 only where the pre-activation is at rounding level
     flip = (out > 0) != (ref["out"] > 0)

@@ -313,6 +313,28 @@ def test_tall_gemm_edges_and_accumulate(m, n, k):
         assert _rel(ys.cpu(), (xs.double() @ w.double().t() + b.double()).cpu()) < 5e-6
 
 
+@pytest.mark.parametrize("m,n,k,splits", [(128, 128, 1001, 3), (512, 256, 17, 1), (256, 128, 20000, 1),
+                                          (128, 384, 4099, 64), (512, 512, 20000, 32)])
+def test_wgrad_dma_ragged_strided(m, n, k, splits):
+    """The LDS-DMA weight-gradient kernel (gemm_wgrad.hip: M, N multiples of 128) on K not a multiple
+    of its 16-row stage and splits whose last stage is partial (rows past the split's end loaded and
+    zeroed), row-strided operands, with and without the bias column sums and accumulate, vs fp64."""
+    import hicgat
+    K = hicgat.kernels.default()
+    torch.manual_seed(m + n + k + splits)
+    dy = torch.randn(k, m + 4, device=DEV)[:, :m]
+    x = torch.randn(k, n + 8, device=DEV)[:, 4:4 + n]
+    rW = dy.double().t() @ x.double()
+    tol = 5e-6 * max(1.0, (k / splits / 512) ** 0.5)
+    dW0, db0 = torch.randn(m, n, device=DEV), torch.randn(m, device=DEV)
+    dW, db = dW0.clone(), db0.clone()
+    K.wgrad(dy, x, dW, db, accumulate=True, splits=splits)
+    assert _rel(dW.cpu(), (rW + dW0.double()).cpu()) < tol
+    assert _rel(db.cpu(), (dy.double().sum(0) + db0.double()).cpu()) < tol
+    dW2 = K.gemm(1, 1, m, n, k, dy, x, torch.empty(m, n, device=DEV), splits=splits)
+    assert _rel(dW2.cpu(), rW.cpu()) < tol
+
+
 @pytest.mark.parametrize("splits", [1, 7, 78])
 def test_wgrad_bias_fold_matches_fp64(splits):
     """hicgat_gemm_wgrad: dW = dY^T X and db = column sums of dY from ONE split-K GEMM launch (the
