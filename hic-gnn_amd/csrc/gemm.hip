@@ -522,9 +522,6 @@ static bool x3_ok(const float *A, int64_t lda, const float *B, int64_t ldb, int 
   return a_ok && b_ok && al && N >= 64 && M >= 32;
 }
 
-int gemm_wgrad_dma_launch(const float *dY, int64_t ldy, const float *X, int64_t ldx, float *C, int64_t ldc, int M,
-                          int N, int K, int splits, float *slab, int accumulate, float *csum,
-                          hipStream_t s);   // gemm_wgrad.hip
 int gemm_tall_launch(bool b_kmajor, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
                      int M, int N, int K, const float *bias, int accumulate, hipStream_t s);   // gemm_tall.hip
 
@@ -540,11 +537,6 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
   // tall node-row problems (Linear forward, input gradient): the 160x128 LDS-DMA kernel (gemm_tall.hip)
   if (!AK && impl == HICGAT_GEMM_F32 && splits == 1 && M >= 1024 && tall_enabled()) {
     const int rc = gemm_tall_launch(BK_, A, lda, B, ldb, C, ldc, M, N, K, bias, acc, s);
-    if (rc != HICGAT_EUNSUPPORTED) return rc;
-  }
-  // weight gradients (both operands K-major) on the LDS-DMA kernel (gemm_wgrad.hip) when they fit
-  if (AK && BK_ && impl == HICGAT_GEMM_F32 && !bias) {
-    const int rc = gemm_wgrad_dma_launch(A, lda, B, ldb, C, ldc, M, N, K, splits, slab, acc, nullptr, s);
     if (rc != HICGAT_EUNSUPPORTED) return rc;
   }
   if (impl != HICGAT_GEMM_F32 && x3_ok<AK, BK_>(A, lda, B, ldb, M, N, K)) {
@@ -621,8 +613,6 @@ extern "C" int hicgat_gemm_wgrad(int M, int N, int K, const float *dY, int64_t l
   hipStream_t s = (hipStream_t)stream;
   float *slab = static_cast<float *>(workspace);
   // the dispatch of hicgat_gemm_ex's fp32 path for the (K-major, K-major) layout
-  const int rc = gemm_wgrad_dma_launch(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, slab, accumulate, db, s);
-  if (rc != HICGAT_EUNSUPPORTED) return rc;
   if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
     return launch<128, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
   if (N >= 128) return launch<64, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);

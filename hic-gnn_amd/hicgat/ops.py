@@ -58,6 +58,9 @@ PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "0") != "0"
 # step; with HICGAT_SRC_WGS=2 they all finish beside it, but the thinner gather takes 611 vs 489 us
 # and the step is the same, 1.953 vs 1.953-1.959 ms median)
 SIDE_ORDER = os.environ.get("HICGAT_SIDE_ORDER", "fifo")
+# deferred side work of at least this many multiply-adds (rows * m * n of a dW GEMM) goes to a
+# second side stream of its own (0: one side stream for all of it)
+SIDE_BIG = float(os.environ.get("HICGAT_SIDE_BIG", "0"))
 # the GAT param_grad split (1): datt_dst / dbias on the second side stream beside the source pass,
 # only datt_src behind it -- measured slower (2.02-2.03 vs 1.95-1.96 ms per step: the 82 MB stream
 # beside the gather slows it more than the 30 us it takes off the tail); 0 (default): all three
@@ -91,9 +94,17 @@ def side_flush(after=None):
         return
     if SIDE_ORDER == "size":
         queue.sort(key=lambda q: -q[2])
-    with _side(*[t for _, keep, _ in queue for t in keep], after=after):
-        for fn, _, _ in queue:
-            fn()
+    lanes = [queue]
+    if SIDE_BIG > 0:
+        # the big dW GEMMs on their own side stream: they start as the gather drains instead of
+        # queueing behind the small launches that crawl beside it
+        lanes = [[q for q in queue if q[2] < SIDE_BIG], [q for q in queue if q[2] >= SIDE_BIG]]
+    for lane, items in zip((0, 2), lanes):
+        if not items:
+            continue
+        with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
+            for fn, _, _ in items:
+                fn()
 
 
 def side_join():
@@ -294,9 +305,12 @@ class _GATConvFn(torch.autograd.Function):
         return (dx, dW, datt_l, datt_r, dbias, None, None, None, None, None)
 
 
-# target workgroups of a split-K weight-gradient GEMM (512 measured best at N = 20000: 0.094 vs
-# 0.108 ms for 512x512x20000 at 1024, fewer fp32 slabs to add; profiles/r01_kbench_x3_sliced.txt)
-_DW_BLOCKS = int(os.environ.get("HICGAT_DW_BLOCKS", "512"))
+# target workgroups of a split-K weight-gradient GEMM.  Alone, 512 measured best at N = 20000 (0.094
+# vs 0.108 ms for 512x512x20000 at 1024, fewer fp32 slabs to add; profiles/r01_kbench_x3_sliced.txt);
+# in the step, where the big dW GEMMs run two at a time beside each other after the source pass,
+# 256 (half the slabs to add) is faster: 1.927 vs 1.942 ms per step, three A/B rounds
+# (profiles/r02d_ab_step.txt)
+_DW_BLOCKS = int(os.environ.get("HICGAT_DW_BLOCKS", "256"))
 
 
 def _splits(m, n, k, target=None):

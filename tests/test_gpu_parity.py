@@ -315,10 +315,10 @@ def test_tall_gemm_edges_and_accumulate(m, n, k):
 
 @pytest.mark.parametrize("m,n,k,splits", [(128, 128, 1001, 3), (512, 256, 17, 1), (256, 128, 20000, 1),
                                           (128, 384, 4099, 64), (512, 512, 20000, 32)])
-def test_wgrad_dma_ragged_strided(m, n, k, splits):
-    """The LDS-DMA weight-gradient kernel (gemm_wgrad.hip: M, N multiples of 128) on K not a multiple
-    of its 16-row stage and splits whose last stage is partial (rows past the split's end loaded and
-    zeroed), row-strided operands, with and without the bias column sums and accumulate, vs fp64."""
+def test_wgrad_ragged_strided(m, n, k, splits):
+    """The split-K weight-gradient GEMM (gemm.hip) on K not a multiple of its 16-row stage, splits
+    whose last stage is partial, row-strided operands, with and without the bias column sums and
+    accumulate, vs fp64."""
     import hicgat
     K = hicgat.kernels.default()
     torch.manual_seed(m + n + k + splits)
