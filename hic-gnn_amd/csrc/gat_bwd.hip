@@ -330,22 +330,32 @@ __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict
   }
 }
 
-// block = 64 output columns x 16 groups (1024 threads); group g adds partials b = g, g+16, ...;
-// the groups are combined in order through LDS (fixed order: bitwise reproducible).  Only
-// P*D / 64 blocks exist, so the partial range is cut 16 ways to keep each thread's chain of
-// dependent loads short (32 partials at nblk = 512).
-constexpr int kPG2Groups = 16;
+// block = 16 output columns x 16 groups (256 threads); group g adds partials b = g, g+16, ...;
+// the groups are combined in order through LDS (fixed order: bitwise reproducible).  The partial
+// range is cut 16 ways to keep each thread's chain of dependent loads short (32 partials at
+// nblk = 512); 256-thread blocks (P*D/16 of them) find room on CUs that the side stream's GEMMs
+// occupy, where 1024-thread blocks waited (25-43 us in the step instead of a few).
+constexpr int kPG2Groups = 16, kPG2Cols = 16;
 struct PGOut {
   float *o[3];
 };
-__global__ __launch_bounds__(1024) void param_grad_stage2(const float *__restrict__ part, int nblk,
-                                                          int P, int D, PGOut out, int accumulate) {
-  __shared__ float red[kPG2Groups][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+__global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict__ part, int nblk, int P, int D,
+                                                         PGOut out, int accumulate) {
+  __shared__ float red[kPG2Groups][kPG2Cols];
+  const int cl = threadIdx.x % kPG2Cols, grp = threadIdx.x / kPG2Cols;
+  const int c = blockIdx.x * kPG2Cols + cl;
   float s = 0.f;
   if (c < P * D) {
-    for (int b = grp; b < nblk; b += kPG2Groups) s += part[(size_t)b * P * D + c];
+    // all of this thread's partials (<= kParamBlocks / 16 = 32) in flight together, then added in order
+    constexpr int kMax = (kParamBlocks + kPG2Groups - 1) / kPG2Groups;
+    float v[kMax];
+#pragma unroll
+    for (int i = 0; i < kMax; ++i) {
+      const int b = grp + i * kPG2Groups;
+      v[i] = b < nblk ? part[(size_t)b * P * D + c] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kMax; ++i) s += v[i];
   }
   red[grp][cl] = s;
   __syncthreads();
@@ -501,8 +511,8 @@ extern "C" int hicgat_gat_param_grad(const float *h, const float *dout, const fl
 #undef HICGAT_PG1
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(param_grad_stage2, dim3((P * D + 63) / 64), dim3(64 * kPG2Groups), 0, s, part, nblk, P, D,
-                     out, accumulate);
+  hipLaunchKernelGGL(param_grad_stage2, dim3((P * D + kPG2Cols - 1) / kPG2Cols), dim3(kPG2Cols * kPG2Groups), 0, s,
+                     part, nblk, P, D, out, accumulate);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

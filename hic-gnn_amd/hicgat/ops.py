@@ -94,6 +94,11 @@ def side_flush(after=None):
         return
     if SIDE_ORDER == "size":
         queue.sort(key=lambda q: -q[2])
+    elif SIDE_ORDER == "small_first":
+        # the reductions without a GEMM (LayerNorm dgamma/dbeta, work 0) first: their inputs are
+        # ready before the gather starts, so they finish beside it instead of delaying the big dW
+        # GEMMs that run after it
+        queue.sort(key=lambda q: q[2] > 0)
     lanes = [queue]
     if SIDE_BIG > 0:
         # the big dW GEMMs on their own side stream: they start as the gather drains instead of
