@@ -645,7 +645,24 @@ class _FusedLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl):
         (dc,) = ctx.saved_tensors
+        if gl is _UNIT_SEEDS.get(gl.device):   # seeded by backward_from_loss: d(loss) = 1 exactly
+            return dc, None, None, None, None, None, None, None
         return dc * gl, None, None, None, None, None, None, None
+
+
+# loss.backward() fills a fresh ones tensor and the loss node then multiplies dcoords by it: two
+# launches per step.  backward_from_loss seeds with one resident ones tensor per device instead (never
+# written), which the loss node recognises by identity and skips the multiply -- the same bits.
+_UNIT_SEEDS = {}
+
+
+def backward_from_loss(loss):
+    """``loss.backward()`` for a scalar loss from ``fused_dist_loss``, without the seed fill and the
+    dcoords scaling launches."""
+    seed = _UNIT_SEEDS.get(loss.device)
+    if seed is None or seed.dtype != loss.dtype:
+        seed = _UNIT_SEEDS[loss.device] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    torch.autograd.backward(loss, grad_tensors=seed)
 
 
 def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):

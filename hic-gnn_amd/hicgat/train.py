@@ -28,7 +28,7 @@ def train_step(model, opt, x, edge_index, truth, kind="mse", stats=None):
     opt.zero_grad()
     loss, stats, coords = model.loss(x, edge_index, truth, kind, stats=stats)
     with ops.overlapped_param_grads(None if x.is_cuda else False):   # dW, db beside the backward
-        loss.backward()
+        ops.backward_from_loss(loss)
     opt.step()
     return loss, stats, coords
 
