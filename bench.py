@@ -48,6 +48,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6290
 L2_PEAK_GBS = 34500.0   # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)")
+MFMA_F32_TFS = 157.3    # dense fp32 MFMA peak, v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md)
 D_FEAT = 512
 HEADS = 2
 
@@ -396,6 +397,21 @@ def main():
                 "note": "achieved/frac: PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) per launch "
                         "/ avg launch time vs 8 TB/s; alg_GBps: SURVEY 8(d) no-reuse bytes (every edge reads a "
                         "whole neighbour row) / time, bounded by the L2 (l2_frac), not HBM"}
+        tiles = wl["adj"].tiles() if not sharded and dom == "gat_agg_fwd" else None
+        if tiles is not None:
+            # dense-tile form (a dense contact map): the tile edges are 32x32 . 32x512 products on the
+            # fp32 matrix cores, every neighbour row read once per 32 destination rows -- the no-reuse
+            # byte model does not apply; the bound is the MFMA rate.  FLOP per launch: two products
+            # (out and out2) per tile; the time is the whole call (remainder gather and epilogue too)
+            flop = tiles.ntiles * 2 * (2.0 * 32 * 32 * D_FEAT)
+            tfs = flop / (avg * 1e-3) / 1e12
+            roof.update({"bound": "mfma", "kernel": "gat_agg_fwd (dense-tile form, hicgat_gat_agg_fwd_tiled)",
+                         "achieved": tfs, "peak": MFMA_F32_TFS, "unit": "TFLOP/s", "frac": tfs / MFMA_F32_TFS,
+                         "traffic": None, "traffic_source": None, "flop_per_launch": flop,
+                         "dense_tiles": tiles.ntiles, "edges_in_tiles": tiles.n_dense, "l2_frac": None,
+                         "note": "dense-tile aggregation: achieved = tile MFMA FLOP (2 products x 2*32*32*512 per "
+                                 "tile) / avg time of the whole call (incl. the remainder gather and epilogue); "
+                                 "alg_GBps is the no-reuse byte model, which tiles (32-row reuse) do not follow"})
 
     result = {
         "metric": f"training steps/sec ({args.model}, fwd+loss+bwd+Adam)",
