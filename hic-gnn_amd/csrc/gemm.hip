@@ -531,11 +531,18 @@ static bool tall_enabled() {
   return on;
 }
 
+// HICGAT_TALL_MIN_TILES (A/B): problems with fewer 160x128 tiles than this go to the 64x128 kernel
+static int64_t tall_min_tiles() {
+  static const int64_t v = getenv("HICGAT_TALL_MIN_TILES") ? atoll(getenv("HICGAT_TALL_MIN_TILES")) : 0;
+  return v;
+}
+
 template <bool AK, bool BK_>
 static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
                     int K, int splits, const float *bias, float *slab, int acc, int impl, hipStream_t s) {
   // tall node-row problems (Linear forward, input gradient): the 160x128 LDS-DMA kernel (gemm_tall.hip)
-  if (!AK && impl == HICGAT_GEMM_F32 && splits == 1 && M >= 1024 && tall_enabled()) {
+  if (!AK && impl == HICGAT_GEMM_F32 && splits == 1 && M >= 1024 && tall_enabled() &&
+      (int64_t)((M + 159) / 160) * (N / 128) >= tall_min_tiles()) {
     const int rc = gemm_tall_launch(BK_, A, lda, B, ldb, C, ldc, M, N, K, bias, acc, s);
     if (rc != HICGAT_EUNSUPPORTED) return rc;
   }
