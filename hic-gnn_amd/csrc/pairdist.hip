@@ -205,23 +205,17 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       const f2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy,
                                               __builtin_elementwise_fma(dz, dz, f2{0x1.0p-100f, 0x1.0p-100f})));
       const f2 inv = f2{__builtin_amdgcn_rsqf(d2.x), __builtin_amdgcn_rsqf(d2.y)};
-      f2 w;
+      const f2 d = d2 * inv;
+      const f2 r = d - tv[h];
+      L2 = __builtin_elementwise_fma(r, r, L2);
       if (PEARSON) {
-        const f2 d = d2 * inv;
-        const f2 r = d - tv[h];
-        L2 = __builtin_elementwise_fma(r, r, L2);
         sd2 += d;
         sdd2 = __builtin_elementwise_fma(d, d, sdd2);
         sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
         st2 += tv[h];
         stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
-        w = r * inv;
-      } else {
-        // w = (d - t)/d = 1 - t/d and (d - t)^2 = w^2 d^2: three packed ops per pair pair instead of
-        // four (d, r, r^2, w), d never formed
-        w = __builtin_elementwise_fma(-tv[h], inv, f2{1.f, 1.f});
-        L2 = __builtin_elementwise_fma(w * w, d2, L2);
       }
+      const f2 w = r * inv;
       px = __builtin_elementwise_fma(w, dx, px);
       py = __builtin_elementwise_fma(w, dy, py);
       pz = __builtin_elementwise_fma(w, dz, pz);
