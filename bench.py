@@ -1,15 +1,23 @@
 """Benchmark: GAT-HiC training steps/sec on MI355X (BASELINE.json metric).
 
   python bench.py [--gpus N --steps K --warmup W] [--workload synth-20000|synth-2000]
-                  [--dist-mode allgather|replicate]
+                  [--dist-mode slab|allgather] [--simulate-world P]
 
 One step = zero_grad + GATConv (MFMA lin_l + fused logits, edge-softmax aggregation) + MLP tail
 + fused distance/MSE loss + backward + Adam, over the whole synthetic Hi-C graph, inputs resident
 in HBM, replayed as one captured hipGraph (``--eager``: kernel by kernel).
 
-N > 1: one rank per GPU over RCCL (hicgat.dist: destination rows sharded by an nnz prefix sum,
-RCCL all-gathers of the 512-d node embeddings; strong scaling -- the same N = 20000 graph is
-split, so ``value`` = whole-model steps per second).  Launched by the driver through
+N > 1: one rank per GPU over RCCL (hicgat.dist: destination rows sharded by an nnz prefix sum;
+"slab" form by default -- the 512-d embeddings gathered once, h recomputed per rank, the source
+pass split by destination owner, so no per-step collective above the 2.4 MB gradient buffer;
+``--dist-mode allgather``: the RCCL all-gather of h before the layer; strong scaling -- the same
+N = 20000 graph is split, so ``value`` = whole-model steps per second).
+
+``--simulate-world P`` (one GPU): runs each of the P ranks' shares of the sharded step in turn
+with the collectives left out (hicgat.dist.SimComm), graph-captured, and reports the per-rank
+step times (``simulated.rank_ms``) plus a step-time model = max over ranks + the modeled time of
+the collectives that are not overlapped (``simulated``; the xGMI / RCCL figures are stated
+assumptions, not measurements).  ``value`` is then that MODEL's steps/s and ``n_gpus`` is 1.  Launched by the driver through
 ``torch.distributed.run`` (RANK / WORLD_SIZE in the environment), or directly as
 ``python bench.py --gpus N``: then this script starts ``torch.distributed.run`` itself as a child
 process (before any GPU call) and exits with its code; it exits non-zero if fewer than N GPUs are
@@ -228,6 +236,84 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+# Modeled collectives of the sharded step (bench.py --simulate-world).  NOT measured here (the pool's
+# GPU boxes have one GPU): assumptions, stated in the JSON line.  RCCL on one MI355X node: 7 xGMI
+# links per GPU (MI355X_MICROARCH.md / SURVEY 5: ~153 GB/s each); a collective costs a latency
+# term plus bytes over the bus bandwidth it sustains.
+RCCL_LAT_US = 12.0         # small-message latency of one RCCL collective inside a captured graph
+RCCL_BUS_GBS = 300.0       # sustained bus bandwidth of an all-reduce / all-gather over 8 ranks
+
+
+def _coll_us(kind, nbytes, P):
+    """Time of one collective over P ranks: all_gather moves (P-1)/P of the buffer into each rank,
+    all_reduce 2 (P-1)/P of it (ring / tree bus-bandwidth convention)."""
+    f = (P - 1) / P * (2.0 if kind == "all_reduce" else 1.0)
+    return RCCL_LAT_US + f * nbytes / (RCCL_BUS_GBS * 1e3)
+
+
+def simulate_world(args):
+    """Per-rank compute of the P-rank sharded step on ONE GPU: each rank's share (its rows, edges,
+    slab, tiles and support rows) with the collectives left out, graph-captured, timed like the
+    real step; then the model: max over ranks + the collectives on the critical path."""
+    import hicgat
+    from hicgat import dist as hdist
+    P = args.simulate_world
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    wl = build_workload(args.workload, args.seed, dev)
+    rank_ms, rank_med, shards = [], [], []
+    truth = wl["truth"]
+    for r in range(P):
+        torch.manual_seed(0)
+        model = hicgat.MODELS[args.model]().to(dev)
+        tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], truth, lr=1e-3, kind=args.loss,
+                                  mode=args.dist_mode, comm=hdist.SimComm(P, r))
+        step = tr.captured(warmup=max(1, args.warmup))
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        evs[0].record()
+        for k in range(args.steps):
+            step()
+            evs[k + 1].record()
+        torch.cuda.synchronize()
+        per = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+        rank_ms.append(float(np.mean(per)))
+        rank_med.append(float(np.median(per)))
+        shards.append({"rows": tr.local_rows, "nnz": tr.local_nnz, "slab_nnz": getattr(tr, "slab_nnz", None),
+                       "tiles": tr.t1 - tr.t0, "support_rows": (tr.s1 - tr.s0) if tr.sf is not None else None})
+        log(f"[sim] P={P} rank {r}: {rank_ms[-1]:.4f} ms/step (median {rank_med[-1]:.4f}) {shards[-1]}")
+        del step, tr, model
+        torch.cuda.empty_cache()
+    n, D = wl["n"], D_FEAT
+    grad_bytes = 4 * 601475
+    R = max(s["rows"] for s in shards)
+    coll = {"coords_all_gather": _coll_us("all_gather", P * R * 3 * 4, P),
+            "loss_all_reduce": _coll_us("all_reduce", (7 + 3 * n) * 8, P),
+            # the tail's bucket runs on the comm stream beside lin_l's dW GEMM: only the GATConv's
+            # bucket (W 512x512 + att + bias) is on the critical path
+            "grad_all_reduce_gat_bucket": _coll_us("all_reduce", 4 * (512 * 512 + 3 * 512), P)}
+    if args.dist_mode == "allgather":
+        coll["h_all_gather"] = _coll_us("all_gather", P * R * D * 4, P)
+        coll["pack_all_gather"] = _coll_us("all_gather", P * R * (D + 8) * 4, P)
+    exposed_us = sum(coll.values())
+    model_ms = max(rank_ms) + exposed_us * 1e-3
+    result = {
+        "metric": f"training steps/sec ({args.model}, fwd+loss+bwd+Adam) -- MODELED {P}-GPU step",
+        "value": 1e3 / model_ms, "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": model_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
+        "config": {"workload": args.workload, "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz,
+                   "parallelism": f"dst-row shard x{P} ({args.dist_mode}), SIMULATED one rank at a time on 1 GPU"},
+        "simulated": {"world": P, "mode": args.dist_mode, "rank_ms": rank_ms, "rank_median_ms": rank_med,
+                      "shards": shards, "collectives_us": coll, "exposed_collectives_us": exposed_us,
+                      "model_ms_per_step": model_ms,
+                      "assumptions": {"rccl_latency_us": RCCL_LAT_US, "rccl_bus_GBps": RCCL_BUS_GBS,
+                                      "note": "rank_ms measured (graph replay of the rank's share, collectives "
+                                              "left out); collectives modeled, not measured (1-GPU box)"}},
+    }
+    print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,9 +325,11 @@ def main():
                     choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
                     help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
                          "N > 1 shards the GAT models only")
-    ap.add_argument("--dist-mode", default="allgather", choices=["allgather", "replicate"],
-                    help="N > 1: all-gather h each step (default) or replicate x and recompute h on every rank "
-                         "(the SURVEY 8(e) ablation)")
+    ap.add_argument("--dist-mode", default="slab", choices=["slab", "allgather"],
+                    help="N > 1: the slab form (default: x replicated, h recomputed per rank, source pass split by "
+                         "destination owner -- no h / dout all-gathers) or the all-gather of h before the layer")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="one GPU: time each rank's share of a P-rank sharded step, collectives left out")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
@@ -256,6 +344,8 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
+    if args.simulate_world:
+        return simulate_world(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -295,7 +385,7 @@ def main():
     if world > 1 or args.selftest_cpu:
         from hicgat import dist as hdist
         runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss, kern=kern,
-                                      replicate_x=args.dist_mode == "replicate")
+                                      mode=args.dist_mode)
         wl["truth"] = None                      # each rank keeps only its band (runner.tband)
         if dev.type == "cuda":
             torch.cuda.empty_cache()
@@ -441,7 +531,7 @@ def main():
         "kernels": kern_t,
     }
     if sharded:
-        result["shard"] = {"rows_per_rank": [int(v) for v in runner.plan.counts],
+        result["shard"] = {"mode": args.dist_mode, "rows_per_rank": [int(v) for v in runner.plan.counts],
                            "nnz_per_rank": [int(v) for v in runner.plan.nnz]}
     if graph_error is not None:
         result["graph_error"] = graph_error

@@ -406,7 +406,8 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
                                                                float *__restrict__ dcoords,
                                                                const double *__restrict__ mom, int64_t m0, int64_t m1,
                                                                int row_blocks, double *__restrict__ mpart,
-                                                               const float4 *__restrict__ corr) {
+                                                               const float4 *__restrict__ corr, int corr_r0,
+                                                               int corr_r1) {
   if (mom && (int)blockIdx.x >= row_blocks) {
     moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
     return;
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
       const float4 o = red[g][lr64];
       s0.x += o.x; s0.y += o.y; s0.z += o.z;
     }
-    if (corr) {
+    if (corr && gi >= corr_r0 && gi < corr_r1) {
       const float4 o = corr[gi];
       s0.x += o.x; s0.y += o.y; s0.z += o.z;
     }
@@ -538,6 +539,7 @@ __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__re
 // d is formed exactly as in the bulk's interior path.  Per-block moment records (fixed order).
 template <bool PEARSON>
 __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__restrict__ coords, int N, float bg,
+                                                               int row_begin, int row_end,
                                                                const int32_t *__restrict__ rowptr,
                                                                const int32_t *__restrict__ col,
                                                                const float *__restrict__ val,
@@ -545,10 +547,10 @@ __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__re
                                                                float4 *__restrict__ corr, double *__restrict__ mom) {
   __shared__ double mred[4][7];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = blockIdx.x * 4 + wv;
+  const int i = row_begin + blockIdx.x * 4 + wv;
   float gx = 0.f, gy = 0.f, gz = 0.f;
   double L = 0.0, sdt = 0.0, st = 0.0, stt = 0.0, dg = 0.0;   // the support's moment changes in fp64
-  if (i < N) {   // wave-uniform
+  if (i < row_end) {   // wave-uniform
     const float xi = coords[3 * (size_t)i], yi = coords[3 * (size_t)i + 1], zi = coords[3 * (size_t)i + 2];
     const int e1 = rowptr[i + 1];
     for (int e = rowptr[i] + lane; e < e1; e += 64) {
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__re
     gy += __shfl_xor(gy, o);
     gz += __shfl_xor(gz, o);
   }
-  if (i < N && lane == 0) corr[i] = make_float4(gx, gy, gz, 0.f);
+  if (i < row_end && lane == 0) corr[i] = make_float4(gx, gy, gz, 0.f);
   double m[7] = {L, 0.0, 0.0, sdt, st, stt, dg};
 #pragma unroll
   for (int c = 0; c < 7; ++c) {
@@ -690,7 +692,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
-                     dcoords, nullptr, (int64_t)0, (int64_t)0, 0, nullptr, nullptr);
+                     dcoords, nullptr, (int64_t)0, (int64_t)0, 0, nullptr, nullptr, 0, 0);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -746,7 +748,7 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   double *mpart = mom + (size_t)tiles * 8;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, (hipStream_t)stream, part,
                      1, N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end,
-                     row_blocks, mpart, nullptr);
+                     row_blocks, mpart, nullptr, 0, 0);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, N, loss_kind, stats,
                      loss);
@@ -783,45 +785,73 @@ extern "C" size_t hicgat_pairdist_support_workspace_bytes(int N) {
          kMomBlocks * 8 * sizeof(double) + (size_t)N * sizeof(float4) + 256;
 }
 
-extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background,
-                                                 const int32_t *rowptr, const int32_t *col, const float *val,
-                                                 const float *diag, int loss_kind, double *stats, float *loss,
-                                                 float *dcoords, void *workspace, size_t workspace_bytes,
-                                                 hicgat_stream_t stream) {
+extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background,
+                                                       const int32_t *rowptr, const int32_t *col, const float *val,
+                                                       const float *diag, int64_t tile_begin, int64_t tile_end,
+                                                       int support_row_begin, int support_row_end, int loss_kind,
+                                                       double *stats, float *loss, float *dcoords, void *workspace,
+                                                       size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !rowptr || !col || !val || !diag || !stats || !workspace) return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_pairdist_support_workspace_bytes(N)) return HICGAT_EINVAL;
   const int nb = pd_nb(N);
-  const int64_t tiles = (int64_t)nb * (nb + 1) / 2, sblocks = pd_support_blocks(N);
+  const int64_t tiles = (int64_t)nb * (nb + 1) / 2;
+  if (tile_end < 0 || tile_end > tiles) tile_end = tiles;
+  if (tile_begin < 0) tile_begin = 0;
+  if (tile_begin > tile_end) return HICGAT_EINVAL;
+  if (support_row_end < 0 || support_row_end > N) support_row_end = N;
+  if (support_row_begin < 0) support_row_begin = 0;
+  if (support_row_begin > support_row_end) return HICGAT_EINVAL;
+  const int64_t nt = tile_end - tile_begin;
+  const int64_t sblocks = (support_row_end - support_row_begin + 3) / 4;
   char *p = static_cast<char *>(workspace);
   float4 *part = reinterpret_cast<float4 *>(p);
+  // moment records: tiles [tile_begin, tile_end) at their tile index, the support blocks right
+  // after tile_end (so [tile_begin, tile_end + sblocks) is one contiguous run; the workspace holds
+  // tiles + pd_support_blocks(N) records, and tile_end + sblocks never exceeds that)
   double *mom = reinterpret_cast<double *>(p + (size_t)tiles * 2 * BT * sizeof(float4));
-  double *mpart = mom + (size_t)(tiles + sblocks) * 8;
+  double *mpart = mom + (size_t)(tiles + pd_support_blocks(N)) * 8;
   float4 *corr = reinterpret_cast<float4 *>(mpart + kMomBlocks * 8);
   hipStream_t s = (hipStream_t)stream;
-  // bulk: every pair i < j at the background value (no T read); support: the entries that differ
-  if (loss_kind == 1)
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(tiles), dim3(256), 0, s, coords,
-                       nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, background);
-  else
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true>), dim3(tiles), dim3(256), 0, s, coords,
-                       nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, background);
-  HICGAT_CHECK_LAUNCH();
-  if (loss_kind == 1)
-    hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background, rowptr,
-                       col, val, diag, corr, mom + (size_t)tiles * 8);
-  else
-    hipLaunchKernelGGL(pairdist_support_kernel<false>, dim3(sblocks), dim3(256), 0, s, coords, N, background, rowptr,
-                       col, val, diag, corr, mom + (size_t)tiles * 8);
-  HICGAT_CHECK_LAUNCH();
+  // bulk: every pair i < j of the tile range at the background value (no T read); support: the
+  // entries of rows [support_row_begin, support_row_end) that differ, and those rows' diagonal
+  if (nt > 0) {
+    if (loss_kind == 1)
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(nt), dim3(256), 0, s, coords,
+                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background);
+    else
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true>), dim3(nt), dim3(256), 0, s, coords,
+                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background);
+    HICGAT_CHECK_LAUNCH();
+  }
+  if (sblocks > 0) {
+    if (loss_kind == 1)
+      hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
+                         support_row_begin, support_row_end, rowptr, col, val, diag, corr,
+                         mom + (size_t)tile_end * 8);
+    else
+      hipLaunchKernelGGL(pairdist_support_kernel<false>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
+                         support_row_begin, support_row_end, rowptr, col, val, diag, corr,
+                         mom + (size_t)tile_end * 8);
+    HICGAT_CHECK_LAUNCH();
+  }
   const float scale = (float)(4.0 / ((double)N * (double)N));
   const int row_blocks = dcoords ? (N + 63) / 64 : 0;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
-                     (int)MODE_SYM, (int64_t)0, tiles, scale, dcoords, mom, (int64_t)0, tiles + sblocks, row_blocks,
-                     mpart, corr);
+                     (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
+                     row_blocks, mpart, corr, support_row_begin, support_row_end);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background,
+                                                 const int32_t *rowptr, const int32_t *col, const float *val,
+                                                 const float *diag, int loss_kind, double *stats, float *loss,
+                                                 float *dcoords, void *workspace, size_t workspace_bytes,
+                                                 hicgat_stream_t stream) {
+  return hicgat_pairdist_mse_fused_support_range(coords, N, background, rowptr, col, val, diag, 0, -1, 0, N,
+                                                 loss_kind, stats, loss, dcoords, workspace, workspace_bytes, stream);
 }

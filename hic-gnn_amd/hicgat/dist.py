@@ -4,35 +4,45 @@ BASELINE.json north star: "partition across the 8 GPUs of one node by sharding d
 with an RCCL all-gather of the 512-d node embeddings"; SURVEY.md section 8(e).  The reference is
 single-process (no collectives anywhere), so every exchange below is new.
 
-Partition (``ShardPlan``):
-  * destination rows in P contiguous blocks balanced by nnz -- bounds from a prefix sum over
-    rowptr (the CSR's own rowptr IS that prefix sum), so a dense Hi-C band and a sparse tail get
-    the same edge count per rank;
-  * every node buffer is [P*R, .] with R = the largest block: rank p's rows sit at buffer rows
-    p*R .. p*R + n_p - 1 (padding after them), so each all-gather is one in-place equal-chunk
-    ``all_gather_into_tensor``.  Global row g lives at buffer row ``gidx[g]``;
-  * each rank holds ONLY its rows of the graph (a padded rowptr whose other rows are empty, its
-    edges with columns remapped to buffer rows), its rows of x, and the band of the truth its
-    share of the upper-triangle loss tiles reads (tile-rows I0..I1, columns from I0*128 on).
+Partition (``ShardPlan``): destination rows in P contiguous blocks balanced by nnz (the CSR's own
+rowptr is the prefix sum), every rank keeping at least one row; the upper-triangle loss tiles in P
+contiguous ranges; the loss's support rows (the contact set of cont2dist's target) in P blocks
+balanced by support nnz.
 
-Per step:
-  forward:  h_p = x_p W^T (MFMA) into its buffer rows -> all_gather(h) [P*R, 512]
-            (``replicate_x=True``: the SURVEY 8(e) ablation -- every rank holds all of x and
-            computes h for every row, no all-gather of h)
-            logits for all rows from the gathered h; aggregation (+ relu, out2, S3) of own rows;
-            MLP tail on own rows -> all_gather(coords) -> global order (one index_select)
-            fused distance/MSE over this rank's tile range of its truth band
-            one fp64 all_reduce of [loss moments | dcoords]; finalize the loss
-  backward: tail backward on own rows -> GAT bwd rows pass (relu backward, delta, da_dst; no
-            gather) -> one all_gather of packed rows [dout (512) | row stats (max, sum, delta,
-            da_dst)] -> GAT source pass on own rows (dh complete: a row's CSR list is every row
-            that lists it, the graph is symmetric) -> dW_p = dh_p^T x_p, datt / dbias partials
-            -> all_reduce(one flat fp32 grad buffer) -> identical Adam on every rank.
-Strong scaling: the step is the same whole-graph step as on one GPU; results equal the 1-GPU
-step up to the summation order of the all-reduces (tests/test_dist_gloo.py).
+Two step forms (``mode``):
 
-The trainer only talks to a kernel object (``hicgat.kernels.HipKernels`` in production), so the
-partitioning and collectives are testable on CPU with gloo and a torch stand-in.
+``"slab"`` (default) -- no per-step collective larger than the 2.4 MB gradient buffer.  The 512-d
+  node embeddings x are constant, so they are all-gathered ONCE (every rank holds all of x, 41 MB)
+  and each rank recomputes h = x W^T for every row (10.5 GFLOP, ~0.1 ms) instead of all-gathering
+  h every step.  The backward's source side is split by DESTINATION owner instead of by source
+  row: rank p runs the source pass over every row r but only over the neighbours i it owns (the
+  "column slab" of the symmetric CSR: nnz/P entries), which needs only its own dout_i / row stats,
+  so the [dout | stats] all-gather disappears too.  That yields a partial dh_r and da_src_r for
+  every r; lin_l's dW = sum_r dh_r x_r^T and datt_src = sum_r da_src_r h_r are linear in them, so
+  each rank forms its partial dW over all rows (x is replicated) and the ordinary gradient
+  all-reduce sums the partials.  Per step: all-gather of coords (N x 3), one fp64 all-reduce of
+  [loss moments | dcoords], the gradient all-reduce in two buckets -- the MLP tail's (ready when
+  the side stream's dW GEMMs finish, reduced on a comm stream beside lin_l's dW GEMM) and the
+  GATConv's -- and identical Adam on every rank.
+``"allgather"`` -- the north star's literal form: each rank computes h for its rows, RCCL
+  all-gather of h [N, 512] before the layer; after the backward's row pass one all-gather of packed
+  rows [dout | row stats] so each rank's source pass covers its own rows r completely (its dW is
+  over its rows only).  The tail's dW GEMMs run on the side stream beside that all-gather and the
+  source pass.
+
+Loss (both forms): the truth in background + support form (``graph.SupportForm``, cont2dist's
+target: background 1 off the contact set), so the O(N^2) pass streams no truth: rank p takes the
+bulk over its tile range and the support rows of its block (``hicgat_pairdist_mse_fused_support_range``),
+and the fp64 all-reduce sums the partial moments and dcoords.  A truth without a support form
+falls back to the dense band of the rank's tile range.
+
+Strong scaling: the step is the same whole-graph step as on one GPU; results equal the 1-GPU step
+up to the summation order of the partial sums (tests/test_dist_gloo.py, world 1 / 2 / 3).
+
+The trainer talks to a kernel object (``hicgat.kernels.HipKernels`` in production) and a comm
+object (``DistComm`` over torch.distributed; ``SimComm`` runs ONE rank's share with the collectives
+left out, for the per-rank compute measurement of bench.py --simulate-world), so the partitioning
+and collectives are testable on CPU with gloo and a torch stand-in.
 """
 import numpy as np
 import torch
@@ -43,11 +53,14 @@ from .ops import _ACTS, weight_grad
 from .optim import FlatAdam
 
 TILE = 128
+MODES = ("slab", "allgather")
 
 
 def partition_rows(rowptr, P):
-    """Contiguous destination-row blocks with ~nnz/P CSR entries each: bounds [P+1], block p =
-    rows [bounds[p], bounds[p+1]).  Boundary p is the row whose CSR start is nearest p*nnz/P."""
+    """Contiguous row blocks with ~nnz/P CSR entries each: bounds [P+1], block p = rows
+    [bounds[p], bounds[p+1]).  Boundary p is the row whose CSR start is nearest p*nnz/P, clamped so
+    that every block keeps at least one row when N >= P (a hub row holding more than nnz/P entries
+    would otherwise put two cuts on the same row)."""
     rp = np.asarray(rowptr, dtype=np.int64)
     N = rp.shape[0] - 1
     nnz = int(rp[-1])
@@ -58,7 +71,9 @@ def partition_rows(rowptr, P):
         r = int(np.searchsorted(rp, t, side="left"))     # first row whose start reaches t
         if r > 0 and (t - rp[r - 1]) < (rp[min(r, N)] - t):
             r -= 1
-        b[p] = min(max(r, b[p - 1]), N)
+        lo = b[p - 1] + (1 if N >= P else 0)
+        hi = N - (P - p) if N >= P else N
+        b[p] = min(max(r, lo), hi)
     return b
 
 
@@ -81,29 +96,37 @@ def tri_row(t, nb):
 class ShardPlan:
     """The static partition of a set_diag'd symmetric CSR (host int arrays) over P ranks."""
 
-    def __init__(self, rowptr, col, P):
+    def __init__(self, rowptr, col, P, support_rowptr=None):
         rp = np.asarray(rowptr, dtype=np.int64)
         self.col = np.asarray(col, dtype=np.int64)
         self.rp = rp
         self.P = P
         self.N = N = rp.shape[0] - 1
+        if N < P:
+            raise ValueError(f"cannot shard {N} rows over {P} ranks: every rank needs at least one row")
         self.bounds = partition_rows(rp, P)
         self.counts = np.diff(self.bounds)
         self.R = R = max(1, int(self.counts.max()))
         owner = np.repeat(np.arange(P, dtype=np.int64), self.counts)
+        self.owner = owner
         self.gidx = owner * R + (np.arange(N, dtype=np.int64) - self.bounds[owner])
         self.nnz = np.array([rp[self.bounds[p + 1]] - rp[self.bounds[p]] for p in range(P)], dtype=np.int64)
         nb = (N + TILE - 1) // TILE
         self.tiles = nb * (nb + 1) // 2
         self.nb = nb
+        self.sbounds = None
+        if support_rowptr is not None:
+            srp = np.asarray(support_rowptr, dtype=np.int64)
+            self.sbounds = partition_rows(srp, P)
+            self.snnz = np.array([srp[self.sbounds[p + 1]] - srp[self.sbounds[p]] for p in range(P)], dtype=np.int64)
 
     def rows(self, rank):
         """(global first row, global end row, first buffer row)."""
         return int(self.bounds[rank]), int(self.bounds[rank + 1]), rank * self.R
 
     def local_csr(self, rank):
-        """Padded rowptr [P*R + 1] (only this rank's buffer rows have edges) and its columns
-        remapped to buffer rows (int32)."""
+        """"allgather" form: padded rowptr [P*R + 1] (only this rank's buffer rows have edges) and
+        its columns remapped to buffer rows (int32)."""
         r0, r1, q0 = self.rows(rank)
         e0, e1 = int(self.rp[r0]), int(self.rp[r1])
         rp = np.empty(self.P * self.R + 1, dtype=np.int64)
@@ -112,12 +135,39 @@ class ShardPlan:
         rp[q0 + (r1 - r0):] = e1 - e0
         return rp.astype(np.int32), self.gidx[self.col[e0:e1]].astype(np.int32)
 
+    def own_csr(self, rank):
+        """"slab" form, forward: rowptr [N + 1] in global numbering in which only this rank's rows
+        have entries, and their (global) columns."""
+        r0, r1, _ = self.rows(rank)
+        e0, e1 = int(self.rp[r0]), int(self.rp[r1])
+        rp = np.empty(self.N + 1, dtype=np.int64)
+        rp[:r0 + 1] = 0
+        rp[r0:r1 + 1] = self.rp[r0:r1 + 1] - e0
+        rp[r1:] = e1 - e0
+        return rp.astype(np.int32), self.col[e0:e1].astype(np.int32)
+
+    def slab_csr(self, rank):
+        """"slab" form, backward source pass: for EVERY row r, the neighbours i of r that this rank
+        owns (columns in [r0, r1)), sorted -- rowptr [N + 1], col (global).  Over the ranks the slabs
+        partition the CSR's entries (the graph is symmetric: i lists r iff r lists i)."""
+        r0, r1, _ = self.rows(rank)
+        keep = (self.col >= r0) & (self.col < r1)
+        row_of = np.repeat(np.arange(self.N, dtype=np.int64), np.diff(self.rp))
+        per_row = np.bincount(row_of[keep], minlength=self.N)
+        rp = np.zeros(self.N + 1, dtype=np.int64)
+        np.cumsum(per_row, out=rp[1:])
+        return rp.astype(np.int32), self.col[keep].astype(np.int32)
+
     def tile_range(self, rank):
         """This rank's contiguous share of the upper-triangle loss tiles."""
         return self.tiles * rank // self.P, self.tiles * (rank + 1) // self.P
 
+    def support_rows(self, rank):
+        """This rank's block of the truth's support rows (balanced by support entries)."""
+        return int(self.sbounds[rank]), int(self.sbounds[rank + 1])
+
     def truth_band(self, rank):
-        """(row0, row1, col0): the truth rows / first column the rank's tile range reads."""
+        """(row0, row1, col0): the truth rows / first column the rank's tile range reads (dense form)."""
         t0, t1 = self.tile_range(rank)
         if t1 <= t0:
             return 0, 0, 0
@@ -125,84 +175,146 @@ class ShardPlan:
         return I0 * TILE, min(self.N, (I1 + 1) * TILE), I0 * TILE
 
 
-def _all_gather_inplace(buf, own, group):
-    """All-gather where this rank's input ``own`` is its own chunk of ``buf`` (RCCL in place)."""
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(buf, own, group=group)
-    else:
-        dist.all_gather(list(buf.chunk(dist.get_world_size(group))), own.clone(), group=group)
+class DistComm:
+    """Collectives over a torch.distributed group (RCCL = backend "nccl" on ROCm, or gloo)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.P = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+
+    def all_gather_inplace(self, buf, own):
+        """All-gather where this rank's input ``own`` is its own chunk of ``buf`` (RCCL in place)."""
+        if self.nccl:
+            dist.all_gather_into_tensor(buf, own, group=self.group)
+        else:
+            dist.all_gather(list(buf.chunk(self.P)), own.clone(), group=self.group)
+
+    def all_reduce(self, t):
+        dist.all_reduce(t, group=self.group)
+
+    def all_gather_list(self, out, t):
+        dist.all_gather(out, t, group=self.group)
+
+
+class SimComm:
+    """ONE rank of a P-rank job with the collectives left out (bench.py --simulate-world): the
+    rank's kernels run exactly as in the real step, on its real shard, so their time is the
+    per-rank compute of a P-GPU step; the buffers the collectives would fill keep their contents."""
+
+    def __init__(self, P, rank):
+        self.P, self.rank, self.nccl, self.group = P, rank, True, None
+
+    def all_gather_inplace(self, buf, own):
+        pass
+
+    def all_reduce(self, t):
+        pass
 
 
 class ShardedTrainer:
-    def __init__(self, model, x, adj, truth, lr=1e-3, kind="mse", group=None, kern=None, replicate_x=False):
+    def __init__(self, model, x, adj, truth, lr=1e-3, kind="mse", group=None, kern=None, mode="slab", comm=None):
         if kern is None:
             from .kernels import default
             kern = default()
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
         self.K = kern
         self.model = model
+        self.comm = comm if comm is not None else DistComm(group)
         self.group = group
-        self.P = P = dist.get_world_size(group)
-        self.rank = rank = dist.get_rank(group)
+        self.P = P = self.comm.P
+        self.rank = rank = self.comm.rank
         self.kind = {"mse": 0, "combined": 1}[kind]
-        self.replicate_x = bool(replicate_x)
+        self.mode = mode
         dev = model.conv.lin_l.weight.device
+        self.cuda = dev.type == "cuda"
         N = x.shape[0]
         self.N = N
-        plan = ShardPlan(adj.rowptr32.cpu().numpy(), adj.col32.cpu().numpy(), P)
+        sf = truth.support
+        if sf is None and not truth.buf.is_cuda:
+            from .graph import SupportForm
+            sf = SupportForm.build_host(truth, 1.0)
+        self.sf = sf
+        plan = ShardPlan(adj.rowptr32.cpu().numpy(), adj.col32.cpu().numpy(), P,
+                         support_rowptr=None if sf is None else sf.rowptr.cpu().numpy())
         self.plan = plan
         R = plan.R
         self.R = R
         self.r0, self.r1, self.q0 = plan.rows(rank)
         self.local_rows = self.r1 - self.r0
         self.q1 = self.q0 + self.local_rows
-        if self.local_rows == 0:
-            raise ValueError(f"rank {rank} owns no rows (P = {P} > rows)")
-        rp, cl = plan.local_csr(rank)
-        self.rowptr = torch.from_numpy(rp).to(dev)
-        self.col = torch.from_numpy(cl).to(dev)
-        self.local_nnz = int(cl.shape[0])
+        self.local_nnz = int(plan.nnz[rank])
         self.gidx = torch.from_numpy(plan.gidx).to(dev)
         conv = model.conv
         self.W, self.att_l, self.att_r, self.bias = conv.lin_l.weight, conv.att_l, conv.att_r, conv.bias
         self.ns = conv.negative_slope
         self.H = conv.heads
         self.D = D = conv.heads * conv.out_channels
-        F = x.shape[1]
         f32 = dict(dtype=torch.float32, device=dev)
         self.x_loc = x[self.r0:self.r1].to(dev).contiguous().float()
-        if self.replicate_x:
-            self.x_pad = torch.zeros((P * R, F), **f32)
-            self.x_pad[self.gidx] = x.to(dev).float()
-        # the truth band of this rank's loss tiles (the full matrix is not kept)
+        # ---- the loss share: bulk tiles [t0, t1) + support rows [s0, s1) (or the dense band) ----
         self.t0, self.t1 = plan.tile_range(rank)
-        b0, b1, c0 = plan.truth_band(rank)
-        self.trow0, self.tcol0 = b0, c0
-        self.tband = truth.buf[b0:b1, c0:].contiguous() if b1 > b0 else torch.zeros((1, 4), **f32)
-        # every [P*R, .] buffer: rank p's rows are the p-th R-row chunk (in-place all-gathers)
-        self.h = torch.zeros((P * R, D), **f32)
-        self.out = torch.zeros((P * R, D), **f32)
-        self.out2 = torch.zeros((P * R, D), **f32)
-        self.gbuf = torch.zeros((P * R, D), **f32)
+        if sf is not None:
+            self.s0, self.s1 = plan.support_rows(rank)
+            self.tband = None
+        else:
+            b0, b1, c0 = plan.truth_band(rank)
+            self.trow0, self.tcol0 = b0, c0
+            self.tband = truth.buf[b0:b1, c0:].contiguous() if b1 > b0 else torch.zeros((1, 4), **f32)
+        # ---- graph and node buffers ---------------------------------------------------------------
+        if mode == "slab":
+            rp, cl = plan.own_csr(rank)
+            self.rowptr, self.col = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
+            rp, cl = plan.slab_csr(rank)
+            self.rowptr_s, self.col_s = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
+            self.slab_nnz = int(cl.shape[0])
+            self.x = x.to(dev).contiguous().float()          # the embeddings, gathered once (constant)
+            rows = N                                          # node buffers in global row order
+            self.a0, self.a1 = self.r0, self.r1               # own rows in buffer numbering
+        else:
+            rp, cl = plan.local_csr(rank)
+            self.rowptr, self.col = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
+            rows = P * R                                      # rank p's rows = the p-th R-row chunk
+            self.a0, self.a1 = self.q0, self.q1
+        self.h = torch.zeros((rows, D), **f32)
+        self.out = torch.zeros((rows, D), **f32)
+        self.out2 = torch.zeros((rows, D), **f32)
+        self.gbuf = torch.zeros((rows, D), **f32)
         self.act = _ACTS[getattr(model, "conv_act", None)]
-        # packed rows [dout (D) | row stats (4H)]: one all-gather carries both to the source pass
-        self.pack = torch.zeros((P * R, D + 4 * self.H), **f32)
-        self.dh = torch.zeros((P * R, D), **f32)
-        self.da_src = torch.zeros((P * R, self.H), **f32)
-        self.rs = torch.zeros((P * R, 4 * self.H), **f32)
+        # packed rows [dout (D) | row stats (4H)] (the "allgather" form all-gathers them as one buffer)
+        self.pack = torch.zeros((rows, D + 4 * self.H), **f32)
+        self.dh = torch.zeros((rows, D), **f32)
+        self.da_src = torch.zeros((rows, self.H), **f32)
+        # row stats; rows this rank does not own stay 0 forever (the slab source pass reads row r's
+        # da_dst for every r: 0 there, so only the owner adds da_dst_r * att_dst into dh_r)
+        self.rs = torch.zeros((rows, 4 * self.H), **f32)
         self.coords_buf = torch.zeros((P * R, 3), **f32)
+        if isinstance(self.comm, SimComm):
+            # the other ranks' coordinates, which the all-gather would bring: any spread-out values
+            g = torch.Generator().manual_seed(rank)
+            self.coords_buf.copy_(torch.randn((P * R, 3), generator=g))
         self.dcoords = torch.zeros((N, 3), **f32)
         # one fp64 all-reduce for the loss moments (7) and dcoords (3N)
         self.red = torch.zeros(7 + 3 * N, dtype=torch.float64, device=dev)
         self.stats = torch.zeros(12, dtype=torch.float64, device=dev)
         self.loss = torch.zeros((), **f32)
         self.opt = FlatAdam(model.flat_parameters(), lr=lr, kern=kern)
+        # gradient buckets: the GATConv's parameters lead the flat buffer (flat_parameters order)
+        conv_ids = {id(p) for p in (self.W, self.att_l, self.att_r, self.bias) if p is not None}
+        ends = [o + p.numel() for p, o in zip(self.opt.params, self.opt.offsets) if id(p) in conv_ids]
+        firsts = [o for p, o in zip(self.opt.params, self.opt.offsets) if id(p) not in conv_ids]
+        cut = (max(ends) + 3) // 4 * 4
+        self.grad_split = cut if (firsts and min(firsts) >= cut) else None
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
         per step removes the ~70 host launches that would otherwise bound a small per-rank shard.
         The ``warmup`` eager steps are real training steps."""
         from .graphs import CapturedStep
-        if dist.get_backend(self.group) != "nccl":
+        if not self.comm.nccl:
             raise RuntimeError("graph capture of the sharded step needs the nccl (RCCL) backend")
         if getattr(self.opt, "step_ctr", None) is None:
             self.opt.enable_device_step()
@@ -211,36 +323,125 @@ class ShardedTrainer:
     def _own(self, buf):
         return buf[self.q0:self.q0 + self.R]
 
-    def step(self):
-        K, g, q0, q1, N, D = self.K, self.group, self.q0, self.q1, self.N, self.D
-        self.opt.zero_grad()
-        self.model.train()
-        W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
-        # ---- forward ------------------------------------------------------------------------
-        if self.replicate_x:
-            _, a_src, a_dst = K.linear_att(self.x_pad, W, al, ar, h=self.h)
+    def _loss(self, coords):
+        K, N = self.K, self.N
+        if self.sf is not None:
+            K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
+                                       self.loss, self.dcoords)
         else:
-            K.linear_att(self.x_loc, W, al, ar, h=self.h[q0:q1])
-            _all_gather_inplace(self.h, self._own(self.h), g)
-            a_src, a_dst = K.att_logits(self.h, al, ar)
-        K.agg_fwd_act(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.act,
-                      self.out, self.out2, self.rs)
-        o = self.out[q0:q1].detach().requires_grad_(True)
-        coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
-        self.coords_buf[q0:q1].copy_(coords_loc.detach())
-        _all_gather_inplace(self.coords_buf, self._own(self.coords_buf), g)
-        coords = self.coords_buf.index_select(0, self.gidx)
-        K.fused_loss(coords, self.tband, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords,
-                     row0=self.trow0, col0=self.tcol0)
+            K.fused_loss(coords, self.tband, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords,
+                         row0=self.trow0, col0=self.tcol0)
         self.red[:7].copy_(self.stats[:7])
         self.red[7:].copy_(self.dcoords.view(-1))
-        dist.all_reduce(self.red, group=g)
+        self.comm.all_reduce(self.red)
         self.stats[:7].copy_(self.red[:7])
         self.dcoords.view(-1).copy_(self.red[7:])
         K.loss_finalize(N, self.kind, self.stats, self.loss)
+
+    def _tail(self):
+        """Tail forward on own rows, the coords all-gather, the loss share and its all-reduce."""
+        a0, a1 = self.a0, self.a1
+        o = self.out[a0:a1].detach().requires_grad_(True)
+        coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
+        self.coords_buf[self.q0:self.q1].copy_(coords_loc.detach())
+        self.comm.all_gather_inplace(self.coords_buf, self._own(self.coords_buf))
+        coords = self.coords_buf.index_select(0, self.gidx)
+        self._loss(coords)
+        return o, coords_loc, coords
+
+    def step(self):
+        self.opt.zero_grad()
+        self.model.train()
+        if self.mode == "slab":
+            coords, tail_done = self._step_slab()
+        else:
+            coords, tail_done = self._step_allgather()
+        self._grad_allreduce(tail_done)
+        self.opt.step()
+        return self.loss, self.stats, coords
+
+    def _grad_allreduce(self, tail_done):
+        """The flat gradient all-reduce in two buckets: the MLP tail's (on the comm stream, after
+        ``tail_done`` -- an event on the side stream after the tail's dW GEMMs, so it runs beside
+        lin_l's dW GEMM) and the GATConv's; the optimizer's stream waits for both."""
+        g, cut = self.opt.grad, self.grad_split
+        if cut is None:
+            self.comm.all_reduce(g)
+            return
+        if self.cuda:
+            cs = self.comm_stream
+            if tail_done:
+                for ev in tail_done:
+                    cs.wait_event(ev)
+            else:                       # no side stream in use: the tail's gradients are on this one
+                cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                self.comm.all_reduce(g[cut:])
+            self.comm.all_reduce(g[:cut])
+            torch.cuda.current_stream().wait_stream(cs)
+        else:
+            self.comm.all_reduce(g[cut:])
+            self.comm.all_reduce(g[:cut])
+
+    def _side_event(self):
+        """Events after the side streams' queued work (the tail's dW GEMMs), or None (CPU)."""
+        return ops.side_record() if self.cuda else None
+
+    def _step_slab(self):
+        K, N, D, H = self.K, self.N, self.D, self.H
+        r0, r1 = self.r0, self.r1
+        W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
+        bias = self.bias.detach()
+        # ---- forward: h and the logits for every row (x replicated), aggregation of own rows ------
+        _, a_src, a_dst = K.linear_att(self.x, W, al, ar, h=self.h)
+        K.agg_fwd_act(self.rowptr, self.col, r0, r1, self.h, a_src, a_dst, bias, self.ns, self.act,
+                      self.out, self.out2, self.rs)
+        o, coords_loc, coords = self._tail()
         # ---- backward -----------------------------------------------------------------------
-        # parameter gradients on the side stream from here to the gradient all-reduce (ops.py)
-        with ops.overlapped_param_grads(self.x_loc.is_cuda and ops.OVERLAP_DEFAULT):
+        tail_done = None
+        dout = self.pack[:, :D]
+        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
+            coords_loc.backward(self.dcoords[r0:r1])
+            self.gbuf[r0:r1].copy_(o.grad)
+            K.agg_bwd_rows(r0, r1, self.act, self.gbuf, self.out, bias, self.out2, dout, self.rs)
+            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the source pass
+            if not self.act:
+                dout[r0:r1].copy_(self.gbuf[r0:r1])
+            # source pass over every row r, restricted to the neighbours this rank owns: partial
+            # dh_r / da_src_r (complete when summed over ranks -- through dW and datt below)
+            K.agg_bwd_src(self.rowptr_s, self.col_s, 0, N, self.h, a_src, a_dst, self.rs, dout, al, ar, self.ns,
+                          self.dh, self.da_src)
+            ops.side_flush(after=fork)
+            tail_done = self._side_event()
+            with torch.no_grad():
+                # lin_l's partial dW over all rows (x replicated) on the side stream, the GAT
+                # parameter column sums beside it on this stream
+                with ops._side(self.dh, self.x):
+                    if self.cuda:
+                        weight_grad(K, self.dh, self.x, out=self.W.grad, accumulate=True)
+                    else:
+                        self.W.grad.addmm_(self.dh.t(), self.x)
+            dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
+            K.param_grad(self.h, None, self.da_src, None, H, out=(self.att_l.grad.view(-1), None, None),
+                         accumulate=True)
+            K.param_grad(self.h[r0:r1], dout[r0:r1].contiguous(), None, self.rs[r0:r1], H,
+                         out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
+        return coords, tail_done
+
+    def _step_allgather(self):
+        K, D = self.K, self.D
+        q0, q1 = self.q0, self.q1
+        W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
+        # ---- forward ------------------------------------------------------------------------
+        K.linear_att(self.x_loc, W, al, ar, h=self.h[q0:q1])
+        self.comm.all_gather_inplace(self.h, self._own(self.h))
+        a_src, a_dst = K.att_logits(self.h, al, ar)
+        K.agg_fwd_act(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.act,
+                      self.out, self.out2, self.rs)
+        o, coords_loc, coords = self._tail()
+        # ---- backward -----------------------------------------------------------------------
+        tail_done = None
+        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
             coords_loc.backward(self.dcoords[self.r0:self.r1])
             dout, rs_all = self.pack[:, :D], self.pack[:, D:]
             self.gbuf[q0:q1].copy_(o.grad)
@@ -250,21 +451,21 @@ class ShardedTrainer:
             if not self.act:
                 dout[q0:q1].copy_(self.gbuf[q0:q1])
             rs_all[q0:q1].copy_(self.rs[q0:q1])
-            _all_gather_inplace(self.pack, self._own(self.pack), g)
+            self.comm.all_gather_inplace(self.pack, self._own(self.pack))
             K.agg_bwd_src(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, rs_all, dout, al, ar, self.ns,
                           self.dh, self.da_src)
             ops.side_flush(after=fork)
+            tail_done = self._side_event()
             dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
             with torch.no_grad():
                 # lin_l's dW on the side stream (joined before the gradient all-reduce), param_grad
                 # beside it on this stream
                 with ops._side(self.dh, self.x_loc):
-                    if self.x_loc.is_cuda:
+                    if self.cuda:
                         weight_grad(K, self.dh[q0:q1], self.x_loc, out=self.W.grad, accumulate=True)
                     else:
                         self.W.grad.addmm_(self.dh[q0:q1].t(), self.x_loc)
             K.param_grad(self.h[q0:q1], dout[q0:q1].contiguous(), self.da_src[q0:q1], self.rs[q0:q1], self.H,
                          out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)
-        dist.all_reduce(self.opt.grad, group=g)
-        self.opt.step()
-        return self.loss, self.stats, coords
+        return coords, tail_done
+

@@ -358,6 +358,22 @@ class SupportForm:
                    "hicgat_truth_support")
         return cls(float(background), rowptr, col, val, diag, nnz)
 
+    @classmethod
+    def build_host(cls, truth, background, max_fraction=SUPPORT_MAX_FRACTION):
+        """The same form of a CPU truth (torch ops; the multi-rank CPU tests), or None."""
+        n = truth.n
+        t = truth.buf[:, :n].float()
+        off = (t != float(background)) & ~torch.eye(n, dtype=torch.bool)
+        nnz = int(off.sum())
+        if nnz > max_fraction * float(n) * float(n):
+            return None
+        rows, cols = off.nonzero(as_tuple=True)
+        rowptr = torch.zeros(n + 1, dtype=torch.int64)
+        rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+        col = cols.to(torch.int32) if nnz else torch.zeros(1, dtype=torch.int32)
+        val = t[rows, cols].contiguous() if nnz else torch.zeros(1)
+        return cls(float(background), rowptr.to(torch.int32), col, val, t.diagonal().contiguous(), nnz)
+
 
 class Truth:
     """fp32 target for the fused distance/MSE kernel: [N, ld] with ld = ceil(N/128)*128.

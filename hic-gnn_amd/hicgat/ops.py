@@ -112,6 +112,21 @@ def side_flush(after=None):
                 fn()
 
 
+def side_record():
+    """Events recorded now on every side stream in use: they complete when the side work issued
+    so far (e.g. the tail's flushed dW GEMMs) has run.  [] when nothing went to a side stream."""
+    if not _SIDE["on"]:
+        return []
+    with _SIDE_LOCK:
+        streams = [_SIDE["streams"][key] for key in _SIDE["mains"]]
+    evs = []
+    for st in streams:
+        ev = torch.cuda.Event()
+        ev.record(st)
+        evs.append(ev)
+    return evs
+
+
 def side_join():
     """Flush the queue, make every stream that forked work onto the side stream wait for it, and
     drop the held inputs.  Always runs the queued launches, even after an exception upstream, so

@@ -228,6 +228,18 @@ int hicgat_pairdist_mse_fused_support(const float *coords, int N, float backgrou
                                       double *stats, float *loss, float *dcoords, void *workspace,
                                       size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_pairdist_support_workspace_bytes(int N);
+/* The background-form loss over a SHARE of the pairs (a rank of hicgat.dist): the bulk over the
+ * upper-triangle tiles [tile_begin, tile_end) and the support rows [support_row_begin,
+ * support_row_end) (their entries j != i and their diagonal).  stats[0..6] and dcoords [N,3] are
+ * that share's partial sums (the sum over shares that cover every tile and every row once is the
+ * whole loss: a caller all-reduces stats[0..6] + dcoords and calls hicgat_pairdist_finalize);
+ * 0, -1, 0, N is hicgat_pairdist_mse_fused_support.  Same workspace. */
+int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background, const int32_t *rowptr,
+                                            const int32_t *col, const float *val, const float *diag,
+                                            int64_t tile_begin, int64_t tile_end, int support_row_begin,
+                                            int support_row_end, int loss_kind, double *stats, float *loss,
+                                            float *dcoords, void *workspace, size_t workspace_bytes,
+                                            hicgat_stream_t stream);
 /* The background form of a symmetric N x N fp32 truth T (leading dim ldt): the sorted CSR of the
  * off-diagonal entries != background, their values, and the diagonal.  Two calls, as
  * hicgat_csr_from_dense: col == NULL fills rowptr (the counts, scanned); then col / val / diag. */

@@ -148,9 +148,12 @@ class CpuKernels:
         n, D = h.shape
         C = D // H
         hv = h.view(n, H, C).double()
-        datt_l = None if da_src is None else (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
-        datt_r = (row_stats[:, 3 * H:4 * H].double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
-        res = (datt_l, datt_r, None if dout is None else dout.double().sum(0).float())
+        want = (True, True, True) if out is None else tuple(o is not None for o in out)
+        datt_l = (da_src.double().unsqueeze(-1) * hv).sum(0).reshape(-1).float() if want[0] else None
+        datt_r = ((row_stats[:, 3 * H:4 * H].double().unsqueeze(-1) * hv).sum(0).reshape(-1).float()
+                  if want[1] else None)
+        dbias = dout.double().sum(0).float() if want[2] else None
+        res = (datt_l, datt_r, dbias)
         if out is None:
             return res
         for o, r in zip(out, res):
@@ -195,6 +198,49 @@ class CpuKernels:
         g.index_add_(0, ii, w.unsqueeze(1) * diff)
         g.index_add_(0, jj, -w.unsqueeze(1) * diff)
         dcoords.copy_(g.float())
+        self.loss_finalize(n, kind, stats, loss)
+
+    def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords):
+        """hicgat_pairdist_mse_fused_support_range: the bulk (every pair of the tile range at the
+        background value) + the support rows [s0, s1) (their differing entries and diagonal)."""
+        nb = (n + BT - 1) // BT
+        c = coords.double()
+        bg = float(sf.background)
+        iu = torch.triu_indices(n, n, 1)
+        ii, jj = iu[0], iu[1]
+        tid = _tri(ii // BT, jj // BT, nb)
+        keep = (tid >= t0) & (tid < t1)
+        ii, jj = ii[keep], jj[keep]
+        diff = c[ii] - c[jj]
+        d = diff.norm(dim=1)
+        r = d - bg
+        m = torch.zeros(7, dtype=torch.float64)
+        m[0] = (r * r).sum()
+        m[1] = d.sum()
+        m[2] = (d * d).sum()
+        m[3] = (d * bg).sum()
+        m[4] = bg * d.numel()
+        m[5] = bg * bg * d.numel()
+        g = torch.zeros((n, 3), dtype=torch.float64)
+        w = torch.where(d > 0, r / d, torch.zeros_like(d))
+        g.index_add_(0, ii, w.unsqueeze(1) * diff)
+        g.index_add_(0, jj, -w.unsqueeze(1) * diff)
+        rp = sf.rowptr.long()
+        si, ei = _rows(rp, s0, s1)
+        sj = sf.col_buf.long()[ei]
+        t = sf.val_buf.double()[ei]
+        sdiff = c[si] - c[sj]
+        sd = sdiff.norm(dim=1)
+        g.index_add_(0, si, torch.where(sd > 0, (bg - t) / sd, torch.zeros_like(sd)).unsqueeze(1) * sdiff)
+        up = sj > si
+        su, tu = sd[up], t[up]
+        m[0] += ((su - tu) ** 2 - (su - bg) ** 2).sum()
+        m[3] += (su * (tu - bg)).sum()
+        m[4] += (tu - bg).sum()
+        m[5] += (tu * tu - bg * bg).sum()
+        m[6] = (sf.diag.double()[s0:s1] ** 2).sum()
+        stats[:7] = m
+        dcoords.copy_((g * (4.0 / (n * n))).float())
         self.loss_finalize(n, kind, stats, loss)
 
     def loss_finalize(self, n, kind, stats, loss):

@@ -1,5 +1,6 @@
-"""CPU, world_size 2 (gloo): the destination-row sharded step (hicgat.dist.ShardedTrainer) equals
-the single-rank step, and the single-rank step equals the autograd oracle.
+"""CPU, world_size 2 and 3 (gloo): the destination-row sharded step (hicgat.dist.ShardedTrainer),
+in both forms ("slab": x replicated, no h / dout all-gathers; "allgather": the north star's h
+all-gather), equals the single-rank step, and the single-rank step equals the autograd oracle.
 
 The trainer runs against tests/cpu_kernels.CpuKernels (torch stand-ins for the HIP kernels), so
 this covers the partition, the all-gathers / all-reduces and the manual backward bookkeeping; the
@@ -57,7 +58,7 @@ def _setup(n, skew=False):
     return hicgat, adj, truth, torch.tensor(x)
 
 
-def _worker(rank, world, port, n, kind, out, skew=False, replicate_x=False):
+def _worker(rank, world, port, n, kind, out, skew=False, mode="slab"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -68,10 +69,12 @@ def _worker(rank, world, port, n, kind, out, skew=False, replicate_x=False):
         torch_tail(hicgat)
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated()
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels(),
-                                        replicate_x=replicate_x)
-        # what this rank holds: its edges, its x rows, its truth band (not the whole matrix)
-        held = torch.tensor([tr.local_nnz, tr.local_rows, tr.tband.numel(), tr.x_loc.shape[0]], dtype=torch.long)
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, kind=kind, kern=CpuKernels(), mode=mode)
+        # what this rank holds: its edges, its x rows, its support rows / entries, its slab entries
+        sf = tr.sf
+        held = torch.tensor([tr.local_nnz, tr.local_rows, tr.s1 - tr.s0,
+                             int(sf.rowptr[tr.s1]) - int(sf.rowptr[tr.s0]), getattr(tr, "slab_nnz", -1),
+                             tr.t1 - tr.t0], dtype=torch.long)
         allheld = [torch.zeros_like(held) for _ in range(world)]
         dist.all_gather(allheld, held)
         losses, grad1, stats1 = [], None, None
@@ -94,24 +97,43 @@ def _worker(rank, world, port, n, kind, out, skew=False, replicate_x=False):
         dist.destroy_process_group()
 
 
-def _run(world, n, kind, tmp_path, skew=False, replicate_x=False):
-    out = str(tmp_path / f"w{world}_{kind}_{int(skew)}{int(replicate_x)}.pt")
-    mp.spawn(_worker, args=(world, _free_port(), n, kind, out, skew, replicate_x), nprocs=world, join=True)
+def _run(world, n, kind, tmp_path, skew=False, mode="slab"):
+    out = str(tmp_path / f"w{world}_{kind}_{int(skew)}{mode}.pt")
+    mp.spawn(_worker, args=(world, _free_port(), n, kind, out, skew, mode), nprocs=world, join=True)
     return torch.load(out, weights_only=True)
+
+
+def _close(a, b):
+    """Step 1 (loss, moments, all-reduced gradient) agrees to summation-order rounding; later
+    steps only loosely, because Adam normalises near-zero gradient entries (e.g. dense3.bias,
+    whose exact gradient is 0 by translation invariance) into lr-sized moves of either sign."""
+    assert abs(b["losses"][0] - a["losses"][0]) <= 1e-6 * abs(a["losses"][0])
+    assert torch.allclose(b["stats"][:9], a["stats"][:9], rtol=1e-9)
+    g1, g2 = a["grad1"], b["grad1"]
+    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
+    np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-3)
 
 
 @pytest.mark.parametrize("kind", ["mse", "combined"])
 def test_sharded_step_equals_single_rank(tmp_path, kind):
-    """Step 1 (loss, moments, all-reduced gradient) agrees to summation-order rounding; later
-    steps only loosely, because Adam normalises near-zero gradient entries (e.g. dense3.bias,
-    whose exact gradient is 0 by translation invariance) into lr-sized moves of either sign."""
     one = _run(1, 300, kind, tmp_path)
     two = _run(2, 300, kind, tmp_path)
-    assert abs(two["losses"][0] - one["losses"][0]) <= 1e-6 * abs(one["losses"][0])
-    assert torch.allclose(two["stats"][:9], one["stats"][:9], rtol=1e-9)
-    g1, g2 = one["grad1"], two["grad1"]
-    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
-    np.testing.assert_allclose(two["losses"], one["losses"], rtol=1e-3)
+    _close(one, two)
+
+
+@pytest.mark.parametrize("mode", ["slab", "allgather"])
+def test_three_uneven_ranks_equal_single_rank(tmp_path, mode):
+    """World 3 on a 301-node graph (uneven rows, edges, tiles and support rows per rank): both
+    step forms equal the world-1 step; the shards partition the edges, the support and the tiles."""
+    one = _run(1, 301, "combined", tmp_path, mode=mode)
+    three = _run(3, 301, "combined", tmp_path, mode=mode)
+    _close(one, three)
+    held, full = three["held"], one["held"][0]
+    assert int(held[:, 0].sum()) == int(full[0]) and int(held[:, 1].sum()) == 301
+    assert int(held[:, 2].sum()) == 301 and int(held[:, 3].sum()) == int(full[3])
+    assert int(held[:, 5].sum()) == int(full[5])
+    if mode == "slab":
+        assert int(held[:, 4].sum()) == int(full[4]) == int(full[0])     # the slabs partition the CSR
 
 
 def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
@@ -150,25 +172,22 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
         assert (mine - pr.grad).abs().max().item() <= 1e-4 * scale, name
 
 
-@pytest.mark.parametrize("replicate_x", [False, True])
-def test_skewed_graph_shards_balance_nnz_and_match_world1(tmp_path, replicate_x):
+@pytest.mark.parametrize("mode", ["slab", "allgather"])
+def test_skewed_graph_shards_balance_nnz_and_match_world1(tmp_path, mode):
     """destination rows split by an nnz prefix sum.  On a dense band + sparse tail
     the two shards hold (nearly) equal edge counts -- very unequal row counts -- each rank holds
-    only its edges / x rows / truth band, and the world-2 step equals the world-1 step (also
-    with x replicated and h recomputed on every rank, the 8(e) ablation)."""
-    one = _run(1, 300, "mse", tmp_path, skew=True)
-    two = _run(2, 300, "mse", tmp_path, skew=True, replicate_x=replicate_x)
+    only its edges, x rows and support rows, and the world-2 step equals the world-1 step."""
+    one = _run(1, 300, "mse", tmp_path, skew=True, mode=mode)
+    two = _run(2, 300, "mse", tmp_path, skew=True, mode=mode)
     held = two["held"]
     nnz0, nnz1 = int(held[0, 0]), int(held[1, 0])
     rows0, rows1 = int(held[0, 1]), int(held[1, 1])
     assert nnz0 + nnz1 == int(one["held"][0, 0])
     assert abs(nnz0 - nnz1) <= 0.02 * (nnz0 + nnz1), (nnz0, nnz1)
     assert rows0 + rows1 == 300 and rows0 < rows1 / 2, (rows0, rows1)     # balance is by edges, not rows
-    assert int(held[0, 2]) < two["truth_numel"] and int(held[1, 2]) < two["truth_numel"]
-    assert abs(two["losses"][0] - one["losses"][0]) <= 1e-6 * abs(one["losses"][0])
-    g1, g2 = one["grad1"], two["grad1"]
-    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
-    np.testing.assert_allclose(two["losses"], one["losses"], rtol=1e-3)
+    s0, s1 = int(held[0, 3]), int(held[1, 3])
+    assert abs(s0 - s1) <= 0.05 * (s0 + s1), (s0, s1)                       # support entries balanced too
+    _close(one, two)
 
 
 def test_partition_rows_prefix_sum():

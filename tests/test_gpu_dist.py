@@ -1,8 +1,10 @@
 """GPU: hicgat.dist.ShardedTrainer on the HIP kernels.
 
-* 1 rank over RCCL ("nccl") vs the single-GPU autograd step (same loss, same gradients);
-* 2 ranks sharing the one GPU over gloo (CUDA tensors) vs 1 rank: the row shards, the all-gathers
-  of h / coords / dout / row stats and the gradient all-reduce give the 1-rank step.
+* 1 rank over RCCL ("nccl") vs the single-GPU autograd step (same loss, same gradients), and the
+  captured step (kernels + RCCL collectives + the comm-stream gradient bucket) vs eager steps;
+* 2 and 3 ranks sharing the one GPU over gloo (CUDA tensors) vs 1 rank, both step forms ("slab":
+  slab source pass + partial dW; "allgather": all-gathers of h and [dout | row stats]);
+* the one-rank-at-a-time simulation (SimComm) used by bench.py --simulate-world.
 The 8-GPU RCCL run itself is the driver's scaling bench.
 """
 import os
@@ -40,7 +42,7 @@ def _inputs(n, dev):
     return hicgat, adj, truth, x
 
 
-def _graph_worker(rank, world, port, n, out):
+def _graph_worker(rank, world, port, n, out, mode):
     """RCCL, captured sharded step (kernels + collectives in one hipGraph) vs eager steps."""
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -54,7 +56,7 @@ def _graph_worker(rank, world, port, n, out):
         for graphed in (False, True):
             torch.manual_seed(0)
             model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
-            tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3)
+            tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode=mode)
             losses = []
             if graphed:
                 step = tr.captured(warmup=2)
@@ -73,15 +75,16 @@ def _graph_worker(rank, world, port, n, out):
         dist.destroy_process_group()
 
 
-def test_sharded_rccl_graph_replay_equals_eager(tmp_path):
-    out = str(tmp_path / "graph.pt")
-    mp.spawn(_graph_worker, args=(1, _port(), 700, out), nprocs=1, join=True)
+@pytest.mark.parametrize("mode", ["slab", "allgather"])
+def test_sharded_rccl_graph_replay_equals_eager(tmp_path, mode):
+    out = str(tmp_path / f"graph_{mode}.pt")
+    mp.spawn(_graph_worker, args=(1, _port(), 700, out, mode), nprocs=1, join=True)
     r = torch.load(out, weights_only=True)
     assert r["eager"][2:] == r["graph"][2:]
     assert torch.equal(r["pe"], r["pg"])
 
 
-def _worker(rank, world, port, backend, n, out, replicate_x=False):
+def _worker(rank, world, port, backend, n, out, mode="slab"):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -95,7 +98,7 @@ def _worker(rank, world, port, backend, n, out, replicate_x=False):
         hicgat, adj, truth, x = _inputs(n, dev)
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, replicate_x=replicate_x)
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode=mode)
         loss, stats, _ = tr.step()
         grad1 = tr.opt.grad.clone().cpu()
         stats = stats.clone()           # the trainer's stats buffer is reused by the next step
@@ -108,9 +111,9 @@ def _worker(rank, world, port, backend, n, out, replicate_x=False):
         dist.destroy_process_group()
 
 
-def _run(world, backend, n, tmp_path, replicate_x=False):
-    out = str(tmp_path / f"{backend}{world}{int(replicate_x)}.pt")
-    mp.spawn(_worker, args=(world, _port(), backend, n, out, replicate_x), nprocs=world, join=True)
+def _run(world, backend, n, tmp_path, mode="slab"):
+    out = str(tmp_path / f"{backend}{world}{mode}.pt")
+    mp.spawn(_worker, args=(world, _port(), backend, n, out, mode), nprocs=world, join=True)
     return torch.load(out, weights_only=True)
 
 
@@ -133,17 +136,38 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path):
     assert (g - res["grad1"]).abs().max().item() <= 1e-5 * g.abs().max().item()
 
 
-@pytest.mark.parametrize("replicate_x", [False, True])
-def test_sharded_two_ranks_equal_one_rank(tmp_path, replicate_x):
-    """nnz-balanced shards (padded buffers, remapped local CSR, truth bands) over gloo on the one
-    GPU; replicate_x: the SURVEY 8(e) ablation (h recomputed on every rank, no h all-gather)."""
+@pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "allgather"), (3, "slab"), (3, "allgather")])
+def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
+    """nnz-balanced shards over gloo on the one GPU, both step forms, 2 and 3 (uneven) ranks."""
     n = 777
     one = _run(1, "gloo", n, tmp_path)
-    two = _run(2, "gloo", n, tmp_path, replicate_x)
-    # the MLP tail runs on 389/388-row shards instead of 777 rows: hipBLASLt may pick another
-    # kernel (another k order) for the smaller GEMMs, so coordinates agree to ~1e-7, not bitwise
-    assert abs(two["loss"][0] - one["loss"][0]) <= 1e-6 * abs(one["loss"][0])
-    assert torch.allclose(two["stats"][:7], one["stats"][:7], rtol=1e-6)
-    g1, g2 = one["grad1"], two["grad1"]
+    many = _run(world, "gloo", n, tmp_path, mode)
+    # the MLP tail runs on shards of the rows and the partial sums (dW, dcoords, loss moments) are
+    # added across ranks: another fp32 summation order, so agreement to rounding, not bitwise
+    assert abs(many["loss"][0] - one["loss"][0]) <= 1e-6 * abs(one["loss"][0])
+    assert torch.allclose(many["stats"][:7], one["stats"][:7], rtol=1e-6)
+    g1, g2 = one["grad1"], many["grad1"]
     assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
-    np.testing.assert_allclose(two["loss"], one["loss"], rtol=1e-3)
+    np.testing.assert_allclose(many["loss"], one["loss"], rtol=1e-3)
+
+
+def test_simulated_ranks_run_their_shares():
+    """bench.py --simulate-world: each rank's share of a 3-rank step runs captured on one GPU with
+    the collectives left out; the shards partition the edges, slabs, tiles and support rows."""
+    hicgat, adj, truth, x = _inputs(777, "cuda")
+    tot = {"nnz": 0, "slab": 0, "tiles": 0, "srows": 0}
+    for r in range(3):
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(3, r))
+        step = tr.captured(warmup=1)
+        for _ in range(2):
+            loss = step()[0]
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss).item()
+        tot["nnz"] += tr.local_nnz
+        tot["slab"] += tr.slab_nnz
+        tot["tiles"] += tr.t1 - tr.t0
+        tot["srows"] += tr.s1 - tr.s0
+    assert tot["nnz"] == tot["slab"] == adj.device_nnz
+    assert tot["srows"] == 777 and tot["tiles"] == tr.plan.tiles

@@ -1,0 +1,82 @@
+#!/bin/bash
+# One parametrised GPU run script (replaces the round-2 one-off gpu_r02*.sh files).
+#
+#   bash tools/gpu_run.sh <tag> <step> [<step> ...]      (outputs: gpurun_out/<tag>_*)
+#
+# steps (each under its own time limit; the script stops at the first failure):
+#   tests        pytest -m gpu (whole GPU suite)
+#   tests:<k>    pytest -m gpu -k <k>
+#   smoke        __graft_entry__.smoke()
+#   bench        default bench.py (N = 1, synth-20000, with the CPU baseline)
+#   bench2000    bench.py --workload synth-2000 --no-cpu-baseline
+#   ab:<env>     bench.py 200 steps under the environment assignment <env> (A/B lines "ab: ...")
+#   prof         rocprofv3 --kernel-trace --stats of bench.py (20 steps, graph replay)
+#   pmc_traffic  two PMC passes (FETCH_SIZE, WRITE_SIZE) of an eager bench -> <tag>_pmc_traffic.json
+#   pmc_mfma     one PMC pass (MFMA busy cycles, F32 MFMA MOPs, GRBM_GUI_ACTIVE) -> <tag>_pmc_mfma.json
+#   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
+#   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world)
+#   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+T=${1:?tag}
+shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+COMMIT=$(cat .commit 2>/dev/null || echo unknown)
+for S in "$@"; do
+  echo "== $S"
+  case "$S" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread \
+        > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_gpu.log; [ $rc -eq 0 ] || exit $rc ;;
+    tests:*)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread -k "${S#tests:}" \
+        > gpurun_out/${T}_pytest_k.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_k.log; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || exit $?
+      tail -1 gpurun_out/${T}_smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit $?
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/${T}_bench.json ;;
+    bench2000)
+      timeout -k 10 300 python bench.py --workload synth-2000 --no-cpu-baseline > gpurun_out/${T}_bench_synth2000.json \
+        2> gpurun_out/${T}_bench_synth2000.err || exit $?
+      grep -o '"ms_per_step": [0-9.]*' gpurun_out/${T}_bench_synth2000.json ;;
+    ab:*)
+      env ${S#ab:} timeout -k 10 180 python bench.py --steps 200 --warmup 10 --no-cpu-baseline > gpurun_out/${T}_ab.json \
+        2> gpurun_out/${T}_ab.err || exit $?
+      echo "ab: ${S#ab:} $(python -c "import json;d=json.loads(open('gpurun_out/${T}_ab.json').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],4), round(d['median_ms_per_step'],4))")" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run --output-format csv -- \
+        python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_rocprof.log 2>&1 || exit $?
+      echo "prof ok" ;;
+    pmc_traffic)
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/${T}_pmc_fetch -o run --output-format csv -- \
+        python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/${T}_pmc_fetch.log 2>&1 || exit $?
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/${T}_pmc_write -o run --output-format csv -- \
+        python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/${T}_pmc_write.log 2>&1 || exit $?
+      python tools/pmc_traffic.py gpurun_out/${T}_pmc_fetch/run_counter_collection.csv \
+        gpurun_out/${T}_pmc_write/run_counter_collection.csv gpurun_out/${T}_pmc_traffic.json synth-20000 \
+        "rocprofv3 --kernel-trace --pmc FETCH_SIZE|WRITE_SIZE -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager" \
+        "$COMMIT" > /dev/null || exit $?
+      echo "pmc_traffic ok" ;;
+    pmc_mfma|pmc_mfma2000)
+      W=synth-20000; [ "$S" = pmc_mfma2000 ] && W=synth-2000
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
+        -d gpurun_out/${T}_${S} -o run --output-format csv -- \
+        python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/${T}_${S}.log 2>&1 || exit $?
+      python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json $W \
+        "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager" \
+        "$COMMIT" || exit $? ;;
+    simrank)
+      for P in 2 4 8; do
+        timeout -k 10 240 python bench.py --simulate-world $P --steps 50 --warmup 5 > gpurun_out/${T}_simrank_P$P.json \
+          2> gpurun_out/${T}_simrank_P$P.err || exit $?
+        python -c "import json;d=json.loads(open('gpurun_out/${T}_simrank_P$P.json').read().strip().splitlines()[-1]);print('P=$P', d['simulated']['rank_ms'], d['simulated']['model_ms_per_step'])"
+      done ;;
+    align)
+      timeout -k 10 600 python tools/run_config5.py gpurun_out/${T}_align > gpurun_out/${T}_align.log 2>&1; rc=$?
+      tail -8 gpurun_out/${T}_align.log; [ $rc -eq 0 ] || exit $rc ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
+echo "== all steps ok"
