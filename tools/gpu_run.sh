@@ -16,6 +16,8 @@
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
 #   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
+#   cli          the reference driver's flow (python -m hicgat.train) on chr19 1 mb with GPU node2vec
+#                features, the default conversion sweep, 1000 steps each -> gpurun_out/<tag>_cli/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:?tag}
 shift
@@ -76,6 +78,12 @@ for S in "$@"; do
     align)
       timeout -k 10 600 python tools/run_config5.py gpurun_out/${T}_align > gpurun_out/${T}_align.log 2>&1; rc=$?
       tail -8 gpurun_out/${T}_align.log; [ $rc -eq 0 ] || exit $rc ;;
+    cli)
+      mkdir -p gpurun_out/${T}_cli
+      python -c "import numpy as np; d = np.load('tests/golden/graph_chr19_1mb.npz'); np.savetxt('gpurun_out/${T}_cli/GM12878_1mb_chr19_list.txt', d['list'], fmt='%d\t%d\t%.6f')" || exit 1
+      (cd hic-gnn_amd && timeout -k 10 500 python -m hicgat.train ../gpurun_out/${T}_cli/GM12878_1mb_chr19_list.txt node2vec \
+        --steps 1000 --out ../gpurun_out/${T}_cli/GM12878_1mb_chr19 > ../gpurun_out/${T}_cli/run.log 2>&1); rc=$?
+      tail -5 gpurun_out/${T}_cli/run.log; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
