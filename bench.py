@@ -56,6 +56,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy ~6290
 L2_PEAK_GBS = 34500.0   # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)")
+MALL_GATHER_GBS = 8600.0  # Infinity-Cache random-row gather rate, 33.5 GB/s per CU (MI355X_MICROARCH.md)
 MFMA_F32_TFS = 157.3    # dense fp32 MFMA peak, v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md)
 D_FEAT = 512
 HEADS = 2
@@ -96,17 +97,43 @@ PMC_KERNELS = {
 }
 
 
+def kernel_src_hash():
+    """sha1 of the kernel sources (hic-gnn_amd/csrc/*): a PMC summary recorded with other kernel
+    sources describes other kernels (tools/pmc_traffic.py and tools/pmc_mfma.py store it)."""
+    import glob
+    import hashlib
+    h = hashlib.sha1()
+    for f in sorted(glob.glob(os.path.join(ROOT, "hic-gnn_amd", "csrc", "*"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _pmc_doc(pattern, workload):
+    """The newest committed PMC summary for ``workload`` recorded with the CURRENT kernel sources,
+    else the newest one flagged stale: (doc, source dict) or (None, None)."""
+    import glob
+    cur = kernel_src_hash()
+    docs = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload:
+            docs.append((d, f))
+    if not docs:
+        return None, None
+    fresh = [x for x in docs if x[0].get("src_hash") == cur]
+    d, f = (fresh or docs)[-1]
+    return d, {"file": os.path.relpath(f, ROOT), "command": d.get("command"), "commit": d.get("commit"),
+               "src_hash": d.get("src_hash"), "current_src_hash": cur, "stale": not fresh}
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of ``kernel`` from the newest committed PMC summary for ``workload``
     (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py from two rocprofv3 --pmc passes
     of this bench: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  (bytes, source) or (None, None)."""
-    import glob
-    best, src = None, None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
-        with open(f) as fh:
-            d = json.load(fh)
-        if d.get("workload") == workload:
-            best, src = d, f
+    best, src = _pmc_doc("*pmc_traffic*.json", workload)
     if best is None:
         return None, None
     tot, seen = 0.0, False
@@ -117,7 +144,31 @@ def pmc_traffic(kernel, workload):
                 seen = True
     if not seen:
         return None, None
-    return tot, {"file": os.path.relpath(src, ROOT), "command": best.get("command"), "commit": best.get("commit")}
+    return tot, src
+
+
+def gemm_block(workload, kern_t):
+    """MFMA utilisation of the GEMMs (north star: "MFMA utilisation against CDNA4 peak"): per kernel
+    shape (template + grid) from the committed rocprofv3 PMC pass (profiles/*pmc_mfma*.json,
+    tools/pmc_mfma.py: FLOP = SQ_INSTS_VALU_MFMA_MOPS_F32 x 512, busy = SQ_VALU_MFMA_BUSY_CYCLES /
+    (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)), plus the live HIP-event time per step of each GEMM family."""
+    doc, src = _pmc_doc("*pmc_mfma*.json", workload)
+    out = {"peak_tflops": MFMA_F32_TFS, "source": src, "shapes": {}}
+    if doc is not None:
+        tot_f = tot_t = 0.0
+        for k, v in doc["kernels"].items():
+            if v["flop"] < 1e9:
+                continue
+            out["shapes"][k] = {"gflop": v["flop"] / 1e9, "tflops": v["tflops_pmc"], "frac": v["tflops_pmc"] / MFMA_F32_TFS,
+                                "mfma_busy": v["mfma_busy"], "clock_ghz": v["clock_ghz"]}
+            tot_f += v["flop"] * v["dispatches"]
+            tot_t += v["duration_s"] * v["dispatches"]
+        if tot_t > 0:
+            out["weighted_tflops"] = tot_f / tot_t / 1e12
+            out["weighted_frac"] = out["weighted_tflops"] / MFMA_F32_TFS
+    out["live_ms_per_step"] = {k: v["total_ms"] / max(1, v["launches"]) * v["launches"] for k, v in kern_t.items()
+                               if k.startswith("gemm") or k == "gat_linear_att"}
+    return out
 
 
 def build_workload(name, seed, device):
@@ -263,7 +314,7 @@ def simulate_world(args):
     wl = build_workload(args.workload, args.seed, dev)
     rank_ms, rank_med, shards = [], [], []
     truth = wl["truth"]
-    for r in range(P):
+    for r in (range(P) if args.sim_rank is None else [args.sim_rank]):
         torch.manual_seed(0)
         model = hicgat.MODELS[args.model]().to(dev)
         tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], truth, lr=1e-3, kind=args.loss,
@@ -330,6 +381,7 @@ def main():
                          "destination owner -- no h / dout all-gathers) or the all-gather of h before the layer")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="one GPU: time each rank's share of a P-rank sharded step, collectives left out")
+    ap.add_argument("--sim-rank", type=int, default=None, help="--simulate-world: only this rank (profiling)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
@@ -478,6 +530,10 @@ def main():
         traffic, src = pmc_traffic(dom, args.workload) if world == 1 else (None, None)
         achieved = traffic / (avg * 1e-3) / 1e9 if traffic else None
         roof = {"bound": "hbm", "kernel": dom,
+                "limiter": "L2->CU row-gather rate (near edges) and the Infinity-Cache (MALL) random-row rate "
+                           "(far edges); the counter bytes are mostly MALL hits (DESIGN.md section 3)",
+                "mall_peak": MALL_GATHER_GBS,
+                "mall_frac": (traffic / (avg * 1e-3) / 1e9 / MALL_GATHER_GBS) if traffic else None,
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic, "traffic_source": src,
@@ -528,6 +584,7 @@ def main():
                             if not args.selftest_cpu else "cpu stand-in")},
         "final_loss": loss_v,
         "roofline": roof,
+        "gemm": gemm_block(args.workload, kern_t) if not args.selftest_cpu else None,
         "kernels": kern_t,
     }
     if sharded:

@@ -140,10 +140,10 @@ __global__ __launch_bounds__(256) void n2v_sgns_kernel(const int *__restrict__ w
         if (d > 0) {
           const uint32_t x = (uint32_t)(rng4(seed, 0x9Dull + epoch, ((uint64_t)w << 20) | (uint64_t)i,
                                              ((uint64_t)j << 8) | (uint64_t)d) % total);
-          int lo = 0, hi = V - 1;                        // first k with cum[k] > x
+          int lo = 0, hi = V - 1;                        // first k with cum[k] >= x (gensim's bisect_left)
           while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (cum[mid] > x) hi = mid;
+            if (cum[mid] >= x) hi = mid;
             else lo = mid + 1;
           }
           target = lo;

@@ -12,9 +12,11 @@ HiC-GNN_node2vec_conversion.py:118 with other p / q / walk lengths):
 (``hicgat_n2v_walks``) and the skip-gram epochs (``hicgat_n2v_sgns_epoch``) run in libhicgat.so;
 the host builds the weighted CSR (networkx's edge / weight rule) and gensim's vocabulary tables
 (downsampling keep probabilities, unigram^0.75 negative-sampling table) from the walk counts.
-Differences from the reference, by construction: the random streams (a counter-based RNG instead of
-Python's / numpy's), the initial vectors (same distribution, U(-0.5/D, 0.5/D)) and the Hogwild
-update order -- node2vec output is stochastic, so no two implementations agree bit for bit.
+Differences from the reference, by construction: the random streams of the walks and of the
+skip-gram (a counter-based RNG instead of Python's / gensim's LCG) and the update order of the
+concurrent skip-gram waves (``max_waves``; the reference trains with one worker) -- node2vec output
+is stochastic, so no two implementations agree bit for bit.  The initial vectors are gensim 4's
+(``initial_vectors``: same generator, same vocabulary order, given the walks).
 """
 import numpy as np
 import torch
@@ -74,8 +76,28 @@ def vocab_tables(counts, sample=1e-3, ns_exponent=0.75):
     return keep.astype(np.float32), cum
 
 
+def initial_vectors(walks, n_words, dimensions, w2v_seed=1):
+    """gensim 4's initial input vectors: ``prep_vectors`` draws ``default_rng(seed).random((V, D))``
+    mapped to U(-1/D, 1/D) for the vocabulary in its order -- ``sort_by_descending_frequency``, a
+    stable sort of the words in first-appearance order of the corpus -- so node n gets row
+    rank(n).  The reference's ``.fit(window=25, min_count=1, batch_words=4)`` passes no seed, so
+    Word2Vec's default seed 1 applies."""
+    flat = walks.reshape(-1)
+    flat = flat[flat >= 0].cpu().numpy().astype(np.int64)
+    counts = np.bincount(flat, minlength=n_words)
+    words, first = np.unique(flat, return_index=True)
+    order = words[np.lexsort((first, -counts[words]))]          # descending count, then first appearance
+    init = np.random.default_rng(seed=w2v_seed).random((len(order), dimensions), dtype=np.float32)
+    init *= 2.0
+    init -= 1.0
+    init /= dimensions
+    vec = np.zeros((n_words, dimensions), dtype=np.float32)     # a node no walk visits stays 0 (not in the vocab)
+    vec[order] = init
+    return vec
+
+
 def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, alpha=0.025, min_alpha=1e-4,
-             sample=1e-3, seed=42, max_waves=None):
+             sample=1e-3, seed=42, max_waves=None, w2v_seed=1):
     """Word2Vec(sg=1, hs=0) over the walks: returns the input vectors syn0 [n_words, dimensions].
     ``max_waves`` bounds the walks trained concurrently (default n_words // 4, within [8, 4096]):
     on a Hi-C-sized vocabulary (58 loci for chr19 1 mb) thousands of concurrent Hogwild writers
@@ -87,9 +109,7 @@ def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, al
     keep, cum = vocab_tables(counts, sample)
     t_keep = torch.tensor(keep, device=dev)
     t_cum = torch.tensor(cum.view(np.int32), device=dev)          # uint32 bits
-    g = torch.Generator(device=dev)
-    g.manual_seed(int(seed))
-    syn0 = (torch.rand((n_words, dimensions), generator=g, device=dev) - 0.5) / dimensions
+    syn0 = torch.tensor(initial_vectors(walks, n_words, dimensions, w2v_seed), device=dev)
     syn1 = torch.zeros_like(syn0)
     st = _lib.stream(dev)
     if max_waves is None:
@@ -103,9 +123,33 @@ def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, al
 
 
 def node2vec(matrix, dimensions=512, walk_length=150, num_walks=50, p=1.75, q=0.4, window=25, epochs=5,
-             negative=5, alpha=0.025, min_alpha=1e-4, sample=1e-3, seed=42, device="cuda"):
+             negative=5, alpha=0.025, min_alpha=1e-4, sample=1e-3, seed=42, device="cuda", max_waves=None):
     """[N, dimensions] node2vec embeddings of ``matrix`` (node order), HiC_GAT_generalize_directly.py's
     defaults."""
     walks = random_walks(matrix, num_walks, walk_length, p, q, seed, device)
     return skipgram(walks, np.asarray(matrix).shape[0], dimensions, window, epochs, negative, alpha, min_alpha,
-                    sample, seed)
+                    sample, seed, max_waves=max_waves)
+
+
+def embedding_stats(emb, truth=None):
+    """Structure of an embedding matrix [N, F] (SURVEY 8(f) f4 has no reference vectors to compare):
+    ``shared`` -- the share of the rows' energy in their common mean, ||mean||^2 / mean ||x_i||^2;
+    ``cos_mean`` -- the mean pairwise cosine; ``locality`` -- Spearman of the pairwise distances
+    of the CENTRED rows against the genomic separation |i - j| (positive: nearby loci embed nearby);
+    ``truth_rho`` -- Spearman of those distances against ``truth`` (e.g. cont2dist of the contacts)."""
+    from scipy.stats import spearmanr
+    e = np.asarray(emb, dtype=np.float64)
+    n = e.shape[0]
+    mu = e.mean(0)
+    shared = float(mu @ mu / np.mean(np.sum(e * e, 1)))
+    u = e / np.maximum(np.linalg.norm(e, axis=1, keepdims=True), 1e-30)
+    iu = np.triu_indices(n, 1)
+    cos = (u @ u.T)[iu]
+    c = e - mu
+    d = np.sqrt(np.maximum(np.sum(c * c, 1)[:, None] + np.sum(c * c, 1)[None, :] - 2 * c @ c.T, 0))[iu]
+    sep = (iu[1] - iu[0]).astype(np.float64)
+    out = {"shared": shared, "cos_mean": float(cos.mean()), "cos_min": float(cos.min()),
+           "norm_mean": float(np.linalg.norm(e, axis=1).mean()), "locality": float(spearmanr(d, sep)[0])}
+    if truth is not None:
+        out["truth_rho"] = float(spearmanr(d, np.asarray(truth, dtype=np.float64)[iu])[0])
+    return out

@@ -389,7 +389,8 @@ class Truth:
     so the off-diagonal becomes tbar (same gradient) and the constant (T_ij - T_ji)^2 / 2 of row i's
     pairs j > i is folded into the diagonal, whose only role is the (0 - T_ii)^2 term of the MSE
     (cdist's diagonal is 0 and carries no gradient): T'_ii = sqrt(T_ii^2 + sum_j>i (T_ij - T_ji)^2/2).
-    The MSE value and its gradient are unchanged (to fp32 rounding); ``asymmetric_source`` records it.
+    The MSE value and its gradient are unchanged (to fp32 rounding); ``asymmetric_source`` records it
+    and ``scoring()`` keeps the target as given for dSCC (the reference ranks truth[triu] itself).
     The combined loss's Pearson term then sees tbar on the upper triangle (a relative change of
     the order of the asymmetry, 1e-7 for R's rounding)."""
 
@@ -404,7 +405,9 @@ class Truth:
         self.buf, self.n, self.ld = buf, n, buf.shape[1]
         view = buf[:, :n]
         self.asymmetric_source = not bool(torch.equal(view, view.t()))
+        self.raw = None
         if self.asymmetric_source:
+            self.raw = view.clone()     # the target as given: dSCC scores its upper triangle (scoring())
             self._symmetrise()
         self.symmetric = True
         self.support = None
@@ -433,3 +436,8 @@ class Truth:
 
     def dense(self):
         return self.buf[:, :self.n]
+
+    def scoring(self):
+        """The matrix whose upper triangle the reference scores dSCC against (HiC-GNN_main.py:135-139
+        takes truth[triu] as given): the target before symmetrisation when it was asymmetric."""
+        return self.raw if self.raw is not None else self.dense()

@@ -660,14 +660,18 @@ class _FusedLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl):
         (dc,) = ctx.saved_tensors
-        if gl is _UNIT_SEEDS.get(gl.device):   # seeded by backward_from_loss: d(loss) = 1 exactly
+        # seeded by backward_from_loss with its resident ones tensor, never written since (the
+        # version counter catches an in-place change by a hook): d(loss) = 1 exactly
+        if gl is _UNIT_SEEDS.get(gl.device) and gl._version == 0:
             return dc, None, None, None, None, None, None, None
         return dc * gl, None, None, None, None, None, None, None
 
 
 # loss.backward() fills a fresh ones tensor and the loss node then multiplies dcoords by it: two
-# launches per step.  backward_from_loss seeds with one resident ones tensor per device instead (never
-# written), which the loss node recognises by identity and skips the multiply -- the same bits.
+# launches per step.  backward_from_loss seeds with one resident ones tensor per device instead, which
+# the loss node recognises by identity AND an unchanged version counter (any in-place write to it --
+# e.g. by a gradient hook -- bumps ``_version``, and the node then multiplies as usual) and skips
+# the multiply -- the same bits.
 _UNIT_SEEDS = {}
 
 
@@ -675,7 +679,7 @@ def backward_from_loss(loss):
     """``loss.backward()`` for a scalar loss from ``fused_dist_loss``, without the seed fill and the
     dcoords scaling launches."""
     seed = _UNIT_SEEDS.get(loss.device)
-    if seed is None or seed.dtype != loss.dtype:
+    if seed is None or seed.dtype != loss.dtype or seed._version != 0:
         seed = _UNIT_SEEDS[loss.device] = torch.ones((), dtype=loss.dtype, device=loss.device)
     torch.autograd.backward(loss, grad_tensors=seed)
 

@@ -121,7 +121,7 @@ def main(argv=None):
         model = MODELS[a.model]().to(data.x.device)
         _, hist = train(model, data, truth, a.learningrate, a.threshold, a.steps, a.loss)
         coords = model.get_model(data.x.float(), data.edge_index).detach()
-        rho = metrics.dscc(coords, truth.dense())
+        rho = metrics.dscc(coords, truth.scoring())
         print(f"conversion {f}: steps {len(hist)} loss {hist[-1]:.6g} dSCC {rho:.6f}")
         runs.append((rho, f, hist[-1], model, coords))
     k = [r[0] for r in runs].index(max(r[0] for r in runs))     # first maximum, as list.index(max)

@@ -12,6 +12,10 @@ graph_chr19_1mb.npz (the reference's contact matrix) and model_GATNetSelectiveRe
 
     python tests/golden/make_dscc_band.py      # ~5 min on 8 cores
 
+``--seeds`` runs the same pipeline at 1 thread for initial-weight seeds 0..3 and writes
+``dscc_seeds_chr19_1mb.npz``: the summation-order-robust protocol of the GPU test (the mean dSCC
+over the four seeds, which both of the device's aggregation forms must reproduce within +-0.005).
+
 ``--features n2v`` uses the node2vec embedding ``n2v_chr19_1mb.npz`` (tests/golden/make_n2v_chr19.py,
 this repo's GPU node2vec with the reference's parameters) instead of the fixture's random features
 and writes ``dscc_band_chr19_1mb_n2v.npz`` (BASELINE configs[0]: 512-d node2vec).
@@ -34,6 +38,7 @@ from oracle import loop as ol  # noqa: E402
 
 K = 3000
 THREADS = (1, 2, 4, 8)
+SEEDS = (0, 1, 2, 3)
 
 
 def main():
@@ -50,20 +55,28 @@ def main():
     truth = ogr.cont2dist(d["y"], 0.5)
     radj = (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))
     dscc, loss = [], []
+    seeds_mode = "--seeds" in sys.argv
+    runs = [(1, sd) for sd in SEEDS] if seeds_mode else [(th, 0) for th in THREADS]
     og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
     try:
-        for th in THREADS:
+        for th, sd in runs:
             torch.set_num_threads(th)
-            torch.manual_seed(0)
+            torch.manual_seed(sd)
             ref = og.GATNetSelectiveResidualsUpdated()
             t0 = time.time()
             hist = ol.train(ref, d["x"], radj, truth, steps=K)
             with torch.no_grad():
                 dscc.append(ol.dscc(ref.get_model(d["x"], radj), truth))
             loss.append(hist[-1])
-            print(f"threads {th}: dSCC {dscc[-1]:.6f}, loss {loss[-1]:.6e} ({time.time() - t0:.0f} s)", flush=True)
+            print(f"threads {th} seed {sd}: dSCC {dscc[-1]:.6f}, loss {loss[-1]:.6e} ({time.time() - t0:.0f} s)",
+                  flush=True)
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    if seeds_mode:
+        np.savez(os.path.join(HERE, "dscc_seeds_chr19_1mb.npz"), steps=np.int64(K), seeds=np.array(SEEDS),
+                 dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
+                 cpu=np.array(platform.processor() or platform.machine()))
+        return
     np.savez(os.path.join(HERE, "dscc_band_chr19_1mb_n2v.npz" if n2v else "dscc_band_chr19_1mb.npz"), steps=np.int64(K), threads=np.array(THREADS),
              dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
              cpu=np.array(platform.processor() or platform.machine()))

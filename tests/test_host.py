@@ -170,3 +170,29 @@ def test_build_tiles_partitions_the_edges(r0, r1, tmin):
         for cb in range((n + 31) // 32):
             listed = cb in set(tcol[tptr[b]:tptr[b + 1]])
             assert listed == (A[rows, 32 * cb:32 * cb + 32].sum() >= max(tmin, 1))
+
+
+def test_asymmetric_truth_scores_the_raw_upper_triangle():
+    """an asymmetric target (R's KR rounding, r_utils.R:74-89) is stored symmetrised for
+    the fused loss, but dSCC ranks the upper triangle AS GIVEN (HiC-GNN_main.py:135-139)."""
+    import hicgat
+    from scipy.stats import spearmanr
+    rng = np.random.default_rng(5)
+    n = 40
+    t = rng.random((n, n))
+    t = t + t.T
+    t[np.triu_indices(n, 1)] *= 1 + 1e-3 * rng.standard_normal(n * (n - 1) // 2)   # rounding-size asymmetry
+    np.fill_diagonal(t, 0)
+    truth = hicgat.Truth(torch.tensor(t, dtype=torch.float32))
+    assert truth.asymmetric_source
+    d = truth.dense()
+    assert torch.equal(d, d.t())
+    iu = np.triu_indices(n, 1)
+    raw = truth.scoring().numpy()
+    assert np.array_equal(raw[iu], t.astype(np.float32)[iu])
+    c = rng.standard_normal((n, 3))
+    dist = np.linalg.norm(c[:, None] - c[None], axis=-1)[iu]
+    rho_raw = spearmanr(raw[iu], dist)[0]
+    assert rho_raw == spearmanr(t.astype(np.float32)[iu], dist)[0]
+    sym = hicgat.Truth(torch.tensor(t + t.T, dtype=torch.float32))
+    assert not sym.asymmetric_source and sym.scoring() is not None and torch.equal(sym.scoring(), sym.dense())

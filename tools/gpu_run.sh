@@ -15,7 +15,9 @@
 #   pmc_mfma     one PMC pass (MFMA busy cycles, F32 MFMA MOPs, GRBM_GUI_ACTIVE) -> <tag>_pmc_mfma.json
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
 #   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world)
+#   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
+#   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
 #   cli          the reference driver's flow (python -m hicgat.train) on chr19 1 mb with GPU node2vec
 #                features, the default conversion sweep, 1000 steps each -> gpurun_out/<tag>_cli/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -75,9 +77,17 @@ for S in "$@"; do
           2> gpurun_out/${T}_simrank_P$P.err || exit $?
         python -c "import json;d=json.loads(open('gpurun_out/${T}_simrank_P$P.json').read().strip().splitlines()[-1]);print('P=$P', d['simulated']['rank_ms'], d['simulated']['model_ms_per_step'])"
       done ;;
+    simprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_simprof -o run --output-format csv -- \
+        python bench.py --simulate-world 8 --sim-rank 0 --steps 20 --warmup 3 > gpurun_out/${T}_simprof.log 2>&1 || exit $?
+      python tools/step_timeline.py gpurun_out/${T}_simprof/run_kernel_trace.csv 10 > gpurun_out/${T}_simprof_timeline.txt || exit $?
+      echo "simprof ok" ;;
     align)
       timeout -k 10 600 python tools/run_config5.py gpurun_out/${T}_align > gpurun_out/${T}_align.log 2>&1; rc=$?
       tail -8 gpurun_out/${T}_align.log; [ $rc -eq 0 ] || exit $rc ;;
+    n2v)
+      timeout -k 10 900 python tools/n2v_study.py gpurun_out/${T}_n2v_study.json > gpurun_out/${T}_n2v_study.log 2>&1; rc=$?
+      tail -12 gpurun_out/${T}_n2v_study.log; [ $rc -eq 0 ] || exit $rc ;;
     cli)
       mkdir -p gpurun_out/${T}_cli
       python -c "import numpy as np; d = np.load('tests/golden/graph_chr19_1mb.npz'); np.savetxt('gpurun_out/${T}_cli/GM12878_1mb_chr19_list.txt', d['list'], fmt='%d\t%d\t%.6f')" || exit 1

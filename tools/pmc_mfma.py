@@ -29,6 +29,11 @@ def _name(s):
     return s.split("(")[0].replace("void ", "").strip()
 
 
+def _key(row):
+    """kernel name + grid size: one kernel template serves several GEMM shapes per step."""
+    return f"{_name(row['Kernel_Name'])} grid={row['Grid_Size']}"
+
+
 def summarise(ctr_csv):
     per = collections.defaultdict(lambda: collections.defaultdict(dict))   # name -> dispatch -> counter
     dur = collections.defaultdict(dict)
@@ -36,7 +41,7 @@ def summarise(ctr_csv):
         for row in csv.DictReader(f):
             if row["Counter_Name"] not in CTRS:
                 continue
-            name = _name(row["Kernel_Name"])
+            name = _key(row)
             d = int(row["Dispatch_Id"])
             per[name][d][row["Counter_Name"]] = per[name][d].get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
             dur[name][d] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
@@ -55,11 +60,20 @@ def summarise(ctr_csv):
     return out
 
 
+def _src_hash():
+    """bench.kernel_src_hash(): which kernel sources these counters were recorded with."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_src_hash
+    return kernel_src_hash()
+
+
 if __name__ == "__main__":
     res = summarise(sys.argv[1])
     doc = {"workload": sys.argv[4] if len(sys.argv) > 4 else "synth-20000",
            "command": sys.argv[5] if len(sys.argv) > 5 else None,
            "commit": sys.argv[6] if len(sys.argv) > 6 else None,
+           "src_hash": _src_hash(),
            "formulas": {"flop": "SQ_INSTS_VALU_MFMA_MOPS_F32 * 512",
                         "mfma_busy": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024)",
                         "clock_ghz": "GRBM_GUI_ACTIVE / 8 / duration"},
@@ -68,5 +82,5 @@ if __name__ == "__main__":
         with open(sys.argv[3], "w") as f:
             f.write(json.dumps(doc, indent=1) + "\n")
     for k, v in sorted(doc["kernels"].items(), key=lambda kv: -kv[1]["flop"] * kv[1]["dispatches"]):
-        print(f"{k[:60]:60s} n={v['dispatches']:3d} GF={v['flop'] / 1e9:7.2f} t={v['duration_s'] * 1e6:7.1f}us "
+        print(f"{k[:90]:90s} n={v['dispatches']:3d} GF={v['flop'] / 1e9:7.2f} t={v['duration_s'] * 1e6:7.1f}us "
               f"TF={v['tflops_pmc']:6.1f} busy={v['mfma_busy']:.3f} clk={v['clock_ghz']:.2f}")

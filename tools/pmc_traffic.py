@@ -40,11 +40,20 @@ def summarise(fetch_csv, write_csv):
     return out
 
 
+def _src_hash():
+    """bench.kernel_src_hash(): which kernel sources these counters were recorded with."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_src_hash
+    return kernel_src_hash()
+
+
 if __name__ == "__main__":
     res = summarise(sys.argv[1], sys.argv[2])
     text = json.dumps({"workload": sys.argv[4] if len(sys.argv) > 4 else "synth-20000",
                        "command": sys.argv[5] if len(sys.argv) > 5 else None,
                        "commit": sys.argv[6] if len(sys.argv) > 6 else None,
+                       "src_hash": _src_hash(),
                        "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
                        "kernels": res}, indent=1)
     if len(sys.argv) > 3:
