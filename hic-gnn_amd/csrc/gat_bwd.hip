@@ -130,7 +130,11 @@ __device__ __forceinline__ void agg_bwd_src_row(
 // Persistent when the grid is smaller than the row-block count (HICGAT_SRC_WGS per CU): each
 // workgroup walks row blocks b, b + gridDim.x, ... (the same XCD for all of them), so the CUs keep
 // free slots for the parameter-gradient GEMMs the side stream runs beside this pass.
-template <bool SPLIT = false, bool PERSIST = false>
+// REMAP: the XCD-aware block order (each XCD a contiguous row range: the rows of a banded Hi-C
+// neighbourhood share that XCD's L2).  Off (plain round-robin over the XCDs) for the multi-GPU "slab"
+// pass, whose heavy rows -- the rank's own diagonal block -- are contiguous: under the remap they
+// would all land on one XCD.
+template <bool SPLIT = false, bool PERSIST = false, bool REMAP = true>
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     float *__restrict__ dh, float *__restrict__ da_src) {
   const int nblk = (row_end - row_begin + 3) / 4;
   if constexpr (!PERSIST) {
-    const int r = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+    const int r = row_begin + (REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wave_in_block();
     if (r < row_end)
       agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh,
                              da_src);
@@ -437,6 +441,32 @@ extern "C" int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *c
   HICGAT_SRC_LAUNCH(false, rows,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
                      row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *col, int N, int H,
+                                         int C, int row_begin, int row_end, const float *h,
+                                         const float *a_src, const float *a_dst,
+                                         const float *row_stats, int64_t ld_stats, const float *dout,
+                                         int64_t ld_dout, const float *att_src, const float *att_dst,
+                                         float neg_slope, float *dh, float *da_src, int flags,
+                                         hicgat_stream_t stream) {
+  if (!(flags & HICGAT_SRC_ROUND_ROBIN))
+    return hicgat_gat_agg_bwd_src_ld(rowptr, col, N, H, C, row_begin, row_end, h, a_src, a_dst, row_stats, ld_stats,
+                                     dout, ld_dout, att_src, att_dst, neg_slope, dh, da_src, stream);
+  if (flags & ~HICGAT_SRC_ROUND_ROBIN) return HICGAT_EINVAL;
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (ld_stats < 4 * H || ld_stats % 4 || ld_dout < H * C || ld_dout % 4) return HICGAT_EINVAL;
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !h || !a_src || !a_dst || !row_stats || !dout || !att_src || !att_dst ||
+      !dh || !da_src)
+    return HICGAT_EINVAL;
+  const int rows = row_end - row_begin;
+  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<false, false, false>), dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst, row_stats, ld_stats, dout,
+                     ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

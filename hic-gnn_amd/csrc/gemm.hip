@@ -531,9 +531,13 @@ static bool tall_enabled() {
   return on;
 }
 
-// HICGAT_TALL_MIN_TILES (A/B): problems with fewer 160x128 tiles than this go to the 64x128 kernel
+// Problems with fewer 160x128 tiles than this go to the 64x128 kernel (2.5x the workgroups): one
+// workgroup per tile with the whole K inside, the tall kernel needs ~one tile per CU -- a rank's
+// 2700-row shard of a multi-GPU step is 68 tiles, a quarter of the chip (57 vs 98 us for 7x fewer
+// FLOP than the 20000-row GEMM).  The single-GPU shapes (>= 250 tiles) keep the tall kernel.
+// HICGAT_TALL_MIN_TILES overrides (A/B).
 static int64_t tall_min_tiles() {
-  static const int64_t v = getenv("HICGAT_TALL_MIN_TILES") ? atoll(getenv("HICGAT_TALL_MIN_TILES")) : 0;
+  static const int64_t v = getenv("HICGAT_TALL_MIN_TILES") ? atoll(getenv("HICGAT_TALL_MIN_TILES")) : 192;
   return v;
 }
 

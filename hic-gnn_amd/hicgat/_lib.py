@@ -36,6 +36,8 @@ SIGNATURES = {
                                         c_i64, c_p, c_p]),
     "hicgat_gat_agg_bwd_src_ld": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                           c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_p]),
+    "hicgat_gat_agg_bwd_src_ex": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                          c_i64, c_p, c_i64, c_p, c_p, c_f, c_p, c_p, c_int, c_p]),
     "hicgat_gat_agg_bwd_src": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_f, c_p, c_p, c_p]),
     "hicgat_gat_agg_fwd_tiled": (c_int, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,

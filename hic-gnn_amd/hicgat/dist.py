@@ -410,13 +410,14 @@ class ShardedTrainer:
             # source pass over every row r, restricted to the neighbours this rank owns: partial
             # dh_r / da_src_r (complete when summed over ranks -- through dW and datt below)
             K.agg_bwd_src(self.rowptr_s, self.col_s, 0, N, self.h, a_src, a_dst, self.rs, dout, al, ar, self.ns,
-                          self.dh, self.da_src)
+                          self.dh, self.da_src, round_robin=True)
             ops.side_flush(after=fork)
             tail_done = self._side_event()
             with torch.no_grad():
-                # lin_l's partial dW over all rows (x replicated) on the side stream, the GAT
-                # parameter column sums beside it on this stream
-                with ops._side(self.dh, self.x):
+                # lin_l's partial dW over all rows (x replicated) on a side stream of its own (lane 2:
+                # beside the tail's dW GEMMs on lane 0, not queued behind them), the GAT parameter
+                # column sums beside it on this stream
+                with ops._side(self.dh, self.x, lane=2):
                     if self.cuda:
                         weight_grad(K, self.dh, self.x, out=self.W.grad, accumulate=True)
                     else:

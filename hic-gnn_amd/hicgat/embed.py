@@ -99,9 +99,9 @@ def initial_vectors(walks, n_words, dimensions, w2v_seed=1):
 def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, alpha=0.025, min_alpha=1e-4,
              sample=1e-3, seed=42, max_waves=None, w2v_seed=1):
     """Word2Vec(sg=1, hs=0) over the walks: returns the input vectors syn0 [n_words, dimensions].
-    ``max_waves`` bounds the walks trained concurrently (default n_words // 4, within [8, 4096]):
-    on a Hi-C-sized vocabulary (58 loci for chr19 1 mb) thousands of concurrent Hogwild writers
-    to the same rows would lose most updates."""
+    ``max_waves`` bounds the walks trained concurrently (default n_words // 64, within [1, 4096]):
+    on a Hi-C-sized vocabulary (58 loci for chr19 1 mb) concurrent Hogwild writers to the same
+    rows would lose updates, so small vocabularies train sequentially."""
     lib = _lib.lib()
     dev = walks.device
     nwalks, L = walks.shape
@@ -113,7 +113,11 @@ def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, al
     syn1 = torch.zeros_like(syn0)
     st = _lib.stream(dev)
     if max_waves is None:
-        max_waves = min(4096, max(8, n_words // 4))
+        # at most one concurrent walk per 64 words: sequential, like the reference's workers=1, for
+        # a Hi-C chromosome at 1 mb / 500 kb (58 / 114 loci); measured on chr19 1 mb, 1 vs 14
+        # concurrent walks give the same embedding structure (common-component share 0.984 vs
+        # 0.980, profiles/r03b_n2v_study.json) at 20 vs 5 s
+        max_waves = max(1, min(4096, n_words // 64))
     for ep in range(epochs):
         _lib.check(lib.hicgat_n2v_sgns_epoch(P(walks), nwalks, L, P(t_keep), P(t_cum), n_words, dimensions, window,
                                              negative, float(alpha), float(min_alpha), ep, epochs,

@@ -158,18 +158,23 @@ class HipKernels:
                                                        P(a_dst), P(dout), float(ns), P(row_stats),
                                                        _lib.stream(h.device)), "hicgat_gat_agg_bwd_dst")
 
-    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src):
+    SRC_ROUND_ROBIN = 1   # include/hicgat.h HICGAT_SRC_ROUND_ROBIN
+
+    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src,
+                    round_robin=False):
+        """``round_robin``: row blocks spread over the XCDs (the multi-GPU slab pass, hicgat.dist)."""
         N = h.shape[0]
         H = a_src.shape[1]
         C = h.shape[1] // H
         # row_stats / dout may be row-strided views (the packed all-gather buffer of hicgat.dist)
         assert row_stats.stride(1) == 1 and dout.stride(1) == 1
         with _timed("gat_agg_bwd_src"):
-            _lib.check(self.lib.hicgat_gat_agg_bwd_src_ld(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
+            _lib.check(self.lib.hicgat_gat_agg_bwd_src_ex(P(rowptr), P(col), N, H, C, r0, r1, P(h), P(a_src),
                                                           P(a_dst), P(row_stats), row_stats.stride(0), P(dout),
                                                           dout.stride(0), P(att_l), P(att_r), float(ns), P(dh),
-                                                          P(da_src), _lib.stream(h.device)),
-                       "hicgat_gat_agg_bwd_src_ld")
+                                                          P(da_src), self.SRC_ROUND_ROBIN if round_robin else 0,
+                                                          _lib.stream(h.device)),
+                       "hicgat_gat_agg_bwd_src_ex")
 
     def param_grad(self, h, dout, da_src, row_stats, H, out=None, accumulate=False):
         """Column sums over the given rows -> (datt_src [D], datt_dst [D], dbias [D]); ``out`` =

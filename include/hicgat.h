@@ -129,6 +129,15 @@ int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *col, int N, 
                               const float *dout, int64_t ld_dout, const float *att_src,
                               const float *att_dst, float neg_slope, float *dh, float *da_src,
                               hicgat_stream_t stream);
+/* The same with launch flags: HICGAT_SRC_ROUND_ROBIN spreads consecutive row blocks over the XCDs
+ * instead of giving each XCD a contiguous row range (the multi-GPU "slab" pass, hicgat.dist, whose
+ * heavy rows are one contiguous block); flags 0 = hicgat_gat_agg_bwd_src_ld. */
+enum { HICGAT_SRC_ROUND_ROBIN = 1 };
+int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *col, int N, int H, int C, int row_begin,
+                              int row_end, const float *h, const float *a_src, const float *a_dst,
+                              const float *row_stats, int64_t ld_stats, const float *dout, int64_t ld_dout,
+                              const float *att_src, const float *att_dst, float neg_slope, float *dh, float *da_src,
+                              int flags, hicgat_stream_t stream);
 /* ---- a4+a5 and the source pass with the dense tiles on the matrix cores (gat_tiles.hip) -------
  * The same results as hicgat_gat_agg_fwd_act / hicgat_gat_agg_bwd_src_ld (fp32; the tiles' sums are
  * added in another order), with the edge set split in two:

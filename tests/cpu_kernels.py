@@ -127,7 +127,8 @@ class CpuKernels:
         row_stats[r0:r1, 2 * H:3 * H] = s1.float()
         row_stats[r0:r1, 3 * H:4 * H] = (s2 - s1 * s3).float()
 
-    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src):
+    def agg_bwd_src(self, rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, att_l, att_r, ns, dh, da_src,
+                    round_robin=False):
         H = a_src.shape[1]
         C = h.shape[1] // H
         r, ei = _rows(rowptr, r0, r1)

@@ -1,0 +1,104 @@
+"""Generate ``config5_band_chr19.npz``: BASELINE configs[4] (train on GM12878 chr19 1 mb, generalise
+to 500 kb) through the CPU oracle at a fixed step count, at 1, 2, 4 and 8 threads and for
+initial-weight seeds 0..3 (1 thread).
+
+Pipeline (HiC_GAT_generalize_directly.py): KR-normalise both zero-diagonal contact matrices
+(r_utils.R restated, oracle.kr), load_input(normed_1mb, emb1), truth = cont2dist(y, 1) (:101,198),
+the flagship trained with the COMBINED loss (mse + alpha (1 - pearson), :206-239) for K fixed steps
+(the threshold stop is chaotic), then the generalisation (:312-336):
+domain_alignment(list_1mb, list_500kb, emb1, emb2) (utils.py:83-109, scipy Procrustes),
+load_input(normed_500kb, fitembed), get_model, dSCC against cont2dist(y_500kb, 1).
+
+Features: the seeded 512-d embeddings of the alignment fixture (``align_chr19_f512.npz``, x 0.1 to
+the node2vec scale), since node2vec / gensim are absent.  Test infrastructure only
+(it runs the oracle under oracle/); tests/test_gpu_parity.py::test_config5_generalisation_matches_oracle
+runs the same pipeline on the device.
+
+    python tests/golden/make_config5_band.py      # ~4 min on 8 cores
+"""
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import align as oal  # noqa: E402
+from oracle import gat as og  # noqa: E402
+from oracle import graph as ogr  # noqa: E402
+from oracle import kr as okr  # noqa: E402
+from oracle import loop as ol  # noqa: E402
+
+K = 1000
+THREADS = (1, 2, 4, 8)
+SEEDS = (0, 1, 2, 3)
+FEATURE_SCALE = 0.1
+
+
+def load():
+    def z(name):
+        with np.load(os.path.join(HERE, name), allow_pickle=False) as f:
+            return {k: f[k] for k in f.files}
+    al = z("align_chr19_f512.npz")
+    g1, g5 = z("graph_chr19_1mb.npz"), z("graph_chr19_500kb.npz")
+    return al, g1, g5
+
+
+def prepare():
+    al, g1, g5 = load()
+    e1 = (FEATURE_SCALE * al["emb1"]).astype(np.float32)
+    e2 = (FEATURE_SCALE * al["emb2"]).astype(np.float32)
+    out = {"list1": al["list1"], "list2": al["list2"], "e1": e1, "e2": e2}
+    for tag, g in (("1mb", g1), ("500kb", g5)):
+        a = np.array(g["matrix"], dtype=np.float64)
+        np.fill_diagonal(a, 0)
+        normed, keep = okr.krnorm(a.copy())
+        assert len(keep) == a.shape[0], "chr19 loci are all kept by KR"
+        out[tag] = normed
+    return out
+
+
+def run(inp, seed, threads):
+    torch.set_num_threads(threads)
+    d1 = ogr.load_input(inp["1mb"].copy(), inp["e1"])
+    truth = ogr.cont2dist(d1["y"], 1)
+    radj = (torch.tensor(d1["rowptr"]), torch.tensor(d1["col"]))
+    torch.manual_seed(seed)
+    ref = og.GATNetSelectiveResidualsUpdated()
+    hist = ol.train(ref, d1["x"], radj, truth, steps=K, loss="combined")
+    fit, _, _, _ = oal.domain_alignment(inp["list1"], inp["list2"], inp["e1"], inp["e2"])
+    d5 = ogr.load_input(inp["500kb"].copy(), fit.astype(np.float32))
+    t5 = ogr.cont2dist(d5["y"], 1)
+    with torch.no_grad():
+        c5 = ref.get_model(d5["x"], (torch.tensor(d5["rowptr"]), torch.tensor(d5["col"])))
+        c1 = ref.get_model(d1["x"], radj)
+    return ol.dscc(c5, t5), ol.dscc(c1, truth), hist[-1]
+
+
+def main():
+    inp = prepare()
+    rows = []
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        runs = [(th, 0) for th in THREADS] + [(1, sd) for sd in SEEDS if sd != 0]
+        for th, sd in runs:
+            t0 = time.time()
+            g, t, loss = run(inp, sd, th)
+            rows.append((th, sd, g, t, loss))
+            print(f"threads {th} seed {sd}: generalised dSCC {g:.6f}, trained dSCC {t:.6f}, loss {loss:.6e} "
+                  f"({time.time() - t0:.0f} s)", flush=True)
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    r = np.array(rows, dtype=np.float64)
+    np.savez(os.path.join(HERE, "config5_band_chr19.npz"), steps=np.int64(K), threads=r[:, 0].astype(np.int64),
+             seeds=r[:, 1].astype(np.int64), dscc_generalised=r[:, 2], dscc_trained=r[:, 3], loss=r[:, 4],
+             feature_scale=np.float64(FEATURE_SCALE), torch=np.array(torch.__version__),
+             cpu=np.array(platform.processor() or platform.machine()))
+
+
+if __name__ == "__main__":
+    main()

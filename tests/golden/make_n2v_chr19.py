@@ -7,7 +7,8 @@ diagonal).  BASELINE configs[0] names "512-d node2vec" features; node2vec / gens
 so the same embedding file is then fed to BOTH sides: the CPU oracle (make_dscc_band.py --features
 n2v) and the device pipeline (tests/test_gpu_parity.py::test_dscc_chr19_1mb_node2vec_matches_oracle).
 
-Needs the GPU:  python tests/golden/make_n2v_chr19.py [out.npz]
+Needs the GPU:  python tests/golden/make_n2v_chr19.py [out.npz [seed]]
+(seed 43: ``n2v_chr19_1mb_s43.npz``, the second seed of the collapse check)
 """
 import os
 import sys
@@ -21,12 +22,13 @@ sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "..",
 def main():
     from hicgat.embed import node2vec
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "n2v_chr19_1mb.npz")
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 42
     with np.load(os.path.join(HERE, "graph_chr19_1mb.npz"), allow_pickle=False) as z:
         a = np.array(z["matrix"], dtype=np.float64)
     np.fill_diagonal(a, 0)
-    x = node2vec(a, seed=42).cpu().numpy().astype(np.float32)
+    x = node2vec(a, seed=seed).cpu().numpy().astype(np.float32)
     assert x.shape == (a.shape[0], 512) and np.isfinite(x).all()
-    np.savez(out, x=x, seed=np.int64(42))
+    np.savez(out, x=x, seed=np.int64(seed))
     print(f"node2vec chr19 1mb: {x.shape}, |x| mean {np.abs(x).mean():.4f} -> {out}")
 
 

@@ -14,10 +14,11 @@
 #   pmc_traffic  two PMC passes (FETCH_SIZE, WRITE_SIZE) of an eager bench -> <tag>_pmc_traffic.json
 #   pmc_mfma     one PMC pass (MFMA busy cycles, F32 MFMA MOPs, GRBM_GUI_ACTIVE) -> <tag>_pmc_mfma.json
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
-#   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world)
+#   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world; _ag: allgather form)
 #   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
 #   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
+#   n2vfix       node2vec embeddings of chr19 1 mb, seeds 43 and 42 (fixtures for the oracle collapse check)
 #   cli          the reference driver's flow (python -m hicgat.train) on chr19 1 mb with GPU node2vec
 #                features, the default conversion sweep, 1000 steps each -> gpurun_out/<tag>_cli/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -71,23 +72,28 @@ for S in "$@"; do
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json $W \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager" \
         "$COMMIT" || exit $? ;;
-    simrank)
+    simrank|simrank_ag)
+      M=slab; [ "$S" = simrank_ag ] && M=allgather
       for P in 2 4 8; do
-        timeout -k 10 240 python bench.py --simulate-world $P --steps 50 --warmup 5 > gpurun_out/${T}_simrank_P$P.json \
-          2> gpurun_out/${T}_simrank_P$P.err || exit $?
-        python -c "import json;d=json.loads(open('gpurun_out/${T}_simrank_P$P.json').read().strip().splitlines()[-1]);print('P=$P', d['simulated']['rank_ms'], d['simulated']['model_ms_per_step'])"
+        timeout -k 10 240 python bench.py --simulate-world $P --dist-mode $M --steps 50 --warmup 5 \
+          > gpurun_out/${T}_simrank_${M}_P$P.json 2> gpurun_out/${T}_simrank_${M}_P$P.err || exit $?
+        python -c "import json;d=json.loads(open('gpurun_out/${T}_simrank_${M}_P$P.json').read().strip().splitlines()[-1]);print('$M P=$P', [round(v,4) for v in d['simulated']['rank_ms']], round(d['simulated']['model_ms_per_step'],4))"
       done ;;
-    simprof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_simprof -o run --output-format csv -- \
-        python bench.py --simulate-world 8 --sim-rank 0 --steps 20 --warmup 3 > gpurun_out/${T}_simprof.log 2>&1 || exit $?
-      python tools/step_timeline.py gpurun_out/${T}_simprof/run_kernel_trace.csv 10 > gpurun_out/${T}_simprof_timeline.txt || exit $?
-      echo "simprof ok" ;;
+    simprof|simprof_ag)
+      M=slab; [ "$S" = simprof_ag ] && M=allgather
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \
+        python bench.py --simulate-world 8 --sim-rank 0 --dist-mode $M --steps 20 --warmup 3 > gpurun_out/${T}_${S}.log 2>&1 || exit $?
+      python tools/step_timeline.py gpurun_out/${T}_${S}/run_kernel_trace.csv 10 > gpurun_out/${T}_${S}_timeline.txt || exit $?
+      echo "$S ok" ;;
     align)
       timeout -k 10 600 python tools/run_config5.py gpurun_out/${T}_align > gpurun_out/${T}_align.log 2>&1; rc=$?
       tail -8 gpurun_out/${T}_align.log; [ $rc -eq 0 ] || exit $rc ;;
     n2v)
       timeout -k 10 900 python tools/n2v_study.py gpurun_out/${T}_n2v_study.json > gpurun_out/${T}_n2v_study.log 2>&1; rc=$?
       tail -12 gpurun_out/${T}_n2v_study.log; [ $rc -eq 0 ] || exit $rc ;;
+    n2vfix)
+      timeout -k 10 300 python tests/golden/make_n2v_chr19.py gpurun_out/${T}_n2v_chr19_1mb_s43.npz 43 || exit $?
+      timeout -k 10 300 python tests/golden/make_n2v_chr19.py gpurun_out/${T}_n2v_chr19_1mb_s42.npz 42 || exit $? ;;
     cli)
       mkdir -p gpurun_out/${T}_cli
       python -c "import numpy as np; d = np.load('tests/golden/graph_chr19_1mb.npz'); np.savetxt('gpurun_out/${T}_cli/GM12878_1mb_chr19_list.txt', d['list'], fmt='%d\t%d\t%.6f')" || exit 1
