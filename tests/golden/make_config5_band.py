@@ -9,6 +9,9 @@ the flagship trained with the COMBINED loss (mse + alpha (1 - pearson), :206-239
 domain_alignment(list_1mb, list_500kb, emb1, emb2) (utils.py:83-109, scipy Procrustes),
 load_input(normed_500kb, fitembed), get_model, dSCC against cont2dist(y_500kb, 1).
 
+The file also holds the 1-thread seed-0 TRAINED weights ("w:<state_dict key>"), so the device's
+generalisation of the oracle's own trained model is checked without training chaos.
+
 Features: the seeded 512-d embeddings of the alignment fixture (``align_chr19_f512.npz``, x 0.1 to
 the node2vec scale), since node2vec / gensim are absent.  Test infrastructure only
 (it runs the oracle under oracle/); tests/test_gpu_parity.py::test_config5_generalisation_matches_oracle
@@ -76,18 +79,22 @@ def run(inp, seed, threads):
     with torch.no_grad():
         c5 = ref.get_model(d5["x"], (torch.tensor(d5["rowptr"]), torch.tensor(d5["col"])))
         c1 = ref.get_model(d1["x"], radj)
-    return ol.dscc(c5, t5), ol.dscc(c1, truth), hist[-1]
+    return ol.dscc(c5, t5), ol.dscc(c1, truth), hist[-1], {k: v.detach().numpy().copy() for k, v in
+                                                            ref.state_dict().items()}
 
 
 def main():
     inp = prepare()
     rows = []
+    weights = None
     og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
     try:
         runs = [(th, 0) for th in THREADS] + [(1, sd) for sd in SEEDS if sd != 0]
         for th, sd in runs:
             t0 = time.time()
-            g, t, loss = run(inp, sd, th)
+            g, t, loss, sd_w = run(inp, sd, th)
+            if th == 1 and sd == 0:
+                weights = sd_w        # the 1-thread seed-0 trained model: the teacher-forced check
             rows.append((th, sd, g, t, loss))
             print(f"threads {th} seed {sd}: generalised dSCC {g:.6f}, trained dSCC {t:.6f}, loss {loss:.6e} "
                   f"({time.time() - t0:.0f} s)", flush=True)
@@ -97,7 +104,8 @@ def main():
     np.savez(os.path.join(HERE, "config5_band_chr19.npz"), steps=np.int64(K), threads=r[:, 0].astype(np.int64),
              seeds=r[:, 1].astype(np.int64), dscc_generalised=r[:, 2], dscc_trained=r[:, 3], loss=r[:, 4],
              feature_scale=np.float64(FEATURE_SCALE), torch=np.array(torch.__version__),
-             cpu=np.array(platform.processor() or platform.machine()))
+             cpu=np.array(platform.processor() or platform.machine()),
+             **{"w:" + k: v for k, v in weights.items()})
 
 
 if __name__ == "__main__":

@@ -86,8 +86,23 @@ for S in "$@"; do
       python tools/step_timeline.py gpurun_out/${T}_${S}/run_kernel_trace.csv 10 > gpurun_out/${T}_${S}_timeline.txt || exit $?
       echo "$S ok" ;;
     align)
-      timeout -k 10 600 python tools/run_config5.py gpurun_out/${T}_align > gpurun_out/${T}_align.log 2>&1; rc=$?
-      tail -8 gpurun_out/${T}_align.log; [ $rc -eq 0 ] || exit $rc ;;
+      # python -m hicgat.align (HiC_GAT_generalize_directly.py's flow) on GM12878 chr19 1 mb -> 500 kb,
+      # 1000 fixed steps of the combined loss: (a) node2vec features made on the GPU (the reference's
+      # configuration), (b) the alignment fixture's seeded embeddings x 0.1 (the GPU test's inputs)
+      D=gpurun_out/${T}_align; mkdir -p $D
+      python -c "
+import numpy as np
+a = np.load('tests/golden/align_chr19_f512.npz')
+np.savetxt('$D/GM12878_1mb_chr19_list.txt', np.load('tests/golden/graph_chr19_1mb.npz')['list'], fmt='%d\t%d\t%.6f')
+np.savetxt('$D/GM12878_500kb_chr19_list.txt', np.load('tests/golden/graph_chr19_500kb.npz')['list'], fmt='%d\t%d\t%.6f')
+np.savetxt('$D/emb_1mb.txt', 0.1 * a['emb1'].astype(np.float64), fmt='%.9g')
+np.savetxt('$D/emb_500kb.txt', 0.1 * a['emb2'].astype(np.float64), fmt='%.9g')" || exit 1
+      (cd hic-gnn_amd && timeout -k 10 400 python -m hicgat.align ../$D/GM12878_1mb_chr19_list.txt ../$D/GM12878_500kb_chr19_list.txt \
+        node2vec node2vec --steps 1000 --weights ../$D/n2v_weights.pt --out ../$D/n2v_GM12878_500kb_chr19 > ../$D/run_node2vec.log 2>&1) || exit $?
+      (cd hic-gnn_amd && timeout -k 10 400 python -m hicgat.align ../$D/GM12878_1mb_chr19_list.txt ../$D/GM12878_500kb_chr19_list.txt \
+        ../$D/emb_1mb.txt ../$D/emb_500kb.txt --steps 1000 --weights ../$D/fix_weights.pt --out ../$D/fix_GM12878_500kb_chr19 \
+        > ../$D/run_fixture.log 2>&1) || exit $?
+      tail -2 $D/run_node2vec.log $D/run_fixture.log ;;
     n2v)
       timeout -k 10 900 python tools/n2v_study.py gpurun_out/${T}_n2v_study.json > gpurun_out/${T}_n2v_study.log 2>&1; rc=$?
       tail -12 gpurun_out/${T}_n2v_study.log; [ $rc -eq 0 ] || exit $rc ;;
