@@ -376,7 +376,7 @@ def main():
                     choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
                     help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
                          "N > 1 shards the GAT models only")
-    ap.add_argument("--dist-mode", default="slab", choices=["slab", "allgather"],
+    ap.add_argument("--dist-mode", default="slab", choices=["slab", "xagg", "allgather"],
                     help="N > 1: the slab form (default: x replicated, h recomputed per rank, source pass split by "
                          "destination owner -- no h / dout all-gathers) or the all-gather of h before the layer")
     ap.add_argument("--simulate-world", type=int, default=0,

@@ -1,0 +1,379 @@
+// GATConv (H = 2, C = 256, F = 512) in AGGREGATE-FIRST order, for the multi-GPU "xagg" step form
+// (hicgat.dist).  The reference computes h = x W^T for every node and aggregates h (PyG 1.7.2
+// GATConv.forward / propagate, models.py:619); by linearity the same layer is
+//   out_i^h = W_h (sum_j alpha_ij^h x_j) + b^h = W_h xa_i^h + b^h,
+//   a_src_j^h = <att_src^h, W_h x_j> = <W_h^T att_src^h, x_j>        (a_dst likewise),
+// so a rank that owns destination rows i needs no h of any other row: it aggregates the (constant,
+// replicated) input rows x_j, and every GEMM runs on its own rows only.  The backward follows the
+// same algebra (d alpha_ij = <dout_i^h, W_h x_j> = <dxa_i^h, x_j> with dxa_i^h = dout_i^h W_h):
+//   dW_h   = sum_i dout_i^h xa_i^h^T + att_src^h g_src^h^T + att_dst^h g_dst^h^T,
+//   g_src^h = sum_j da_src_j^h x_j,   g_dst^h = sum_i da_dst_i^h x_i,
+//   datt_src^h = W_h g_src^h,  datt_dst^h = W_h g_dst^h,
+// every term a sum over the rank's rows (or its edges) -- partial sums the gradient all-reduce adds.
+// Same values as the h-first order up to fp32 reassociation (tests/test_dist_gloo.py,
+// tests/test_gpu_dist.py).
+//
+// Kernels (one wave per row, wave64, no atomics):
+//   xagg_vec_kernel     v = [W_0^T att_src^0, W_1^T att_src^1, W_0^T att_dst^0, W_1^T att_dst^1] [4, 512]
+//   xagg_logits_kernel  a_src / a_dst [N, 2] = x . v (every row: the rank's neighbours are anywhere)
+//   xagg_fwd_kernel     own rows: softmax stats, then ONE gather pass over x_j accumulating
+//                       xa^h = sum alpha x_j and xa2^h = sum alpha lrelu' x_j for both heads
+//                       (S3 into row_stats as the h-first training form does, gat_fwd.hip)
+//   xagg_bias_relu      y0 += bias, o = relu(y0)      (after the [xa; xa2] W_h^T GEMMs)
+//   xagg_edge_kernel    own rows: per edge ds_ij^h = alpha lrelu' (<dxa_i^h, x_j> - delta_i^h)
+//                       written in the rank's CSR order
+//   xagg_slab_sum       every row j: da_src_j = sum of ds over the rank's edges (i, j), read
+//                       through the column slab (the transpose, by a precomputed permutation)
+//   xagg_param_finish   dW += att (x) g terms, datt_src / datt_dst = W_h g
+#include "common.hpp"
+
+#ifndef HICGAT_XAGG_U
+#define HICGAT_XAGG_U 4   // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
+#endif
+
+namespace hicgat {
+
+// ---- v [4][512]: block b = (which, 256-column half); thread k sums 256 weights of its column ---
+__global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__ W, const float *__restrict__ att_s,
+                                                       const float *__restrict__ att_d, float *__restrict__ v) {
+  const int which = blockIdx.x >> 1;                 // 0, 1: att_src heads 0, 1; 2, 3: att_dst heads 0, 1
+  const int k = (blockIdx.x & 1) * 256 + threadIdx.x;
+  const int hd = which & 1;
+  const float *att = (which < 2 ? att_s : att_d) + hd * 256;
+  const float *w = W + (size_t)hd * 256 * 512 + k;
+  float s = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < 256; ++c) s = fmaf(att[c], w[(size_t)c * 512], s);
+  v[which * 512 + k] = s;
+}
+
+// ---- a_src / a_dst for every row: lane l holds float4 #l and #64+l of x_n and of each v --------
+__global__ __launch_bounds__(256) void xagg_logits_kernel(const float *__restrict__ x, const float *__restrict__ v,
+                                                          int N, float *__restrict__ a_src, float *__restrict__ a_dst) {
+  const int lane = lane_id();
+  const int n = blockIdx.x * 4 + wave_in_block();
+  if (n >= N) return;
+  const float4 *x4 = reinterpret_cast<const float4 *>(x) + (size_t)n * 128;
+  const float4 *v4 = reinterpret_cast<const float4 *>(v);
+  const float4 xa = x4[lane], xb = x4[64 + lane];
+  float r[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) r[w] = f4_dot(xa, v4[w * 128 + lane]) + f4_dot(xb, v4[w * 128 + 64 + lane]);
+  transpose_reduce<4>(r, lane);   // lane 0: r0, 16: r1, 32: r2, 48: r3
+  const float s0 = readlane_f(r[0], 0), s1 = readlane_f(r[0], 16);
+  const float d0 = readlane_f(r[0], 32), d1 = readlane_f(r[0], 48);
+  if (lane == 0) {
+    *reinterpret_cast<float2 *>(a_src + 2 * (size_t)n) = make_float2(s0, s1);
+    *reinterpret_cast<float2 *>(a_dst + 2 * (size_t)n) = make_float2(d0, d1);
+  }
+}
+
+// ---- own rows: softmax statistics + one gather pass over x_j ---------------------------------
+// X4 [2 heads][2 kinds][rows][512]: kind 0 = xa (sum alpha x_j), kind 1 = xa2 (sum alpha lrelu' x_j);
+// row i of the launch range is local row i - row_begin.  row_stats (global rows): (max, sum) and S3.
+__global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                       int row_begin, int row_end, const float *__restrict__ x,
+                                                       const float *__restrict__ a_src,
+                                                       const float *__restrict__ a_dst, float ns,
+                                                       float *__restrict__ X4, float *__restrict__ row_stats) {
+  constexpr int U = HICGAT_XAGG_U;
+  const int lane = lane_id();
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (i >= row_end) return;
+  const int rows = row_end - row_begin, r = i - row_begin;
+  const int beg = rowptr[i], end = rowptr[i + 1];
+  const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
+  const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
+  float m0 = -INFINITY, m1 = -INFINITY;
+  for (int e = beg + lane; e < end; e += 64) {
+    const float2 s = as2[col[e]];
+    m0 = fmaxf(m0, lrelu(s.x + ad.x, ns));
+    m1 = fmaxf(m1, lrelu(s.y + ad.y, ns));
+  }
+  m0 = wave_max(m0);
+  m1 = wave_max(m1);
+  float s0 = 0.f, s1 = 0.f;
+  for (int e = beg + lane; e < end; e += 64) {
+    const float2 s = as2[col[e]];
+    s0 += expf(lrelu(s.x + ad.x, ns) - m0);
+    s1 += expf(lrelu(s.y + ad.y, ns) - m1);
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  const float den0 = s0 + 1e-16f, den1 = s1 + 1e-16f;
+  const float4 *x4 = reinterpret_cast<const float4 *>(x);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // [head][kind][half]: head h, kind 0 (alpha) / 1 (alpha lrelu'), columns 4l.. (half 0) / 256+4l.. (1)
+  float4 acc[2][2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b][0] = acc[a][b][1] = z4;
+  float t0 = 0.f, t1 = 0.f;
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    int j = i;
+    float p0 = 0.f, p1 = 0.f, q0 = 0.f, q1 = 0.f;
+    if (e < end) {
+      j = col[e];
+      const float2 s = as2[j];
+      const float e0 = s.x + ad.x, e1 = s.y + ad.y;
+      p0 = expf(lrelu(e0, ns) - m0) / den0;
+      p1 = expf(lrelu(e1, ns) - m1) / den1;
+      q0 = p0 * (e0 > 0.f ? 1.f : ns);
+      q1 = p1 * (e1 > 0.f ? 1.f : ns);
+      t0 += q0;
+      t1 += q1;
+    }
+    const int cnt = min(64, end - base);
+    for (int k = 0; k < cnt; k += U) {
+      float4 va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t jj = (size_t)readlane_i(j, k + u);   // k + u < 64: U divides 64
+        va[u] = x4[jj * 128 + lane];
+        vb[u] = x4[jj * 128 + 64 + lane];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {   // slots past the row's end hold weight 0 (the padded lanes)
+        const float w00 = readlane_f(p0, k + u), w01 = readlane_f(q0, k + u);
+        const float w10 = readlane_f(p1, k + u), w11 = readlane_f(q1, k + u);
+        acc[0][0][0] = f4_fma(w00, va[u], acc[0][0][0]);
+        acc[0][0][1] = f4_fma(w00, vb[u], acc[0][0][1]);
+        acc[0][1][0] = f4_fma(w01, va[u], acc[0][1][0]);
+        acc[0][1][1] = f4_fma(w01, vb[u], acc[0][1][1]);
+        acc[1][0][0] = f4_fma(w10, va[u], acc[1][0][0]);
+        acc[1][0][1] = f4_fma(w10, vb[u], acc[1][0][1]);
+        acc[1][1][0] = f4_fma(w11, va[u], acc[1][1][0]);
+        acc[1][1][1] = f4_fma(w11, vb[u], acc[1][1][1]);
+      }
+    }
+  }
+  float4 *o4 = reinterpret_cast<float4 *>(X4);
+#pragma unroll
+  for (int hd = 0; hd < 2; ++hd)
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd) {
+      float4 *dst = o4 + (((size_t)(hd * 2 + kd) * rows + r) * 128);
+      dst[lane] = acc[hd][kd][0];
+      dst[64 + lane] = acc[hd][kd][1];
+    }
+  t0 = wave_sum(t0);
+  t1 = wave_sum(t1);
+  float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+  if (lane == 0) {
+    rs4[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
+    rs4[2 * (size_t)i + 1] = make_float4(t0, t1, 0.f, 0.f);
+  }
+}
+
+// ---- y0 += bias; o = relu(y0) (torch.relu: x <= 0 -> 0) over [rows, 512] -----------------------
+__global__ __launch_bounds__(256) void xagg_bias_relu_kernel(float *__restrict__ y0, const float *__restrict__ bias,
+                                                             float *__restrict__ o, int64_t n4) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n4) return;
+  float4 v = reinterpret_cast<float4 *>(y0)[t];
+  const float4 b = reinterpret_cast<const float4 *>(bias)[t & 127];
+  v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  reinterpret_cast<float4 *>(y0)[t] = v;
+  reinterpret_cast<float4 *>(o)[t] = f4_relu(v);
+}
+
+// ---- own rows: per-edge softmax-gradient terms (the destination pass of the aggregate-first form) --
+// dxa [rows][1024] (local rows): head h at columns 512h..; row_stats (global) holds delta at [4:6]
+// (agg_bwd_rows_kernel).  ds [nnz_own][2] in the rank's CSR order (rowptr[row_begin] = 0).
+__global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                                        int row_begin, int row_end, const float *__restrict__ x,
+                                                        const float *__restrict__ a_src,
+                                                        const float *__restrict__ a_dst,
+                                                        const float *__restrict__ row_stats,
+                                                        const float *__restrict__ dxa, float ns,
+                                                        float *__restrict__ ds) {
+  constexpr int U = HICGAT_XAGG_U;
+  const int lane = lane_id();
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
+  if (i >= row_end) return;
+  const int r = i - row_begin;
+  const int beg = rowptr[i], end = rowptr[i + 1];
+  const float4 *x4 = reinterpret_cast<const float4 *>(x);
+  const float4 *d4 = reinterpret_cast<const float4 *>(dxa) + (size_t)r * 256;
+  const float4 d00 = d4[lane], d01 = d4[64 + lane], d10 = d4[128 + lane], d11 = d4[192 + lane];
+  const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
+  const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
+  const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
+  const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
+  const int hh = lane >> 5;                       // after transpose_reduce<2U>: head of this lane's sum
+  constexpr int kShift = U == 8 ? 2 : U == 4 ? 3 : U == 2 ? 4 : 5;
+  const int kk = (lane >> kShift) & (U - 1);
+  const bool owner = (lane & ((1 << kShift) - 1)) == 0;
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    int j = i;
+    float al0 = 0.f, al1 = 0.f, alp0 = 0.f, alp1 = 0.f;
+    if (e < end) {
+      j = col[e];
+      const float2 s = as2[j];
+      const float e0 = s.x + ad.x, e1 = s.y + ad.y;
+      al0 = expf(lrelu(e0, ns) - ms.x) / (ms.z + 1e-16f);
+      al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
+      alp0 = al0 * (e0 > 0.f ? 1.f : ns);
+      alp1 = al1 * (e1 > 0.f ? 1.f : ns);
+    }
+    const int cnt = min(64, end - base);
+    for (int k = 0; k < cnt; k += U) {
+      float4 va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t jj = (size_t)readlane_i(j, k + u);   // k + u < 64: U divides 64
+        va[u] = x4[jj * 128 + lane];
+        vb[u] = x4[jj * 128 + 64 + lane];
+      }
+      float v[2 * U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = f4_dot(d00, va[u]) + f4_dot(d01, vb[u]);
+        v[U + u] = f4_dot(d10, va[u]) + f4_dot(d11, vb[u]);
+      }
+      transpose_reduce<2 * U>(v, lane);
+      const int src = k + kk;
+      const float pa = __shfl(alp0, src), pb = __shfl(alp1, src);   // every lane shuffles (no divergence)
+      const float p = hh ? pb : pa;
+      if (owner && src < cnt) ds[2 * (size_t)(base + src) + hh] = p * (v[0] - (hh ? dl.y : dl.x));
+    }
+  }
+}
+
+// ---- every row j: da_src_j = sum over the slab entries (j, i) of ds at the rank's edge (i, j) ------
+__global__ __launch_bounds__(256) void xagg_slab_sum_kernel(const int *__restrict__ rowptr_s,
+                                                            const int *__restrict__ perm, int N,
+                                                            const float *__restrict__ ds,
+                                                            float *__restrict__ da_src) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= N) return;
+  const float2 *ds2 = reinterpret_cast<const float2 *>(ds);
+  float a = 0.f, b = 0.f;
+  for (int k = rowptr_s[j]; k < rowptr_s[j + 1]; ++k) {
+    const float2 v = ds2[perm[k]];
+    a += v.x;
+    b += v.y;
+  }
+  reinterpret_cast<float2 *>(da_src)[j] = make_float2(a, b);
+}
+
+// ---- dW[w, :] += att_src[w] g_src[h, :] + att_dst[w] g_dst[h, :]; datt[w] += <W[w, :], g[h, :]> -----
+// one block per row w = 256 h + c of W (512 rows), 256 threads over its 512 columns
+__global__ __launch_bounds__(256) void xagg_param_finish_kernel(const float *__restrict__ W,
+                                                                const float *__restrict__ att_s,
+                                                                const float *__restrict__ att_d,
+                                                                const float *__restrict__ g_src,
+                                                                const float *__restrict__ g_dst,
+                                                                float *__restrict__ dW, float *__restrict__ datt_s,
+                                                                float *__restrict__ datt_d) {
+  __shared__ float red[2][4];
+  const int w = blockIdx.x, hd = w >> 8, t = threadIdx.x;
+  const float as = att_s[w], adv = att_d[w];
+  float ps = 0.f, pd = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = q * 256 + t;
+    const float gs = g_src[hd * 512 + k], gd = g_dst[hd * 512 + k];
+    const float wk = W[(size_t)w * 512 + k];
+    dW[(size_t)w * 512 + k] += fmaf(as, gs, adv * gd);
+    ps = fmaf(wk, gs, ps);
+    pd = fmaf(wk, gd, pd);
+  }
+  ps = wave_sum(ps);
+  pd = wave_sum(pd);
+  if (lane_id() == 0) {
+    red[0][t >> 6] = ps;
+    red[1][t >> 6] = pd;
+  }
+  __syncthreads();
+  if (t == 0) {
+    datt_s[w] += ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    datt_d[w] += ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+}  // namespace hicgat
+
+using namespace hicgat;
+
+extern "C" size_t hicgat_xagg_vec_bytes(void) { return 4 * 512 * sizeof(float); }
+
+extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
+                                  int F, int H, int C, float *vec, float *a_src, float *a_dst,
+                                  hicgat_stream_t stream) {
+  if (N < 0) return HICGAT_EINVAL;
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (!W || !att_src || !att_dst || !vec) return HICGAT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(xagg_vec_kernel, dim3(8), dim3(256), 0, s, W, att_src, att_dst, vec);
+  HICGAT_CHECK_LAUNCH();
+  if (N == 0) return HICGAT_OK;
+  if (!x || !a_src || !a_dst) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_logits_kernel, dim3((N + 3) / 4), dim3(256), 0, s, x, vec, N, a_src, a_dst);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
+                               int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope,
+                               float *X4, float *row_stats, hicgat_stream_t stream) {
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !x || !a_src || !a_dst || !X4 || !row_stats) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_fwd_kernel, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, (hipStream_t)stream, rowptr,
+                     col, row_begin, row_end, x, a_src, a_dst, neg_slope, X4, row_stats);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_bias_relu(float *y0, const float *bias, float *o, int rows, int D,
+                                     hicgat_stream_t stream) {
+  if (rows < 0 || D != 512) return D != 512 ? HICGAT_EUNSUPPORTED : HICGAT_EINVAL;
+  if (rows == 0) return HICGAT_OK;
+  if (!y0 || !bias || !o) return HICGAT_EINVAL;
+  const int64_t n4 = (int64_t)rows * D / 4;
+  hipLaunchKernelGGL(xagg_bias_relu_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y0,
+                     bias, o, n4);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
+                                int row_end, const float *x, const float *a_src, const float *a_dst,
+                                const float *row_stats, const float *dxa, float neg_slope, float *ds,
+                                hicgat_stream_t stream) {
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (row_end == row_begin) return HICGAT_OK;
+  if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !ds) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_edge_kernel, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, (hipStream_t)stream, rowptr,
+                     col, row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, ds);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds,
+                                    float *da_src, hicgat_stream_t stream) {
+  if (N < 0) return HICGAT_EINVAL;
+  if (N == 0) return HICGAT_OK;
+  if (!rowptr_s || !perm || !ds || !da_src) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_slab_sum_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rowptr_s, perm,
+                     N, ds, da_src);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_param_finish(const float *W, const float *att_src, const float *att_dst, const float *g_src,
+                                        const float *g_dst, int F, int H, int C, float *dW, float *datt_src,
+                                        float *datt_dst, hicgat_stream_t stream) {
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (!W || !att_src || !att_dst || !g_src || !g_dst || !dW || !datt_src || !datt_dst) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_param_finish_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, W, att_src, att_dst,
+                     g_src, g_dst, dW, datt_src, datt_dst);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

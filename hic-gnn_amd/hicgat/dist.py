@@ -53,7 +53,7 @@ from .ops import _ACTS, weight_grad
 from .optim import FlatAdam
 
 TILE = 128
-MODES = ("slab", "allgather")
+MODES = ("slab", "xagg", "allgather")
 
 
 def partition_rows(rowptr, P):
@@ -157,6 +157,22 @@ class ShardPlan:
         rp = np.zeros(self.N + 1, dtype=np.int64)
         np.cumsum(per_row, out=rp[1:])
         return rp.astype(np.int32), self.col[keep].astype(np.int32)
+
+    def slab_perm(self, rank):
+        """For every slab entry (row j, neighbour i) of ``slab_csr``: the index of the transposed
+        edge (i, j) in ``own_csr``'s entries (the "xagg" form reads its per-edge terms through it)."""
+        r0, r1, _ = self.rows(rank)
+        e0, e1 = int(self.rp[r0]), int(self.rp[r1])
+        N = np.int64(self.N)
+        own_rows = np.repeat(np.arange(r0, r1, dtype=np.int64), np.diff(self.rp[r0:r1 + 1]))
+        own_keys = own_rows * N + self.col[e0:e1]                 # sorted: the CSR is row-major sorted
+        srp, scol = self.slab_csr(rank)
+        srows = np.repeat(np.arange(self.N, dtype=np.int64), np.diff(srp.astype(np.int64)))
+        keys = scol.astype(np.int64) * N + srows
+        perm = np.searchsorted(own_keys, keys)
+        if perm.size and not np.array_equal(own_keys[np.minimum(perm, own_keys.size - 1)], keys):
+            raise ValueError("the CSR is not structurally symmetric: a slab entry has no transposed edge")
+        return perm.astype(np.int32)
 
     def tile_range(self, rank):
         """This rank's contiguous share of the upper-triangle loss tiles."""
@@ -264,7 +280,7 @@ class ShardedTrainer:
             self.trow0, self.tcol0 = b0, c0
             self.tband = truth.buf[b0:b1, c0:].contiguous() if b1 > b0 else torch.zeros((1, 4), **f32)
         # ---- graph and node buffers ---------------------------------------------------------------
-        if mode == "slab":
+        if mode in ("slab", "xagg"):
             rp, cl = plan.own_csr(rank)
             self.rowptr, self.col = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
             rp, cl = plan.slab_csr(rank)
@@ -278,6 +294,21 @@ class ShardedTrainer:
             self.rowptr, self.col = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
             rows = P * R                                      # rank p's rows = the p-th R-row chunk
             self.a0, self.a1 = self.q0, self.q1
+        if mode == "xagg":
+            Rl, F = self.local_rows, x.shape[1]
+            self.perm_s = torch.from_numpy(plan.slab_perm(rank)).to(dev)
+            self.x2 = torch.cat([self.x, self.x], 1).contiguous()          # [x | x]: one column sum per head
+            self.X4 = torch.zeros((2, 2, Rl, F), **f32)                     # (xa, xa2) per head, own rows
+            self.Y2 = torch.zeros((2, Rl, D), **f32)                        # [out (pre-act + bias); out2]
+            self.O = torch.zeros((Rl, D), **f32)                            # relu(out): the tail's input
+            self.dout_l = torch.zeros((Rl, D), **f32)
+            self.dxa = torch.zeros((Rl, 2 * F), **f32)
+            self.ds = torch.zeros((max(1, self.local_nnz), 2), **f32)
+            self.a_src = torch.zeros((N, self.H), **f32)
+            self.a_dst = torch.zeros((N, self.H), **f32)
+            self.g_src = torch.zeros(2 * F, **f32)
+            self.g_dst = torch.zeros(2 * F, **f32)
+            rows = 0                                                       # no [N, D] node buffers
         self.h = torch.zeros((rows, D), **f32)
         self.out = torch.zeros((rows, D), **f32)
         self.out2 = torch.zeros((rows, D), **f32)
@@ -286,10 +317,10 @@ class ShardedTrainer:
         # packed rows [dout (D) | row stats (4H)] (the "allgather" form all-gathers them as one buffer)
         self.pack = torch.zeros((rows, D + 4 * self.H), **f32)
         self.dh = torch.zeros((rows, D), **f32)
-        self.da_src = torch.zeros((rows, self.H), **f32)
+        self.da_src = torch.zeros((N if mode == "xagg" else rows, self.H), **f32)
         # row stats; rows this rank does not own stay 0 forever (the slab source pass reads row r's
         # da_dst for every r: 0 there, so only the owner adds da_dst_r * att_dst into dh_r)
-        self.rs = torch.zeros((rows, 4 * self.H), **f32)
+        self.rs = torch.zeros((N if mode == "xagg" else rows, 4 * self.H), **f32)
         self.coords_buf = torch.zeros((P * R, 3), **f32)
         if isinstance(self.comm, SimComm):
             # the other ranks' coordinates, which the all-gather would bring: any spread-out values
@@ -338,10 +369,12 @@ class ShardedTrainer:
         self.dcoords.view(-1).copy_(self.red[7:])
         K.loss_finalize(N, self.kind, self.stats, self.loss)
 
-    def _tail(self):
-        """Tail forward on own rows, the coords all-gather, the loss share and its all-reduce."""
-        a0, a1 = self.a0, self.a1
-        o = self.out[a0:a1].detach().requires_grad_(True)
+    def _tail(self, o=None):
+        """Tail forward on own rows (input ``o``, default this rank's rows of ``out``), the coords
+        all-gather, the loss share and its all-reduce."""
+        if o is None:
+            o = self.out[self.a0:self.a1]
+        o = o.detach().requires_grad_(True)
         coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
         self.coords_buf[self.q0:self.q1].copy_(coords_loc.detach())
         self.comm.all_gather_inplace(self.coords_buf, self._own(self.coords_buf))
@@ -354,6 +387,8 @@ class ShardedTrainer:
         self.model.train()
         if self.mode == "slab":
             coords, tail_done = self._step_slab()
+        elif self.mode == "xagg":
+            coords, tail_done = self._step_xagg()
         else:
             coords, tail_done = self._step_allgather()
         self._grad_allreduce(tail_done)
@@ -427,6 +462,60 @@ class ShardedTrainer:
                          accumulate=True)
             K.param_grad(self.h[r0:r1], dout[r0:r1].contiguous(), None, self.rs[r0:r1], H,
                          out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
+        return coords, tail_done
+
+    def _step_xagg(self):
+        """Aggregate-first GATConv (gat_xagg.hip): x replicated, every GEMM on own rows only."""
+        K, D, H = self.K, self.D, self.H
+        r0, r1, Rl = self.r0, self.r1, self.local_rows
+        F = self.x.shape[1]
+        C = D // H
+        W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
+        bias = self.bias.detach()
+        # ---- forward ------------------------------------------------------------------------
+        K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst)
+        K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
+        Y2f = self.Y2.view(2 * Rl, D)
+        for hd in range(H):          # [out; out2] (head hd columns) = [xa; xa2]^hd W_hd^T
+            K.gemm(0, 0, 2 * Rl, C, F, self.X4[hd].view(2 * Rl, F), W[hd * C:(hd + 1) * C],
+                   Y2f[:, hd * C:(hd + 1) * C], name="gemm_fwd")
+        Y0, Y1 = self.Y2[0], self.Y2[1]
+        if self.act:
+            K.xagg_bias_relu(Y0, bias, self.O)
+            o, coords_loc, coords = self._tail(self.O)
+        else:
+            Y0.add_(bias)
+            o, coords_loc, coords = self._tail(Y0)
+        # ---- backward -----------------------------------------------------------------------
+        tail_done = None
+        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
+            coords_loc.backward(self.dcoords[r0:r1])
+            rs_own = self.rs[r0:r1]
+            if self.act:
+                K.agg_bwd_rows(0, Rl, 1, o.grad, Y0, bias, Y1, self.dout_l, rs_own)
+            else:
+                self.dout_l.copy_(o.grad)
+                K.agg_bwd_rows(0, Rl, 0, self.dout_l, Y0, bias, Y1, None, rs_own)
+            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
+            for hd in range(H):      # dxa^hd = dout^hd W_hd
+                K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
+                       self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx")
+            K.xagg_edge(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
+                        self.ds)
+            K.xagg_slab_sum(self.rowptr_s, self.perm_s, self.ds, self.da_src)
+            ops.side_flush(after=fork)
+            tail_done = self._side_event()
+            with torch.no_grad():
+                K.param_grad(self.x2, None, self.da_src, None, H, out=(self.g_src, None, None))
+                K.param_grad(self.x2[r0:r1], None, None, rs_own, H, out=(None, self.g_dst, None))
+                if self.bias is not None:
+                    K.colsum(self.dout_l, self.bias.grad, accumulate=True)
+                for hd in range(H):  # dW_hd += dout^hd^T xa^hd (K = own rows, split)
+                    K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
+                           self.W.grad[hd * C:(hd + 1) * C], accumulate=True, splits=ops._splits(C, F, Rl),
+                           name="gemm_dw")
+                K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
+                                    self.att_r.grad.view(-1))
         return coords, tail_done
 
     def _step_allgather(self):

@@ -193,6 +193,51 @@ class HipKernels:
                                                       _lib.stream(dev)), "hicgat_gat_param_grad")
         return datt_l, datt_r, dbias
 
+    # -- aggregate-first GATConv (gat_xagg.hip): the multi-GPU "xagg" step (hicgat.dist) ---------------
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst):
+        """a_src / a_dst [N, 2] = x . (W_h^T att^h) for every row of x."""
+        N, F = x.shape
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        vec = _lib.workspace(self.lib.hicgat_xagg_vec_bytes(), x.device)
+        with _timed("xagg_logits"):
+            _lib.check(self.lib.hicgat_xagg_logits(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src),
+                                                   P(a_dst), _lib.stream(x.device)), "hicgat_xagg_logits")
+
+    def xagg_fwd(self, rowptr, col, r0, r1, x, a_src, a_dst, ns, X4, row_stats):
+        """Own rows [r0, r1): X4 [2, 2, r1 - r0, 512] = (xa, xa2) per head; row stats (global rows)."""
+        N, F = x.shape
+        assert X4.shape == (2, 2, r1 - r0, F) and X4.is_contiguous() and row_stats.shape[0] == N
+        with _timed("gat_agg_fwd"):
+            _lib.check(self.lib.hicgat_xagg_fwd(P(rowptr), P(col), N, F, 2, F // 2, r0, r1, P(x), P(a_src), P(a_dst),
+                                                float(ns), P(X4), P(row_stats), _lib.stream(x.device)),
+                       "hicgat_xagg_fwd")
+
+    def xagg_bias_relu(self, y0, bias, o):
+        rows, D = y0.shape
+        assert y0.is_contiguous() and o.is_contiguous() and o.shape == y0.shape
+        _lib.check(self.lib.hicgat_xagg_bias_relu(P(y0), P(bias), P(o), rows, D, _lib.stream(y0.device)),
+                   "hicgat_xagg_bias_relu")
+
+    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds):
+        N, F = x.shape
+        assert dxa.shape == (r1 - r0, 2 * F) and dxa.is_contiguous()
+        with _timed("gat_agg_bwd_dst"):
+            _lib.check(self.lib.hicgat_xagg_edge(P(rowptr), P(col), N, F, 2, F // 2, r0, r1, P(x), P(a_src), P(a_dst),
+                                                 P(row_stats), P(dxa), float(ns), P(ds), _lib.stream(x.device)),
+                       "hicgat_xagg_edge")
+
+    def xagg_slab_sum(self, rowptr_s, perm, ds, da_src):
+        N = da_src.shape[0]
+        with _timed("gat_agg_bwd_src"):
+            _lib.check(self.lib.hicgat_xagg_slab_sum(P(rowptr_s), P(perm), N, P(ds), P(da_src), _lib.stream(ds.device)),
+                       "hicgat_xagg_slab_sum")
+
+    def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        _lib.check(self.lib.hicgat_xagg_param_finish(P(W), P(att_l), P(att_r), P(g_src), P(g_dst), W.shape[1], H, C,
+                                                     P(dW), P(datt_l), P(datt_r), _lib.stream(W.device)),
+                   "hicgat_xagg_param_finish")
+
     # -- f1: SAGEConv (layers.py:41-79) --------------------------------------------------------------
     def sage_weights(self, A, rowptr, col):
         n = A.shape[0]

@@ -138,6 +138,42 @@ int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *col, int N, 
                               const float *row_stats, int64_t ld_stats, const float *dout, int64_t ld_dout,
                               const float *att_src, const float *att_dst, float neg_slope, float *dh, float *da_src,
                               int flags, hicgat_stream_t stream);
+/* ---- GATConv in aggregate-first order (gat_xagg.hip; the multi-GPU "xagg" step of hicgat.dist) ----
+ * Reference: the same PyG 1.7.2 GATConv (models.py:619) -- out_i^h = W_h (sum_j alpha_ij^h x_j) +
+ * b^h and a_src_j^h = <W_h^T att_src^h, x_j> are the h-first expressions regrouped, so a rank that
+ * owns destination rows needs no other rank's h and runs every GEMM on its own rows.  F = 512,
+ * H = 2, C = 256 only.  Row ranges [row_begin, row_end) are the rank's rows of a CSR in global
+ * numbering whose rowptr[row_begin] = 0 (hicgat.dist.ShardPlan.own_csr); per-row outputs marked
+ * "local" are indexed i - row_begin, row_stats by the global row.
+ *   hicgat_xagg_logits: vec [4][512] = W_h^T att_src^h (h = 0, 1), W_h^T att_dst^h; a_src / a_dst
+ *     [N][2] = x . vec for all N rows (workspace vec: hicgat_xagg_vec_bytes()).
+ *   hicgat_xagg_fwd: softmax statistics (row_stats [N][8]: max, sum at [0:4], S3 at [4:6]) and
+ *     X4 [2 heads][2 kinds][rows][512] (local): kind 0 xa = sum alpha x_j, kind 1 xa2 = sum alpha
+ *     lrelu'(e) x_j.  The caller then forms [out; out2] per head = [xa; xa2] W_h^T (hicgat_gemm_ex).
+ *   hicgat_xagg_bias_relu: y0 += bias, o = relu(y0) over [rows][512].
+ *   hicgat_xagg_edge: ds [nnz_own][2] (the rank's CSR order) = alpha lrelu'(e) (<dxa_i^h, x_j> -
+ *     delta_i^h), dxa [rows][1024] (local; head h at columns 512h = dout_i^h W_h), delta from
+ *     row_stats[i][4:6] (hicgat_gat_agg_bwd_rows).
+ *   hicgat_xagg_slab_sum: da_src [N][2], da_src_j = sum over the slab entries k of row j
+ *     (rowptr_s, N + 1) of ds[perm[k]] (perm: the rank's CSR index of the transposed edge).
+ *   hicgat_xagg_param_finish: dW[256h + c][:] += att_src^h[c] g_src[h][:] + att_dst^h[c] g_dst[h][:],
+ *     datt_src^h[c] += <W[256h + c][:], g_src[h][:]>, datt_dst likewise (g [2][512]: sum_j da_j^h x_j). */
+size_t hicgat_xagg_vec_bytes(void);
+int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N, int F,
+                       int H, int C, float *vec, float *a_src, float *a_dst, hicgat_stream_t stream);
+int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
+                    int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope, float *X4,
+                    float *row_stats, hicgat_stream_t stream);
+int hicgat_xagg_bias_relu(float *y0, const float *bias, float *o, int rows, int D, hicgat_stream_t stream);
+int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
+                     int row_end, const float *x, const float *a_src, const float *a_dst, const float *row_stats,
+                     const float *dxa, float neg_slope, float *ds, hicgat_stream_t stream);
+int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, float *da_src,
+                         hicgat_stream_t stream);
+int hicgat_xagg_param_finish(const float *W, const float *att_src, const float *att_dst, const float *g_src,
+                             const float *g_dst, int F, int H, int C, float *dW, float *datt_src, float *datt_dst,
+                             hicgat_stream_t stream);
+
 /* ---- a4+a5 and the source pass with the dense tiles on the matrix cores (gat_tiles.hip) -------
  * The same results as hicgat_gat_agg_fwd_act / hicgat_gat_agg_bwd_src_ld (fp32; the tiles' sums are
  * added in another order), with the edge set split in two:

@@ -166,6 +166,86 @@ class CpuKernels:
                 o.copy_(r)
         return out
 
+    # -- GEMM / column sums (hicgat_gemm_ex, hicgat_colsum): the "xagg" step runs its GEMMs here ----
+    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=1, name="gemm",
+             impl=None):
+        opA = (A.t() if a_kmajor else A)[:M, :K].double()
+        opB = (B if b_kmajor else B.t())[:K, :N].double()
+        r = opA @ opB
+        if bias is not None:
+            r = r + bias.double()
+        if accumulate:
+            r = r + C.double()
+        C.copy_(r.float())
+        return C
+
+    def colsum(self, A, out, accumulate=False):
+        r = A.double().sum(0)
+        out.copy_((r + out.double()).float() if accumulate else r.float())
+        return out
+
+    # -- aggregate-first GATConv (gat_xagg.hip) -------------------------------------------------------
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst):
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        Wd = W.double().view(H, C, -1)
+        vs = torch.einsum("hc,hck->hk", att_l.double().view(H, C), Wd)
+        vd = torch.einsum("hc,hck->hk", att_r.double().view(H, C), Wd)
+        a_src.copy_((x.double() @ vs.t()).float())
+        a_dst.copy_((x.double() @ vd.t()).float())
+
+    def xagg_fwd(self, rowptr, col, r0, r1, x, a_src, a_dst, ns, X4, row_stats):
+        H = 2
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        e = a_src[j] + a_dst[row]
+        le = F.leaky_relu(e, ns)
+        n = r1 - r0
+        idx = (row - r0).view(-1, 1).expand_as(le)
+        m = torch.full((n, H), float("-inf")).scatter_reduce(0, idx, le, reduce="amax", include_self=True)
+        u = torch.exp(le - m[row - r0])
+        ssum = torch.zeros((n, H)).index_add(0, row - r0, u)
+        al = (u / (ssum[row - r0] + 1e-16)).double()
+        lp = torch.where(e > 0, torch.ones_like(e), torch.full_like(e, ns)).double()
+        xj = x[j].double()
+        for hd in range(H):
+            X4[hd, 0] = torch.zeros((n, x.shape[1]), dtype=torch.float64).index_add(
+                0, row - r0, al[:, hd:hd + 1] * xj).float()
+            X4[hd, 1] = torch.zeros((n, x.shape[1]), dtype=torch.float64).index_add(
+                0, row - r0, (al * lp)[:, hd:hd + 1] * xj).float()
+        row_stats[r0:r1, 0:H] = m
+        row_stats[r0:r1, H:2 * H] = ssum
+        row_stats[r0:r1, 2 * H:3 * H] = torch.zeros((n, H), dtype=torch.float64).index_add(
+            0, row - r0, al * lp).float()
+
+    def xagg_bias_relu(self, y0, bias, o):
+        y0.add_(bias)
+        o.copy_(torch.relu(y0))
+
+    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds):
+        H = 2
+        Fd = x.shape[1]
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        al, lp = self._alpha(a_src, a_dst, row_stats, row, j, ns, H)
+        g = (dxa[row - r0].double().view(-1, H, Fd) * x[j].double().unsqueeze(1)).sum(-1)
+        delta = row_stats[row, 2 * H:3 * H].double()
+        ds[ei - int(rowptr[r0])] = (al * lp * (g - delta)).float()
+
+    def xagg_slab_sum(self, rowptr_s, perm, ds, da_src):
+        N = da_src.shape[0]
+        j, k = _rows(rowptr_s, 0, N)
+        da_src.copy_(torch.zeros((N, 2), dtype=torch.float64).index_add(0, j, ds[perm.long()[k]].double()).float())
+
+    def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
+        H, C = att_l.shape[-2], att_l.shape[-1]
+        gs, gd = g_src.double().view(H, -1), g_dst.double().view(H, -1)
+        al, ar = att_l.double().view(H, C), att_r.double().view(H, C)
+        Wd = W.double().view(H, C, -1)
+        dW.copy_((dW.double().view(H, C, -1) + al.unsqueeze(-1) * gs.unsqueeze(1)
+                  + ar.unsqueeze(-1) * gd.unsqueeze(1)).view_as(dW).float())
+        datt_l.copy_((datt_l.double().view(H, C) + torch.einsum("hck,hk->hc", Wd, gs)).view_as(datt_l).float())
+        datt_r.copy_((datt_r.double().view(H, C) + torch.einsum("hck,hk->hc", Wd, gd)).view_as(datt_r).float())
+
     def num_tiles(self, n):
         nb = (n + BT - 1) // BT
         return nb * (nb + 1) // 2

@@ -103,14 +103,16 @@ def _run(world, n, kind, tmp_path, skew=False, mode="slab"):
     return torch.load(out, weights_only=True)
 
 
-def _close(a, b):
+def _close(a, b, stats_rtol=1e-9, loss_rtol=1e-6, grad_rtol=1e-5):
     """Step 1 (loss, moments, all-reduced gradient) agrees to summation-order rounding; later
     steps only loosely, because Adam normalises near-zero gradient entries (e.g. dense3.bias,
-    whose exact gradient is 0 by translation invariance) into lr-sized moves of either sign."""
-    assert abs(b["losses"][0] - a["losses"][0]) <= 1e-6 * abs(a["losses"][0])
-    assert torch.allclose(b["stats"][:9], a["stats"][:9], rtol=1e-9)
+    whose exact gradient is 0 by translation invariance) into lr-sized moves of either sign.
+    Shards of the same form share the forward bit for bit up to the coordinates (stats to 1e-9);
+    the aggregate-first form rounds the GATConv output differently (fp32: the north star's 1e-5)."""
+    assert abs(b["losses"][0] - a["losses"][0]) <= loss_rtol * abs(a["losses"][0])
+    assert torch.allclose(b["stats"][:9], a["stats"][:9], rtol=stats_rtol)
     g1, g2 = a["grad1"], b["grad1"]
-    assert (g2 - g1).abs().max().item() <= 1e-5 * g1.abs().max().item()
+    assert (g2 - g1).abs().max().item() <= grad_rtol * g1.abs().max().item()
     np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-3)
 
 
@@ -121,7 +123,16 @@ def test_sharded_step_equals_single_rank(tmp_path, kind):
     _close(one, two)
 
 
-@pytest.mark.parametrize("mode", ["slab", "allgather"])
+def test_aggregate_first_form_equals_h_first_form(tmp_path):
+    """The "xagg" form (out = W (sum alpha x) + b, gat_xagg.hip) is the same layer as the h-first
+    form regrouped: world 1 and world 2 xagg against world 1 slab."""
+    one = _run(1, 300, "combined", tmp_path, mode="slab")
+    tol = dict(stats_rtol=1e-5, loss_rtol=1e-5, grad_rtol=1e-4)
+    _close(one, _run(1, 300, "combined", tmp_path, mode="xagg"), **tol)
+    _close(one, _run(2, 300, "combined", tmp_path, mode="xagg"), **tol)
+
+
+@pytest.mark.parametrize("mode", ["slab", "xagg", "allgather"])
 def test_three_uneven_ranks_equal_single_rank(tmp_path, mode):
     """World 3 on a 301-node graph (uneven rows, edges, tiles and support rows per rank): both
     step forms equal the world-1 step; the shards partition the edges, the support and the tiles."""
@@ -132,7 +143,7 @@ def test_three_uneven_ranks_equal_single_rank(tmp_path, mode):
     assert int(held[:, 0].sum()) == int(full[0]) and int(held[:, 1].sum()) == 301
     assert int(held[:, 2].sum()) == 301 and int(held[:, 3].sum()) == int(full[3])
     assert int(held[:, 5].sum()) == int(full[5])
-    if mode == "slab":
+    if mode in ("slab", "xagg"):
         assert int(held[:, 4].sum()) == int(full[4]) == int(full[0])     # the slabs partition the CSR
 
 
@@ -172,7 +183,7 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
         assert (mine - pr.grad).abs().max().item() <= 1e-4 * scale, name
 
 
-@pytest.mark.parametrize("mode", ["slab", "allgather"])
+@pytest.mark.parametrize("mode", ["slab", "xagg", "allgather"])
 def test_skewed_graph_shards_balance_nnz_and_match_world1(tmp_path, mode):
     """destination rows split by an nnz prefix sum.  On a dense band + sparse tail
     the two shards hold (nearly) equal edge counts -- very unequal row counts -- each rank holds

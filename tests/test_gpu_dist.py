@@ -75,7 +75,7 @@ def _graph_worker(rank, world, port, n, out, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["slab", "allgather"])
+@pytest.mark.parametrize("mode", ["slab", "xagg", "allgather"])
 def test_sharded_rccl_graph_replay_equals_eager(tmp_path, mode):
     out = str(tmp_path / f"graph_{mode}.pt")
     mp.spawn(_graph_worker, args=(1, _port(), 700, out, mode), nprocs=1, join=True)
@@ -123,24 +123,31 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path):
+@pytest.mark.parametrize("mode", ["slab", "xagg"])
+def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode):
+    """World 1 over RCCL vs the single-GPU step; the aggregate-first form ("xagg": out = W (sum
+    alpha x) + b, gat_xagg.hip) rounds the GATConv differently: loss to the north star's 1e-5,
+    gradients to 1e-4 of their max (fp32 reassociation)."""
     n = 777
-    res = _run(1, "nccl", n, tmp_path)
+    res = _run(1, "nccl", n, tmp_path, mode)
     hicgat, adj, truth, x = _inputs(n, "cuda")
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
     opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)   # the trainer's flat layout
     loss, stats, _ = hicgat.train.train_step(model, opt, x, adj, truth)
-    assert abs(float(loss) - res["loss"][0]) <= 1e-6 * abs(float(loss))
+    lt, gt = (1e-6, 1e-5) if mode == "slab" else (1e-5, 1e-4)
+    assert abs(float(loss) - res["loss"][0]) <= lt * abs(float(loss))
     g = opt.grad.cpu()
-    assert (g - res["grad1"]).abs().max().item() <= 1e-5 * g.abs().max().item()
+    assert (g - res["grad1"]).abs().max().item() <= gt * g.abs().max().item()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "allgather"), (3, "slab"), (3, "allgather")])
+@pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "xagg"), (2, "allgather"), (3, "slab"), (3, "xagg"),
+                                        (3, "allgather")])
 def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
-    """nnz-balanced shards over gloo on the one GPU, both step forms, 2 and 3 (uneven) ranks."""
+    """nnz-balanced shards over gloo on the one GPU, every step form, 2 and 3 (uneven) ranks, against
+    world 1 of the same form."""
     n = 777
-    one = _run(1, "gloo", n, tmp_path)
+    one = _run(1, "gloo", n, tmp_path, mode)
     many = _run(world, "gloo", n, tmp_path, mode)
     # the MLP tail runs on shards of the rows and the partial sums (dW, dcoords, loss moments) are
     # added across ranks: another fp32 summation order, so agreement to rounding, not bitwise
@@ -151,7 +158,8 @@ def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
     np.testing.assert_allclose(many["loss"], one["loss"], rtol=1e-3)
 
 
-def test_simulated_ranks_run_their_shares():
+@pytest.mark.parametrize("mode", ["slab", "xagg"])
+def test_simulated_ranks_run_their_shares(mode):
     """bench.py --simulate-world: each rank's share of a 3-rank step runs captured on one GPU with
     the collectives left out; the shards partition the edges, slabs, tiles and support rows."""
     hicgat, adj, truth, x = _inputs(777, "cuda")
@@ -159,7 +167,7 @@ def test_simulated_ranks_run_their_shares():
     for r in range(3):
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(3, r))
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(3, r), mode=mode)
         step = tr.captured(warmup=1)
         for _ in range(2):
             loss = step()[0]

@@ -1,0 +1,98 @@
+"""GPU: the aggregate-first GATConv kernels (gat_xagg.hip) one by one against the float64 torch
+stand-ins of tests/cpu_kernels.py (which tests/test_dist_gloo.py ties to the h-first form and the
+autograd oracle), on a 600-node synthetic Hi-C graph sharded over 3 ranks (rank 1's rows)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "hic-gnn_amd"), HERE):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def case():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hicgat
+    from hicgat import synth
+    from hicgat.dist import ShardPlan
+    n = 600
+    i, j, c = synth.contact_pairs(n, density=0.05, seed=11)
+    A = synth.dense_contacts(n, i, j, c, device="cuda")
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    plan = ShardPlan(adj.rowptr32.cpu().numpy(), adj.col32.cpu().numpy(), 3)
+    rank = 1
+    r0, r1, _ = plan.rows(rank)
+    rp, cl = plan.own_csr(rank)
+    srp, scl = plan.slab_csr(rank)
+    perm = plan.slab_perm(rank)
+    g = torch.Generator().manual_seed(3)
+    x = 0.1 * torch.randn((n, 512), generator=g)
+    torch.manual_seed(0)
+    conv = hicgat.GATConv(512, 256, heads=2)
+    W = conv.lin_l.weight.detach().clone()
+    al, ar = conv.att_l.detach().clone(), conv.att_r.detach().clone()
+    return dict(n=n, r0=r0, r1=r1, rp=torch.from_numpy(rp), cl=torch.from_numpy(cl), srp=torch.from_numpy(srp),
+                perm=torch.from_numpy(perm), x=x, W=W, al=al, ar=ar, nnz=int(cl.shape[0]))
+
+
+def test_xagg_kernels_match_float64_reference(case):
+    import hicgat
+    from cpu_kernels import CpuKernels
+    K, R = hicgat.kernels.default(), CpuKernels()
+    d = case
+    n, r0, r1 = d["n"], d["r0"], d["r1"]
+    rows = r1 - r0
+    dev = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in d.items()}
+    out = {}
+    for name, kern, t in (("ref", R, d), ("gpu", K, dev)):
+        loc = "cuda" if name == "gpu" else "cpu"
+        a_src = torch.zeros((n, 2), device=loc)
+        a_dst = torch.zeros((n, 2), device=loc)
+        kern.xagg_logits(t["x"], t["W"], t["al"], t["ar"], a_src, a_dst)
+        out[name] = {"a_src": a_src.clone(), "a_dst": a_dst.clone()}
+        if name == "gpu":
+            # the rest from the SAME logits (the reference's): each comparison isolates one kernel
+            a_src.copy_(out["ref"]["a_src"])
+            a_dst.copy_(out["ref"]["a_dst"])
+        X4 = torch.zeros((2, 2, rows, 512), device=loc)
+        rs = torch.zeros((n, 8), device=loc)
+        kern.xagg_fwd(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, 0.2, X4, rs)
+        out[name].update(X4=X4.clone(), rs=rs.clone())
+        # backward pieces from a fixed dxa / delta
+        gen = torch.Generator().manual_seed(7)
+        dxa = torch.randn((rows, 1024), generator=gen).to(loc)
+        rs[r0:r1, 4:6] = torch.randn((rows, 2), generator=gen).to(loc)
+        ds = torch.zeros((d["nnz"], 2), device=loc)
+        kern.xagg_edge(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs, dxa, 0.2, ds)
+        da_src = torch.zeros((n, 2), device=loc)
+        kern.xagg_slab_sum(t["srp"], t["perm"], ds, da_src)
+        out[name].update(ds=ds.clone(), da_src=da_src.clone())
+        gs = torch.randn(1024, generator=gen).to(loc)
+        gd = torch.randn(1024, generator=gen).to(loc)
+        dW = torch.randn((512, 512), generator=gen).to(loc)
+        dl = torch.randn(512, generator=gen).to(loc)
+        dr = torch.randn(512, generator=gen).to(loc)
+        kern.xagg_param_finish(t["W"], t["al"], t["ar"], gs, gd, dW, dl, dr)
+        out[name].update(dW=dW, dl=dl, dr=dr)
+        y0 = torch.randn((rows, 512), generator=gen).to(loc)
+        o = torch.empty_like(y0)
+        kern.xagg_bias_relu(y0, torch.randn(512, generator=gen).to(loc), o)
+        out[name].update(y0=y0, o=o)
+    g, r = out["gpu"], out["ref"]
+    errs = {k: _rel(g[k], r[k]) for k in ("a_src", "a_dst", "X4", "ds", "da_src", "dW", "dl", "dr", "y0", "o")}
+    errs["rs_stats"] = _rel(g["rs"][d["r0"]:d["r1"], :4], r["rs"][d["r0"]:d["r1"], :4])
+    errs["rs_s3"] = _rel(g["rs"][d["r0"]:d["r1"], 4:6], r["rs"][d["r0"]:d["r1"], 4:6])
+    print({k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < 1e-5 for v in errs.values()), errs

@@ -72,15 +72,15 @@ for S in "$@"; do
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json $W \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager" \
         "$COMMIT" || exit $? ;;
-    simrank|simrank_ag)
-      M=slab; [ "$S" = simrank_ag ] && M=allgather
+    simrank|simrank_ag|simrank_xa)
+      M=slab; [ "$S" = simrank_ag ] && M=allgather; [ "$S" = simrank_xa ] && M=xagg
       for P in 2 4 8; do
         timeout -k 10 240 python bench.py --simulate-world $P --dist-mode $M --steps 50 --warmup 5 \
           > gpurun_out/${T}_simrank_${M}_P$P.json 2> gpurun_out/${T}_simrank_${M}_P$P.err || exit $?
         python -c "import json;d=json.loads(open('gpurun_out/${T}_simrank_${M}_P$P.json').read().strip().splitlines()[-1]);print('$M P=$P', [round(v,4) for v in d['simulated']['rank_ms']], round(d['simulated']['model_ms_per_step'],4))"
       done ;;
-    simprof|simprof_ag)
-      M=slab; [ "$S" = simprof_ag ] && M=allgather
+    simprof|simprof_ag|simprof_xa)
+      M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \
         python bench.py --simulate-world 8 --sim-rank 0 --dist-mode $M --steps 20 --warmup 3 > gpurun_out/${T}_${S}.log 2>&1 || exit $?
       python tools/step_timeline.py gpurun_out/${T}_${S}/run_kernel_trace.csv 10 > gpurun_out/${T}_${S}_timeline.txt || exit $?
