@@ -44,8 +44,13 @@ SEEDS = (0, 1, 2, 3)
 def main():
     with np.load(os.path.join(HERE, "graph_chr19_1mb.npz"), allow_pickle=False) as z:
         a = np.array(z["matrix"], dtype=np.float64)
-    n2v = "--features" in sys.argv and sys.argv[sys.argv.index("--features") + 1] == "n2v"
-    src = "n2v_chr19_1mb.npz" if n2v else "model_GATNetSelectiveResidualsUpdated.npz"
+    feat = sys.argv[sys.argv.index("--features") + 1] if "--features" in sys.argv else "fixture"
+    n2v = feat.startswith("n2v")
+    # n2v: n2v_chr19_1mb.npz (seed 42); n2v43: n2v_chr19_1mb_s43.npz (the second node2vec seed)
+    src = {"fixture": "model_GATNetSelectiveResidualsUpdated.npz", "n2v": "n2v_chr19_1mb.npz",
+           "n2v43": "n2v_chr19_1mb_s43.npz"}[feat]
+    out_name = {"fixture": "dscc_band_chr19_1mb.npz", "n2v": "dscc_band_chr19_1mb_n2v.npz",
+                "n2v43": "dscc_band_chr19_1mb_n2v43.npz"}[feat]
     with np.load(os.path.join(HERE, src), allow_pickle=False) as z:
         x = np.asarray(z["x"], dtype=np.float32)
     np.fill_diagonal(a, 0)
@@ -77,7 +82,7 @@ def main():
                  dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
                  cpu=np.array(platform.processor() or platform.machine()))
         return
-    np.savez(os.path.join(HERE, "dscc_band_chr19_1mb_n2v.npz" if n2v else "dscc_band_chr19_1mb.npz"), steps=np.int64(K), threads=np.array(THREADS),
+    np.savez(os.path.join(HERE, out_name), steps=np.int64(K), threads=np.array(THREADS),
              dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
              cpu=np.array(platform.processor() or platform.machine()))
 
