@@ -138,7 +138,11 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode):
     lt, gt = (1e-6, 1e-5) if mode == "slab" else (1e-5, 1e-4)
     assert abs(float(loss) - res["loss"][0]) <= lt * abs(float(loss))
     g = opt.grad.cpu()
-    assert (g - res["grad1"]).abs().max().item() <= gt * g.abs().max().item()
+    names = {id(p): n for n, p in model.named_parameters()}
+    per = {names[id(p)]: ((g[o:o + p.numel()] - res["grad1"][o:o + p.numel()]).abs().max().item(),
+                          g[o:o + p.numel()].abs().max().item()) for p, o in zip(opt.params, opt.offsets)}
+    print({k: f"{d:.1e}/{m:.1e}" for k, (d, m) in per.items()})
+    assert (g - res["grad1"]).abs().max().item() <= gt * g.abs().max().item(), per
 
 
 @pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "xagg"), (2, "allgather"), (3, "slab"), (3, "xagg"),

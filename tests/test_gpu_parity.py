@@ -1163,7 +1163,7 @@ def test_config5_generalisation_matches_oracle():
         normed[tag] = hicgat.kr.KRnorm(a)[0].cpu().numpy()
     # teacher-forced generalisation of the oracle's trained model
     model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
-    sdict = {k[2:]: torch.tensor(band[k]) for k in band.files if k.startswith("w:")}
+    sdict = {k[2:]: torch.tensor(band[k]) for k in band if k.startswith("w:")}
     model.load_state_dict(sdict)
     rho_tf, _ = hicgat.align.generalize(model, al["list1"], al["list2"], e1, e2, normed["500kb"], 1)
     g_ref = float(band["dscc_generalised"][ref_i])
