@@ -407,7 +407,7 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
                                                                const double *__restrict__ mom, int64_t m0, int64_t m1,
                                                                int row_blocks, double *__restrict__ mpart,
                                                                const float4 *__restrict__ corr, int corr_r0,
-                                                               int corr_r1) {
+                                                               int corr_r1, double *__restrict__ dc64) {
   if (mom && (int)blockIdx.x >= row_blocks) {
     moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
     return;
@@ -454,9 +454,16 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
       const float4 o = corr[gi];
       s0.x += o.x; s0.y += o.y; s0.z += o.z;
     }
-    dcoords[3 * (size_t)gi] = s0.x * scale;
-    dcoords[3 * (size_t)gi + 1] = s0.y * scale;
-    dcoords[3 * (size_t)gi + 2] = s0.z * scale;
+    const float gx = s0.x * scale, gy = s0.y * scale, gz = s0.z * scale;
+    if (dc64) {   // the fp32 values, widened: straight into a caller's fp64 all-reduce buffer
+      dc64[3 * (size_t)gi] = gx;
+      dc64[3 * (size_t)gi + 1] = gy;
+      dc64[3 * (size_t)gi + 2] = gz;
+    } else {
+      dcoords[3 * (size_t)gi] = gx;
+      dcoords[3 * (size_t)gi + 1] = gy;
+      dcoords[3 * (size_t)gi + 2] = gz;
+    }
   }
 }
 
@@ -692,7 +699,7 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, part, 1, N, nb, (int)MODE_FULL, (int64_t)0, tiles, 1.0f,
-                     dcoords, nullptr, (int64_t)0, (int64_t)0, 0, nullptr, nullptr, 0, 0);
+                     dcoords, nullptr, (int64_t)0, (int64_t)0, 0, nullptr, nullptr, 0, 0, nullptr);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -748,7 +755,7 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   double *mpart = mom + (size_t)tiles * 8;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, (hipStream_t)stream, part,
                      1, N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end,
-                     row_blocks, mpart, nullptr, 0, 0);
+                     row_blocks, mpart, nullptr, 0, 0, nullptr);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mpart, N, loss_kind, stats,
                      loss);
@@ -789,8 +796,9 @@ extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int 
                                                        const int32_t *rowptr, const int32_t *col, const float *val,
                                                        const float *diag, int64_t tile_begin, int64_t tile_end,
                                                        int support_row_begin, int support_row_end, int loss_kind,
-                                                       double *stats, float *loss, float *dcoords, void *workspace,
-                                                       size_t workspace_bytes, hicgat_stream_t stream) {
+                                                       double *stats, float *loss, float *dcoords, double *dcoords64,
+                                                       void *workspace, size_t workspace_bytes,
+                                                       hicgat_stream_t stream) {
   if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !rowptr || !col || !val || !diag || !stats || !workspace) return HICGAT_EINVAL;
@@ -837,10 +845,10 @@ extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int 
     HICGAT_CHECK_LAUNCH();
   }
   const float scale = (float)(4.0 / ((double)N * (double)N));
-  const int row_blocks = dcoords ? (N + 63) / 64 : 0;
+  const int row_blocks = (dcoords || dcoords64) ? (N + 63) / 64 : 0;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
                      (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
-                     row_blocks, mpart, corr, support_row_begin, support_row_end);
+                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
   HICGAT_CHECK_LAUNCH();
@@ -853,5 +861,6 @@ extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, flo
                                                  float *dcoords, void *workspace, size_t workspace_bytes,
                                                  hicgat_stream_t stream) {
   return hicgat_pairdist_mse_fused_support_range(coords, N, background, rowptr, col, val, diag, 0, -1, 0, N,
-                                                 loss_kind, stats, loss, dcoords, workspace, workspace_bytes, stream);
+                                                 loss_kind, stats, loss, dcoords, nullptr, workspace, workspace_bytes,
+                                                 stream);
 }

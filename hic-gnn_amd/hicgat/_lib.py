@@ -72,7 +72,7 @@ SIGNATURES = {
     "hicgat_xagg_slab_sum": (c_int, [c_p, c_p, c_int, c_p, c_p, c_p]),
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_pairdist_mse_fused_support_range": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64, c_int,
-                                                        c_int, c_int, c_p, c_p, c_p, c_p, c_sz, c_p]),
+                                                        c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_truth_support": (c_int, [c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),

@@ -327,9 +327,11 @@ class ShardedTrainer:
             g = torch.Generator().manual_seed(rank)
             self.coords_buf.copy_(torch.randn((P * R, 3), generator=g))
         self.dcoords = torch.zeros((N, 3), **f32)
-        # one fp64 all-reduce for the loss moments (7) and dcoords (3N)
-        self.red = torch.zeros(7 + 3 * N, dtype=torch.float64, device=dev)
-        self.stats = torch.zeros(12, dtype=torch.float64, device=dev)
+        # one fp64 all-reduce buffer [stats (12) | dcoords (3N)]: the support-form loss writes both
+        # straight into it (the finalised entries 7..11 are recomputed after the sum)
+        self.red = torch.zeros(12 + 3 * N, dtype=torch.float64, device=dev)
+        self.stats = self.red[:12]
+        self.dc64 = self.red[12:].view(N, 3)
         self.loss = torch.zeros((), **f32)
         self.opt = FlatAdam(model.flat_parameters(), lr=lr, kern=kern)
         # gradient buckets: the GATConv's parameters lead the flat buffer (flat_parameters order)
@@ -355,19 +357,20 @@ class ShardedTrainer:
         return buf[self.q0:self.q0 + self.R]
 
     def _loss(self, coords):
+        """The loss share, one fp64 all-reduce of [moments | dcoords], the finalised loss; returns
+        this rank's rows of dcoords (fp32) for the tail's backward."""
         K, N = self.K, self.N
         if self.sf is not None:
             K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
-                                       self.loss, self.dcoords)
+                                       self.loss, self.dc64)
         else:
             K.fused_loss(coords, self.tband, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords,
                          row0=self.trow0, col0=self.tcol0)
-        self.red[:7].copy_(self.stats[:7])
-        self.red[7:].copy_(self.dcoords.view(-1))
+            self.dc64.copy_(self.dcoords)
         self.comm.all_reduce(self.red)
-        self.stats[:7].copy_(self.red[:7])
-        self.dcoords.view(-1).copy_(self.red[7:])
         K.loss_finalize(N, self.kind, self.stats, self.loss)
+        self.dcoords[self.r0:self.r1].copy_(self.dc64[self.r0:self.r1])
+        return self.dcoords[self.r0:self.r1]
 
     def _tail(self, o=None):
         """Tail forward on own rows (input ``o``, default this rank's rows of ``out``), the coords

@@ -282,12 +282,14 @@ class HipKernels:
 
     def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords):
         """A rank's share of the background-form loss: bulk tiles [t0, t1), support rows [s0, s1)
-        (partial moments and dcoords; the caller all-reduces them and calls ``loss_finalize``)."""
+        (partial moments and dcoords; the caller all-reduces them and calls ``loss_finalize``).
+        A float64 ``dcoords`` receives the fp32 gradient values widened (one all-reduce buffer)."""
         ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
+        d32, d64 = (None, dcoords) if dcoords.dtype == torch.float64 else (dcoords, None)
         with _timed("pairdist_mse_fused"):
             _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range(
                 P(coords), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(t0),
-                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(dcoords), P(ws), ws.numel(),
+                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ws), ws.numel(),
                 _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range")
 
     def loss_finalize(self, n, kind, stats, loss):

@@ -278,13 +278,15 @@ size_t hicgat_pairdist_support_workspace_bytes(int N);
  * support_row_end) (their entries j != i and their diagonal).  stats[0..6] and dcoords [N,3] are
  * that share's partial sums (the sum over shares that cover every tile and every row once is the
  * whole loss: a caller all-reduces stats[0..6] + dcoords and calls hicgat_pairdist_finalize);
- * 0, -1, 0, N is hicgat_pairdist_mse_fused_support.  Same workspace. */
+ * 0, -1, 0, N is hicgat_pairdist_mse_fused_support.  dcoords64 (instead of dcoords): the same
+ * fp32 gradient values widened to fp64, e.g. right behind stats[12] in one fp64 buffer that the
+ * caller all-reduces as a whole.  Same workspace. */
 int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background, const int32_t *rowptr,
                                             const int32_t *col, const float *val, const float *diag,
                                             int64_t tile_begin, int64_t tile_end, int support_row_begin,
                                             int support_row_end, int loss_kind, double *stats, float *loss,
-                                            float *dcoords, void *workspace, size_t workspace_bytes,
-                                            hicgat_stream_t stream);
+                                            float *dcoords, double *dcoords64, void *workspace,
+                                            size_t workspace_bytes, hicgat_stream_t stream);
 /* The background form of a symmetric N x N fp32 truth T (leading dim ldt): the sorted CSR of the
  * off-diagonal entries != background, their values, and the diagonal.  Two calls, as
  * hicgat_csr_from_dense: col == NULL fills rowptr (the counts, scanned); then col / val / diag. */

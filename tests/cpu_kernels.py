@@ -321,7 +321,8 @@ class CpuKernels:
         m[5] += (tu * tu - bg * bg).sum()
         m[6] = (sf.diag.double()[s0:s1] ** 2).sum()
         stats[:7] = m
-        dcoords.copy_((g * (4.0 / (n * n))).float())
+        gf = (g * (4.0 / (n * n))).float()
+        dcoords.copy_(gf.to(dcoords.dtype).view_as(dcoords))
         self.loss_finalize(n, kind, stats, loss)
 
     def loss_finalize(self, n, kind, stats, loss):

@@ -57,3 +57,40 @@ def test_second_step_table_factors():
     tot = sum(raw.values())
     assert list(nb) == [0, 2, 3]
     assert np.allclose(pr, [raw[k] / tot for k in nb])
+
+
+def test_initial_vectors_follow_gensim4_prep_vectors():
+    """gensim 4 ``prep_vectors``: default_rng(seed).random((V, D)) * 2 - 1, / D, rows in the
+    vocabulary order (descending count, ties by first appearance); Word2Vec's default seed 1."""
+    import torch
+    from hicgat import embed
+    walks = torch.tensor([[2, 0, 2, 1, -1], [3, 2, 0, 0, 2]], dtype=torch.int32)   # counts 0:3 1:1 2:4 3:1
+    v = embed.initial_vectors(walks, 5, 8, w2v_seed=1)
+    ref = np.random.default_rng(seed=1).random((4, 8), dtype=np.float32) * 2.0 - 1.0
+    ref /= 8
+    order = [2, 0, 1, 3]                  # 2 (4x), 0 (3x), then 1 and 3 (1x each) by first appearance
+    for rank, node in enumerate(order):
+        assert np.array_equal(v[node], ref[rank])
+    assert not v[4].any()                 # never visited: not in the vocabulary
+    assert np.abs(v[:4]).max() < 1.0 / 8
+
+
+@pytest.mark.parametrize("fixture", ["n2v_chr19_1mb.npz", "n2v_chr19_1mb_s43.npz"])
+def test_node2vec_chr19_embedding_structure(fixture):
+    """BASELINE configs[0]'s 512-d node2vec features (this repo's GPU node2vec with the reference's
+    parameters, seeds 42 and 43, tests/golden/make_n2v_chr19.py): the embedding is dominated by one
+    common direction -- the shift of skip-gram's implicit shifted-PMI factorisation on a 58-word,
+    fully co-occurring vocabulary -- with the genomic structure in the small centred remainder.
+    Measured and pinned here (why config 0's dSCC collapses on both sides)."""
+    from hicgat import embed
+    from oracle import graph as ogr
+    from oracle import kr as okr
+    x = np.asarray(load_golden(fixture)["x"], dtype=np.float32)
+    a = np.array(load_golden("graph_chr19_1mb.npz")["matrix"], dtype=np.float64)
+    np.fill_diagonal(a, 0)
+    normed, _ = okr.krnorm(a.copy())
+    t = ogr.cont2dist(ogr.load_input(normed.copy(), x)["y"], 0.5).numpy()
+    st = embed.embedding_stats(x, t)
+    print(fixture, {k: round(v, 4) for k, v in st.items()})
+    assert st["shared"] > 0.95 and st["cos_mean"] > 0.95      # common-component dominated
+    assert st["locality"] > 0.2 and st["truth_rho"] > 0.5     # the structure is in the centred remainder
