@@ -101,7 +101,11 @@ def main():
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
     r = np.array(rows, dtype=np.float64)
+    # the scipy Procrustes fit of the 500 kb embedding (rank deficient: R is not unique on the null
+    # space, so the device's own fit may differ there; the teacher-forced check feeds this one)
+    fit, _, _, _ = oal.domain_alignment(inp["list1"], inp["list2"], inp["e1"], inp["e2"])
     np.savez(os.path.join(HERE, "config5_band_chr19.npz"), steps=np.int64(K), threads=r[:, 0].astype(np.int64),
+             fit500=fit.astype(np.float32),
              seeds=r[:, 1].astype(np.int64), dscc_generalised=r[:, 2], dscc_trained=r[:, 3], loss=r[:, 4],
              feature_scale=np.float64(FEATURE_SCALE), torch=np.array(torch.__version__),
              cpu=np.array(platform.processor() or platform.machine()),

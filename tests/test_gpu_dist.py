@@ -183,3 +183,48 @@ def test_simulated_ranks_run_their_shares(mode):
         tot["srows"] += tr.s1 - tr.s0
     assert tot["nnz"] == tot["slab"] == adj.device_nnz
     assert tot["srows"] == 777 and tot["tiles"] == tr.plan.tiles
+
+
+@pytest.mark.parametrize("mode", ["slab", "xagg"])
+def test_world1_step_matches_float64_standin(mode):
+    """One world-1 step of each form on the HIP kernels against the same step on the float64 torch
+    stand-ins (tests/cpu_kernels.py, tied to the autograd oracle by tests/test_dist_gloo.py), per
+    parameter: localises a kernel / GEMM-call fault to the gradient it touches."""
+    import torch.distributed as dist
+    from cpu_kernels import CpuKernels, torch_tail
+    hicgat, adj, truth, x = _inputs(300, "cuda")
+    res = {}
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    cls = hicgat.GATNetSelectiveResidualsUpdated
+    saved = (cls.post_act, cls.tail)
+    try:
+        for dev in ("cuda", "cpu"):
+            if dev == "cpu":
+                torch_tail(hicgat)
+                from hicgat import synth
+                i, j, _ = synth.contact_pairs(300, density=0.05, seed=3)
+                a2 = hicgat.Adj(torch.tensor(i), torch.tensor(j), None, (300, 300)).to_symmetric().to("cpu")
+                t2 = hicgat.Truth(truth.dense().cpu())
+                kw = dict(kern=CpuKernels())
+            else:
+                a2, t2, kw = adj, truth, {}
+            torch.manual_seed(0)
+            model = cls().to(dev)
+            tr = hicgat.dist.ShardedTrainer(model, x.to(dev), a2, t2, lr=1e-3, mode=mode, **kw)
+            loss, stats, _ = tr.step()
+            res[dev] = (float(loss), tr.opt.grad.detach().cpu().clone(), tr.opt, model)
+    finally:
+        cls.post_act, cls.tail = saved
+        dist.destroy_process_group()
+    (lg, gg, opt, model), (lc, gc, _, _) = res["cuda"], res["cpu"]
+    names = {id(p): n for n, p in model.named_parameters()}
+    per = {names[id(p)]: ((gg[o:o + p.numel()] - gc[o:o + p.numel()]).abs().max().item(),
+                          gc[o:o + p.numel()].abs().max().item()) for p, o in zip(opt.params, opt.offsets)}
+    print(mode, f"loss {lg:.8e} vs {lc:.8e}", {k: f"{d:.1e}/{m:.1e}" for k, (d, m) in per.items()})
+    assert abs(lg - lc) <= 1e-5 * abs(lc)
+    for k, (d, m) in per.items():
+        if k == "dense3.bias":      # exactly 0 (translation invariance): rounding noise only
+            continue
+        assert d <= 2e-4 * m, (k, d, m)
