@@ -185,14 +185,15 @@ def test_simulated_ranks_run_their_shares(mode):
     assert tot["srows"] == 777 and tot["tiles"] == tr.plan.tiles
 
 
+@pytest.mark.parametrize("n", [300, 777])
 @pytest.mark.parametrize("mode", ["slab", "xagg"])
-def test_world1_step_matches_float64_standin(mode):
+def test_world1_step_matches_float64_standin(mode, n):
     """One world-1 step of each form on the HIP kernels against the same step on the float64 torch
     stand-ins (tests/cpu_kernels.py, tied to the autograd oracle by tests/test_dist_gloo.py), per
     parameter: localises a kernel / GEMM-call fault to the gradient it touches."""
     import torch.distributed as dist
     from cpu_kernels import CpuKernels, torch_tail
-    hicgat, adj, truth, x = _inputs(300, "cuda")
+    hicgat, adj, truth, x = _inputs(n, "cuda")
     res = {}
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_port())
@@ -204,8 +205,8 @@ def test_world1_step_matches_float64_standin(mode):
             if dev == "cpu":
                 torch_tail(hicgat)
                 from hicgat import synth
-                i, j, _ = synth.contact_pairs(300, density=0.05, seed=3)
-                a2 = hicgat.Adj(torch.tensor(i), torch.tensor(j), None, (300, 300)).to_symmetric().to("cpu")
+                i, j, _ = synth.contact_pairs(n, density=0.05, seed=3)
+                a2 = hicgat.Adj(torch.tensor(i), torch.tensor(j), None, (n, n)).to_symmetric().to("cpu")
                 t2 = hicgat.Truth(truth.dense().cpu())
                 kw = dict(kern=CpuKernels())
             else:

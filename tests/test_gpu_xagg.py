@@ -96,3 +96,45 @@ def test_xagg_kernels_match_float64_reference(case):
     errs["rs_s3"] = _rel(g["rs"][d["r0"]:d["r1"], 4:6], r["rs"][d["r0"]:d["r1"], 4:6])
     print({k: f"{v:.1e}" for k, v in errs.items()})
     assert all(v < 1e-5 for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("shape", ["fwd_1554", "dxa_777", "dw_777_split"])
+def test_xagg_gemm_calls_match_float64(shape):
+    """The GEMM calls of the xagg step (hicgat.dist._step_xagg) at the world-1 n = 777 shapes, with
+    their strided operands and outputs, against float64 torch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hicgat
+    from hicgat import ops
+    K = hicgat.kernels.default()
+    g = torch.Generator().manual_seed(5)
+    R = 777
+    W = torch.randn((512, 512), generator=g).cuda()
+    if shape == "fwd_1554":
+        X4 = torch.randn((2, 2, R, 512), generator=g).cuda()
+        Y2 = torch.zeros((2, R, 512)).cuda()
+        Y2f = Y2.view(2 * R, 512)
+        for hd in range(2):
+            K.gemm(0, 0, 2 * R, 256, 512, X4[hd].view(2 * R, 512), W[hd * 256:(hd + 1) * 256], Y2f[:, hd * 256:(hd + 1) * 256])
+        ref = torch.cat([X4[hd].view(2 * R, 512).double() @ W[hd * 256:(hd + 1) * 256].double().t() for hd in range(2)], 1)
+        got = Y2f
+    elif shape == "dxa_777":
+        dout = torch.randn((R, 512), generator=g).cuda()
+        dxa = torch.zeros((R, 1024)).cuda()
+        for hd in range(2):
+            K.gemm(0, 1, R, 512, 256, dout[:, hd * 256:(hd + 1) * 256], W[hd * 256:(hd + 1) * 256], dxa[:, hd * 512:(hd + 1) * 512])
+        ref = torch.cat([dout[:, hd * 256:(hd + 1) * 256].double() @ W[hd * 256:(hd + 1) * 256].double() for hd in range(2)], 1)
+        got = dxa
+    else:
+        dout = torch.randn((R, 512), generator=g).cuda()
+        X4 = torch.randn((2, 2, R, 512), generator=g).cuda()
+        dW = torch.randn((512, 512), generator=g).cuda()
+        ref = dW.double().clone()
+        for hd in range(2):
+            K.gemm(1, 1, 256, 512, R, dout[:, hd * 256:(hd + 1) * 256], X4[hd, 0], dW[hd * 256:(hd + 1) * 256],
+                   accumulate=True, splits=ops._splits(256, 512, R))
+            ref[hd * 256:(hd + 1) * 256] += dout[:, hd * 256:(hd + 1) * 256].double().t() @ X4[hd, 0].double()
+        got = dW
+    err = _rel(got, ref)
+    print(shape, f"{err:.2e}")
+    assert err < 1e-5
