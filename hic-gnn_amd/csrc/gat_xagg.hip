@@ -22,8 +22,10 @@
 //   xagg_bias_relu      y0 += bias, o = relu(y0)      (after the [xa; xa2] W_h^T GEMMs)
 //   xagg_edge_kernel    own rows: per edge ds_ij^h = alpha lrelu' (<dxa_i^h, x_j> - delta_i^h)
 //                       written in the rank's CSR order
+//   xagg_rows_bwd       own rows: dout = g relu'(y0), delta^h = <dout^h, y0^h - b^h> (no gather)
 //   xagg_slab_sum       every row j: da_src_j = sum of ds over the rank's edges (i, j), read
-//                       through the column slab (the transpose, by a precomputed permutation)
+//                       through the column slab (the transpose, by a precomputed permutation),
+//                       and g_src^h = sum_j da_src_j^h x_j in the same pass (+ xagg_colred)
 //   xagg_param_finish   dW += att (x) g terms, datt_src / datt_dst = W_h g
 #include "common.hpp"
 
@@ -179,16 +181,56 @@ __global__ __launch_bounds__(256) void xagg_bias_relu_kernel(float *__restrict__
   reinterpret_cast<float4 *>(o)[t] = f4_relu(v);
 }
 
+// ---- own rows: dout = g [y0 > 0] (relu backward, ACT) or g; delta^h = <dout^h, y0^h - bias^h>; the
+// forward's S3 moves to row_stats[6:8] (the edge pass forms da_dst there from it) ------------------
+template <int ACT>
+__global__ __launch_bounds__(256) void xagg_rows_bwd_kernel(int rows, const float *__restrict__ g,
+                                                            const float *__restrict__ y0,
+                                                            const float *__restrict__ bias, float *__restrict__ dout,
+                                                            float *__restrict__ row_stats) {
+  const int lane = lane_id();
+  const int r = blockIdx.x * 4 + wave_in_block();
+  if (r >= rows) return;
+  const size_t o0 = (size_t)r * 128 + lane, o1 = o0 + 64;
+  const float4 *g4 = reinterpret_cast<const float4 *>(g);
+  const float4 *y4 = reinterpret_cast<const float4 *>(y0);
+  const float4 *b4 = reinterpret_cast<const float4 *>(bias);
+  float4 d0 = g4[o0], d1 = g4[o1];
+  const float4 y0v = y4[o0], y1v = y4[o1], b0 = b4[lane], b1 = b4[64 + lane];
+  if (ACT) {
+    d0 = make_float4(y0v.x <= 0.f ? 0.f : d0.x, y0v.y <= 0.f ? 0.f : d0.y, y0v.z <= 0.f ? 0.f : d0.z,
+                     y0v.w <= 0.f ? 0.f : d0.w);
+    d1 = make_float4(y1v.x <= 0.f ? 0.f : d1.x, y1v.y <= 0.f ? 0.f : d1.y, y1v.z <= 0.f ? 0.f : d1.z,
+                     y1v.w <= 0.f ? 0.f : d1.w);
+  }
+  float4 *d4 = reinterpret_cast<float4 *>(dout);
+  d4[o0] = d0;
+  d4[o1] = d1;
+  const float4 e0 = make_float4(y0v.x - b0.x, y0v.y - b0.y, y0v.z - b0.z, y0v.w - b0.w);
+  const float4 e1 = make_float4(y1v.x - b1.x, y1v.y - b1.y, y1v.z - b1.z, y1v.w - b1.w);
+  float v[2] = {f4_dot(d0, e0), f4_dot(d1, e1)};
+  transpose_reduce<2>(v, lane);   // lane 0: head 0, lane 32: head 1
+  const float dl0 = readlane_f(v[0], 0), dl1 = readlane_f(v[0], 32);
+  if (lane == 0) {
+    float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+    const float4 t = rs4[2 * (size_t)r + 1];   // (S3_0, S3_1, -, -) from xagg_fwd
+    rs4[2 * (size_t)r + 1] = make_float4(dl0, dl1, t.x, t.y);
+  }
+}
+
 // ---- own rows: per-edge softmax-gradient terms (the destination pass of the aggregate-first form) --
 // dxa [rows][1024] (local rows): head h at columns 512h..; row_stats (global) holds delta at [4:6]
 // (agg_bwd_rows_kernel).  ds [nnz_own][2] in the rank's CSR order (rowptr[row_begin] = 0).
+// xa2 != NULL (X4's kind-1 planes, local rows; the caller's forward skipped out2): the row's
+// da_dst^h = <dxa_i^h, xa2_i^h> - delta_i^h S3_i^h is formed here too, with S3 read from
+// row_stats[6:8] (xagg_rows_bwd put it there) and da_dst written over it.
 __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                         int row_begin, int row_end, const float *__restrict__ x,
                                                         const float *__restrict__ a_src,
                                                         const float *__restrict__ a_dst,
-                                                        const float *__restrict__ row_stats,
+                                                        float *__restrict__ row_stats,
                                                         const float *__restrict__ dxa, float ns,
-                                                        float *__restrict__ ds) {
+                                                        float *__restrict__ ds, const float *__restrict__ xa2) {
   constexpr int U = HICGAT_XAGG_U;
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
@@ -241,23 +283,83 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
       if (owner && src < cnt) ds[2 * (size_t)(base + src) + hh] = p * (v[0] - (hh ? dl.y : dl.x));
     }
   }
+  if (xa2) {
+    const int rows = row_end - row_begin;
+    const float4 *q0 = reinterpret_cast<const float4 *>(xa2) + (size_t)r * 128;                     // head 0
+    const float4 *q1 = reinterpret_cast<const float4 *>(xa2) + ((size_t)2 * rows + r) * 128;         // head 1
+    float v[2] = {f4_dot(d00, q0[lane]) + f4_dot(d01, q0[64 + lane]), f4_dot(d10, q1[lane]) + f4_dot(d11, q1[64 + lane])};
+    transpose_reduce<2>(v, lane);
+    const float p0 = readlane_f(v[0], 0), p1 = readlane_f(v[0], 32);
+    if (lane == 0) {
+      const float2 s3 = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 6);
+      *reinterpret_cast<float2 *>(row_stats + 8 * (size_t)i + 6) = make_float2(fmaf(-dl.x, s3.x, p0), fmaf(-dl.y, s3.y, p1));
+    }
+  }
 }
 
-// ---- every row j: da_src_j = sum over the slab entries (j, i) of ds at the rank's edge (i, j) ------
+// ---- every row j: da_src_j = sum over the slab entries (j, i) of ds at the rank's edge (i, j), and
+// g_src^h += da_src_j^h x_j: persistent waves (wave w takes rows w, w + W, ...), lanes over a row's
+// entries (float2 wave sum), then x_j's 512 columns (8 per lane) into the wave's two 512-column
+// partial rows; part [W][2][512] is summed in wave order by xagg_colred_kernel (no atomics). ------
+constexpr int kSlabWaves = 1024;   // partial rows of g_src (256 workgroups x 4 waves)
 __global__ __launch_bounds__(256) void xagg_slab_sum_kernel(const int *__restrict__ rowptr_s,
                                                             const int *__restrict__ perm, int N,
                                                             const float *__restrict__ ds,
-                                                            float *__restrict__ da_src) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= N) return;
+                                                            const float *__restrict__ x,
+                                                            float *__restrict__ da_src, float *__restrict__ part) {
+  const int lane = lane_id();
+  const int w = blockIdx.x * 4 + wave_in_block(), W = gridDim.x * 4;
   const float2 *ds2 = reinterpret_cast<const float2 *>(ds);
-  float a = 0.f, b = 0.f;
-  for (int k = rowptr_s[j]; k < rowptr_s[j + 1]; ++k) {
-    const float2 v = ds2[perm[k]];
-    a += v.x;
-    b += v.y;
+  const float4 *x4 = reinterpret_cast<const float4 *>(x);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 g00 = z4, g01 = z4, g10 = z4, g11 = z4;   // head 0 / 1, columns 4l.. / 256+4l..
+  for (int j = w; j < N; j += W) {
+    float a = 0.f, b = 0.f;
+    for (int k = rowptr_s[j] + lane; k < rowptr_s[j + 1]; k += 64) {
+      const float2 v = ds2[perm[k]];
+      a += v.x;
+      b += v.y;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) reinterpret_cast<float2 *>(da_src)[j] = make_float2(a, b);
+    const float4 xa = x4[(size_t)j * 128 + lane], xb = x4[(size_t)j * 128 + 64 + lane];
+    g00 = f4_fma(a, xa, g00);
+    g01 = f4_fma(a, xb, g01);
+    g10 = f4_fma(b, xa, g10);
+    g11 = f4_fma(b, xb, g11);
   }
-  reinterpret_cast<float2 *>(da_src)[j] = make_float2(a, b);
+  float4 *p4 = reinterpret_cast<float4 *>(part) + (size_t)w * 256;
+  p4[lane] = g00;
+  p4[64 + lane] = g01;
+  p4[128 + lane] = g10;
+  p4[192 + lane] = g11;
+}
+
+// out[c] = sum_w part[w][c] over the kSlabWaves partial rows, c < 1024: block = 16 columns x 16
+// groups, group q adds w = q, q + 16, ... with its loads in flight, groups combined in order.
+__global__ __launch_bounds__(256) void xagg_colred_kernel(const float *__restrict__ part, int nw, float *__restrict__ out) {
+  __shared__ float red[16][16];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  constexpr int kMax = kSlabWaves / 16;
+  float v[kMax];
+#pragma unroll
+  for (int t = 0; t < kMax; ++t) {
+    const int w = grp + 16 * t;
+    v[t] = w < nw ? part[(size_t)w * 1024 + c] : 0.f;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int t = 0; t < kMax; ++t) acc += v[t];
+  red[grp][cl] = acc;
+  __syncthreads();
+  if (grp == 0) {
+    float tsum = red[0][cl];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) tsum += red[q][cl];
+    out[c] = tsum;
+  }
 }
 
 // ---- dW[w, :] += att_src[w] g_src[h, :] + att_dst[w] g_dst[h, :]; datt[w] += <W[w, :], g[h, :]> -----
@@ -342,27 +444,50 @@ extern "C" int hicgat_xagg_bias_relu(float *y0, const float *bias, float *o, int
   return HICGAT_OK;
 }
 
+extern "C" int hicgat_xagg_rows_bwd(int rows, int D, int act, const float *g, const float *y0, const float *bias,
+                                    float *dout, float *row_stats, hicgat_stream_t stream) {
+  if (rows < 0 || (act != 0 && act != 1)) return HICGAT_EINVAL;
+  if (D != 512) return HICGAT_EUNSUPPORTED;
+  if (rows == 0) return HICGAT_OK;
+  if (!g || !y0 || !bias || !dout || !row_stats) return HICGAT_EINVAL;
+  if (act)
+    hipLaunchKernelGGL(xagg_rows_bwd_kernel<1>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, rows, g, y0,
+                       bias, dout, row_stats);
+  else
+    hipLaunchKernelGGL(xagg_rows_bwd_kernel<0>, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, rows, g, y0,
+                       bias, dout, row_stats);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 extern "C" int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
-                                int row_end, const float *x, const float *a_src, const float *a_dst,
-                                const float *row_stats, const float *dxa, float neg_slope, float *ds,
+                                int row_end, const float *x, const float *a_src, const float *a_dst, float *row_stats,
+                                const float *dxa, const float *xa2, float neg_slope, float *ds,
                                 hicgat_stream_t stream) {
   if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (row_end == row_begin) return HICGAT_OK;
   if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !ds) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_edge_kernel, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, (hipStream_t)stream, rowptr,
-                     col, row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, ds);
+                     col, row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, ds, xa2);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
+extern "C" size_t hicgat_xagg_slab_workspace_bytes(void) { return (size_t)kSlabWaves * 1024 * sizeof(float); }
+
 extern "C" int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds,
-                                    float *da_src, hicgat_stream_t stream) {
+                                    const float *x, float *da_src, float *g_src, void *workspace,
+                                    size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0) return HICGAT_EINVAL;
-  if (N == 0) return HICGAT_OK;
-  if (!rowptr_s || !perm || !ds || !da_src) return HICGAT_EINVAL;
-  hipLaunchKernelGGL(xagg_slab_sum_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rowptr_s, perm,
-                     N, ds, da_src);
+  if (!rowptr_s || !perm || !ds || !x || !da_src || !g_src || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_xagg_slab_workspace_bytes()) return HICGAT_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  float *part = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(xagg_slab_sum_kernel, dim3(kSlabWaves / 4), dim3(256), 0, s, rowptr_s, perm, N, ds, x, da_src,
+                     part);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(xagg_colred_kernel, dim3(1024 / 16), dim3(256), 0, s, part, kSlabWaves, g_src);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

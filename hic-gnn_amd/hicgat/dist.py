@@ -299,7 +299,7 @@ class ShardedTrainer:
             self.perm_s = torch.from_numpy(plan.slab_perm(rank)).to(dev)
             self.x2 = torch.cat([self.x, self.x], 1).contiguous()          # [x | x]: one column sum per head
             self.X4 = torch.zeros((2, 2, Rl, F), **f32)                     # (xa, xa2) per head, own rows
-            self.Y2 = torch.zeros((2, Rl, D), **f32)                        # [out (pre-act + bias); out2]
+            self.Y0 = torch.zeros((Rl, D), **f32)                           # out (pre-activation + bias)
             self.O = torch.zeros((Rl, D), **f32)                            # relu(out): the tail's input
             self.dout_l = torch.zeros((Rl, D), **f32)
             self.dxa = torch.zeros((Rl, 2 * F), **f32)
@@ -341,6 +341,7 @@ class ShardedTrainer:
         cut = (max(ends) + 3) // 4 * 4
         self.grad_split = cut if (firsts and min(firsts) >= cut) else None
         self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
+        self.head_stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
@@ -467,6 +468,20 @@ class ShardedTrainer:
                          out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
         return coords, tail_done
 
+    def _heads(self, fn):
+        """``fn(hd)`` for both heads: head 1 on a second stream (the per-head GEMMs on a rank's
+        shard are a quarter of the chip's workgroups each), joined before returning."""
+        if not self.cuda:
+            fn(0)
+            fn(1)
+            return
+        main = torch.cuda.current_stream()
+        self.head_stream.wait_stream(main)
+        fn(0)
+        with torch.cuda.stream(self.head_stream):
+            fn(1)
+        main.wait_stream(self.head_stream)
+
     def _step_xagg(self):
         """Aggregate-first GATConv (gat_xagg.hip): x replicated, every GEMM on own rows only."""
         K, D, H = self.K, self.D, self.H
@@ -478,11 +493,10 @@ class ShardedTrainer:
         # ---- forward ------------------------------------------------------------------------
         K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst)
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
-        Y2f = self.Y2.view(2 * Rl, D)
-        for hd in range(H):          # [out; out2] (head hd columns) = [xa; xa2]^hd W_hd^T
-            K.gemm(0, 0, 2 * Rl, C, F, self.X4[hd].view(2 * Rl, F), W[hd * C:(hd + 1) * C],
-                   Y2f[:, hd * C:(hd + 1) * C], name="gemm_fwd")
-        Y0, Y1 = self.Y2[0], self.Y2[1]
+        Y0 = self.Y0
+        # out (head hd columns) = xa^hd W_hd^T; the forward needs no out2 (da_dst comes from dxa . xa2)
+        self._heads(lambda hd: K.gemm(0, 0, Rl, C, F, self.X4[hd, 0], W[hd * C:(hd + 1) * C],
+                                      Y0[:, hd * C:(hd + 1) * C], name="gemm_fwd"))
         if self.act:
             K.xagg_bias_relu(Y0, bias, self.O)
             o, coords_loc, coords = self._tail(self.O)
@@ -494,29 +508,24 @@ class ShardedTrainer:
         with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
             coords_loc.backward(self.dcoords[r0:r1])
             rs_own = self.rs[r0:r1]
-            if self.act:
-                K.agg_bwd_rows(0, Rl, 1, o.grad, Y0, bias, Y1, self.dout_l, rs_own)
-            else:
-                self.dout_l.copy_(o.grad)
-                K.agg_bwd_rows(0, Rl, 0, self.dout_l, Y0, bias, Y1, None, rs_own)
+            K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
             fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
-            for hd in range(H):      # dxa^hd = dout^hd W_hd
-                K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
-                       self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx")
+            # dxa^hd = dout^hd W_hd
+            self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
+                                          self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx"))
             K.xagg_edge(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
-                        self.ds)
-            K.xagg_slab_sum(self.rowptr_s, self.perm_s, self.ds, self.da_src)
+                        self.ds, xa2=self.X4[:, 1])
+            K.xagg_slab_sum(self.rowptr_s, self.perm_s, self.ds, self.x, self.da_src, self.g_src)
             ops.side_flush(after=fork)
             tail_done = self._side_event()
             with torch.no_grad():
-                K.param_grad(self.x2, None, self.da_src, None, H, out=(self.g_src, None, None))
                 K.param_grad(self.x2[r0:r1], None, None, rs_own, H, out=(None, self.g_dst, None))
                 if self.bias is not None:
                     K.colsum(self.dout_l, self.bias.grad, accumulate=True)
-                for hd in range(H):  # dW_hd += dout^hd^T xa^hd (K = own rows, split)
-                    K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
-                           self.W.grad[hd * C:(hd + 1) * C], accumulate=True, splits=ops._splits(C, F, Rl),
-                           name="gemm_dw")
+                # dW_hd += dout^hd^T xa^hd (K = own rows, split)
+                self._heads(lambda hd: K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
+                                              self.W.grad[hd * C:(hd + 1) * C], accumulate=True,
+                                              splits=ops._splits(C, F, Rl), name="gemm_dw"))
                 K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
                                     self.att_r.grad.view(-1))
         return coords, tail_done

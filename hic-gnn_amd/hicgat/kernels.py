@@ -218,19 +218,30 @@ class HipKernels:
         _lib.check(self.lib.hicgat_xagg_bias_relu(P(y0), P(bias), P(o), rows, D, _lib.stream(y0.device)),
                    "hicgat_xagg_bias_relu")
 
-    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds):
+    def xagg_rows_bwd(self, act, g, y0, bias, dout, row_stats):
+        """Own rows: dout = g relu'(y0) (act) or g, delta -> row_stats[:, 4:6], S3 -> [:, 6:8]."""
+        rows, D = y0.shape
+        assert row_stats.shape == (rows, 8) and row_stats.is_contiguous()
+        with _timed("gat_agg_bwd_rows"):
+            _lib.check(self.lib.hicgat_xagg_rows_bwd(rows, D, int(act), P(g), P(y0), P(bias), P(dout), P(row_stats),
+                                                     _lib.stream(y0.device)), "hicgat_xagg_rows_bwd")
+
+    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds, xa2=None):
+        """Per-edge softmax terms of own rows; with ``xa2`` (X4[:, 1]) also da_dst (row_stats[:, 6:8])."""
         N, F = x.shape
         assert dxa.shape == (r1 - r0, 2 * F) and dxa.is_contiguous()
         with _timed("gat_agg_bwd_dst"):
             _lib.check(self.lib.hicgat_xagg_edge(P(rowptr), P(col), N, F, 2, F // 2, r0, r1, P(x), P(a_src), P(a_dst),
-                                                 P(row_stats), P(dxa), float(ns), P(ds), _lib.stream(x.device)),
+                                                 P(row_stats), P(dxa), P(xa2), float(ns), P(ds), _lib.stream(x.device)),
                        "hicgat_xagg_edge")
 
-    def xagg_slab_sum(self, rowptr_s, perm, ds, da_src):
+    def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
+        """da_src (every row, through the slab) and g_src [2, 512] = sum_j da_src_j x_j."""
         N = da_src.shape[0]
+        ws = _lib.workspace(self.lib.hicgat_xagg_slab_workspace_bytes(), ds.device)
         with _timed("gat_agg_bwd_src"):
-            _lib.check(self.lib.hicgat_xagg_slab_sum(P(rowptr_s), P(perm), N, P(ds), P(da_src), _lib.stream(ds.device)),
-                       "hicgat_xagg_slab_sum")
+            _lib.check(self.lib.hicgat_xagg_slab_sum(P(rowptr_s), P(perm), N, P(ds), P(x), P(da_src), P(g_src), P(ws),
+                                                     ws.numel(), _lib.stream(ds.device)), "hicgat_xagg_slab_sum")
 
     def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
         H, C = att_l.shape[-2], att_l.shape[-1]

@@ -151,11 +151,16 @@ int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *col, int N, 
  *     X4 [2 heads][2 kinds][rows][512] (local): kind 0 xa = sum alpha x_j, kind 1 xa2 = sum alpha
  *     lrelu'(e) x_j.  The caller then forms [out; out2] per head = [xa; xa2] W_h^T (hicgat_gemm_ex).
  *   hicgat_xagg_bias_relu: y0 += bias, o = relu(y0) over [rows][512].
+ *   hicgat_xagg_rows_bwd: own rows (local row_stats view): dout = g [y0 > 0] (act 1) or g,
+ *     delta^h = <dout^h, y0^h - bias^h> into row_stats[4:6]; the forward's S3 moves to [6:8].
  *   hicgat_xagg_edge: ds [nnz_own][2] (the rank's CSR order) = alpha lrelu'(e) (<dxa_i^h, x_j> -
  *     delta_i^h), dxa [rows][1024] (local; head h at columns 512h = dout_i^h W_h), delta from
- *     row_stats[i][4:6] (hicgat_gat_agg_bwd_rows).
+ *     row_stats[i][4:6]; with xa2 (X4's kind-1 planes: X4 + rows*512) also da_dst^h =
+ *     <dxa_i^h, xa2_i^h> - delta_i^h S3_i^h into row_stats[i][6:8] (S3 read from there).
  *   hicgat_xagg_slab_sum: da_src [N][2], da_src_j = sum over the slab entries k of row j
- *     (rowptr_s, N + 1) of ds[perm[k]] (perm: the rank's CSR index of the transposed edge).
+ *     (rowptr_s, N + 1) of ds[perm[k]] (perm: the rank's CSR index of the transposed edge), and
+ *     g_src [2][512] = sum_j da_src_j^h x_j (x: all N rows), fixed-order partial sums
+ *     (workspace hicgat_xagg_slab_workspace_bytes()).
  *   hicgat_xagg_param_finish: dW[256h + c][:] += att_src^h[c] g_src[h][:] + att_dst^h[c] g_dst[h][:],
  *     datt_src^h[c] += <W[256h + c][:], g_src[h][:]>, datt_dst likewise (g [2][512]: sum_j da_j^h x_j). */
 size_t hicgat_xagg_vec_bytes(void);
@@ -165,10 +170,14 @@ int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int
                     int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope, float *X4,
                     float *row_stats, hicgat_stream_t stream);
 int hicgat_xagg_bias_relu(float *y0, const float *bias, float *o, int rows, int D, hicgat_stream_t stream);
+int hicgat_xagg_rows_bwd(int rows, int D, int act, const float *g, const float *y0, const float *bias, float *dout,
+                         float *row_stats, hicgat_stream_t stream);
 int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
-                     int row_end, const float *x, const float *a_src, const float *a_dst, const float *row_stats,
-                     const float *dxa, float neg_slope, float *ds, hicgat_stream_t stream);
-int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, float *da_src,
+                     int row_end, const float *x, const float *a_src, const float *a_dst, float *row_stats,
+                     const float *dxa, const float *xa2, float neg_slope, float *ds, hicgat_stream_t stream);
+size_t hicgat_xagg_slab_workspace_bytes(void);
+int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, const float *x,
+                         float *da_src, float *g_src, void *workspace, size_t workspace_bytes,
                          hicgat_stream_t stream);
 int hicgat_xagg_param_finish(const float *W, const float *att_src, const float *att_dst, const float *g_src,
                              const float *g_dst, int F, int H, int C, float *dW, float *datt_src, float *datt_dst,

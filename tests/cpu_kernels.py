@@ -221,7 +221,20 @@ class CpuKernels:
         y0.add_(bias)
         o.copy_(torch.relu(y0))
 
-    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds):
+    def xagg_rows_bwd(self, act, g, y0, bias, dout, row_stats):
+        H = 2
+        rows, D = y0.shape
+        d = g.double()
+        y = y0.double()
+        if act:
+            d = torch.where(y > 0, d, torch.zeros_like(d))
+        dout.copy_(d.float())
+        delta = (d * (y - bias.double())).view(rows, H, D // H).sum(-1)
+        s3 = row_stats[:, 2 * H:3 * H].clone()
+        row_stats[:, 2 * H:3 * H] = delta.float()
+        row_stats[:, 3 * H:4 * H] = s3
+
+    def xagg_edge(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, ds, xa2=None):
         H = 2
         Fd = x.shape[1]
         row, ei = _rows(rowptr, r0, r1)
@@ -230,11 +243,18 @@ class CpuKernels:
         g = (dxa[row - r0].double().view(-1, H, Fd) * x[j].double().unsqueeze(1)).sum(-1)
         delta = row_stats[row, 2 * H:3 * H].double()
         ds[ei - int(rowptr[r0])] = (al * lp * (g - delta)).float()
+        if xa2 is not None:
+            dx = dxa.double().view(r1 - r0, H, Fd)
+            q = torch.stack([(dx[:, hd] * xa2[hd].double()).sum(-1) for hd in range(H)], 1)
+            s3 = row_stats[r0:r1, 3 * H:4 * H].double()
+            row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
 
-    def xagg_slab_sum(self, rowptr_s, perm, ds, da_src):
+    def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
         N = da_src.shape[0]
         j, k = _rows(rowptr_s, 0, N)
-        da_src.copy_(torch.zeros((N, 2), dtype=torch.float64).index_add(0, j, ds[perm.long()[k]].double()).float())
+        da = torch.zeros((N, 2), dtype=torch.float64).index_add(0, j, ds[perm.long()[k]].double())
+        da_src.copy_(da.float())
+        g_src.copy_((da.t() @ x.double()).reshape(-1).float())
 
     def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
         H, C = att_l.shape[-2], att_l.shape[-1]

@@ -70,15 +70,21 @@ def test_xagg_kernels_match_float64_reference(case):
         rs = torch.zeros((n, 8), device=loc)
         kern.xagg_fwd(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, 0.2, X4, rs)
         out[name].update(X4=X4.clone(), rs=rs.clone())
-        # backward pieces from a fixed dxa / delta
+        # backward pieces from a fixed upstream gradient
         gen = torch.Generator().manual_seed(7)
+        gout = torch.randn((rows, 512), generator=gen).to(loc)
+        y0 = torch.randn((rows, 512), generator=gen).to(loc)
+        bb = torch.randn(512, generator=gen).to(loc)
+        dout = torch.empty((rows, 512), device=loc)
+        kern.xagg_rows_bwd(1, gout, y0, bb, dout, rs[r0:r1])
+        out[name].update(dout=dout.clone(), rs_rows=rs[r0:r1].clone())
         dxa = torch.randn((rows, 1024), generator=gen).to(loc)
-        rs[r0:r1, 4:6] = torch.randn((rows, 2), generator=gen).to(loc)
         ds = torch.zeros((d["nnz"], 2), device=loc)
-        kern.xagg_edge(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs, dxa, 0.2, ds)
+        kern.xagg_edge(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs, dxa, 0.2, ds, xa2=X4[:, 1])
         da_src = torch.zeros((n, 2), device=loc)
-        kern.xagg_slab_sum(t["srp"], t["perm"], ds, da_src)
-        out[name].update(ds=ds.clone(), da_src=da_src.clone())
+        g_src = torch.zeros(1024, device=loc)
+        kern.xagg_slab_sum(t["srp"], t["perm"], ds, t["x"], da_src, g_src)
+        out[name].update(ds=ds.clone(), da_src=da_src.clone(), g_src=g_src.clone(), rs_edge=rs[r0:r1].clone())
         gs = torch.randn(1024, generator=gen).to(loc)
         gd = torch.randn(1024, generator=gen).to(loc)
         dW = torch.randn((512, 512), generator=gen).to(loc)
@@ -91,7 +97,8 @@ def test_xagg_kernels_match_float64_reference(case):
         kern.xagg_bias_relu(y0, torch.randn(512, generator=gen).to(loc), o)
         out[name].update(y0=y0, o=o)
     g, r = out["gpu"], out["ref"]
-    errs = {k: _rel(g[k], r[k]) for k in ("a_src", "a_dst", "X4", "ds", "da_src", "dW", "dl", "dr", "y0", "o")}
+    errs = {k: _rel(g[k], r[k]) for k in ("a_src", "a_dst", "X4", "dout", "rs_rows", "ds", "da_src", "g_src",
+                                           "rs_edge", "dW", "dl", "dr", "y0", "o")}
     errs["rs_stats"] = _rel(g["rs"][d["r0"]:d["r1"], :4], r["rs"][d["r0"]:d["r1"], :4])
     errs["rs_s3"] = _rel(g["rs"][d["r0"]:d["r1"], 4:6], r["rs"][d["r0"]:d["r1"], 4:6])
     print({k: f"{v:.1e}" for k, v in errs.items()})
