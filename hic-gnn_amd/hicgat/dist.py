@@ -44,6 +44,8 @@ object (``DistComm`` over torch.distributed; ``SimComm`` runs ONE rank's share w
 left out, for the per-rank compute measurement of bench.py --simulate-world), so the partitioning
 and collectives are testable on CPU with gloo and a torch stand-in.
 """
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -54,6 +56,8 @@ from .optim import FlatAdam
 
 TILE = 128
 MODES = ("slab", "xagg", "allgather")
+# "xagg": head 1's GEMMs on a second stream beside head 0's (1, default) or both on one stream (0)
+HEAD_STREAM = os.environ.get("HICGAT_HEAD_STREAM", "1") != "0"
 
 
 def partition_rows(rowptr, P):
@@ -471,7 +475,7 @@ class ShardedTrainer:
     def _heads(self, fn):
         """``fn(hd)`` for both heads: head 1 on a second stream (the per-head GEMMs on a rank's
         shard are a quarter of the chip's workgroups each), joined before returning."""
-        if not self.cuda:
+        if not self.cuda or not HEAD_STREAM:
             fn(0)
             fn(1)
             return

@@ -12,9 +12,10 @@ graph_chr19_1mb.npz (the reference's contact matrix) and model_GATNetSelectiveRe
 
     python tests/golden/make_dscc_band.py      # ~5 min on 8 cores
 
-``--seeds`` runs the same pipeline at 1 thread for initial-weight seeds 0..3 and writes
-``dscc_seeds_chr19_1mb.npz``: the summation-order-robust protocol of the GPU test (the mean dSCC
-over the four seeds, which both of the device's aggregation forms must reproduce within +-0.005).
+``--seeds`` runs the same pipeline at 1 thread for initial-weight seeds 0..7 (one process per seed)
+and writes ``dscc_seeds_chr19_1mb.npz``: the summation-order-robust protocol of the GPU test (the
+MEDIAN dSCC over the eight seeds, which both of the device's aggregation forms must reproduce within
++-0.005; a mean over four seeds moved by 1.3e-2 when one device seed fell into another basin).
 
 ``--features n2v`` uses the node2vec embedding ``n2v_chr19_1mb.npz`` (tests/golden/make_n2v_chr19.py,
 this repo's GPU node2vec with the reference's parameters) instead of the fixture's random features
@@ -38,7 +39,23 @@ from oracle import loop as ol  # noqa: E402
 
 K = 3000
 THREADS = (1, 2, 4, 8)
-SEEDS = (0, 1, 2, 3)
+SEEDS = tuple(range(8))
+
+
+def _run(th, sd, d, radj, truth):
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        torch.set_num_threads(th)
+        torch.manual_seed(sd)
+        ref = og.GATNetSelectiveResidualsUpdated()
+        t0 = time.time()
+        hist = ol.train(ref, d["x"], radj, truth, steps=K)
+        with torch.no_grad():
+            rho = ol.dscc(ref.get_model(d["x"], radj), truth)
+        print(f"threads {th} seed {sd}: dSCC {rho:.6f}, loss {hist[-1]:.6e} ({time.time() - t0:.0f} s)", flush=True)
+        return rho, hist[-1]
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
 
 
 def main():
@@ -59,24 +76,17 @@ def main():
     d = ogr.load_input(normed.copy(), x)
     truth = ogr.cont2dist(d["y"], 0.5)
     radj = (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))
-    dscc, loss = [], []
     seeds_mode = "--seeds" in sys.argv
     runs = [(1, sd) for sd in SEEDS] if seeds_mode else [(th, 0) for th in THREADS]
-    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
-    try:
-        for th, sd in runs:
-            torch.set_num_threads(th)
-            torch.manual_seed(sd)
-            ref = og.GATNetSelectiveResidualsUpdated()
-            t0 = time.time()
-            hist = ol.train(ref, d["x"], radj, truth, steps=K)
-            with torch.no_grad():
-                dscc.append(ol.dscc(ref.get_model(d["x"], radj), truth))
-            loss.append(hist[-1])
-            print(f"threads {th} seed {sd}: dSCC {dscc[-1]:.6f}, loss {loss[-1]:.6e} ({time.time() - t0:.0f} s)",
-                  flush=True)
-    finally:
-        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    if seeds_mode:
+        # 1-thread runs: one process per seed (same arithmetic as running them one after another)
+        import multiprocessing as mpr
+        with mpr.get_context("fork").Pool(min(len(runs), os.cpu_count() or 1)) as pool:
+            res = pool.starmap(_run, [(th, sd, d, radj, truth) for th, sd in runs])
+    else:
+        res = [_run(th, sd, d, radj, truth) for th, sd in runs]
+    dscc = [r[0] for r in res]
+    loss = [r[1] for r in res]
     if seeds_mode:
         np.savez(os.path.join(HERE, "dscc_seeds_chr19_1mb.npz"), steps=np.int64(K), seeds=np.array(SEEDS),
                  dscc=np.array(dscc), loss=np.array(loss), torch=np.array(torch.__version__),
