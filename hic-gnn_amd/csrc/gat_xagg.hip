@@ -13,7 +13,7 @@
 // Same values as the h-first order up to fp32 reassociation (tests/test_dist_gloo.py,
 // tests/test_gpu_dist.py).
 //
-// Kernels (one wave per row, wave64, no atomics):
+// Kernels (wave64, no atomics; the two gather passes one row per 4-wave block, the others one wave per row):
 //   xagg_vec_kernel     v = [W_0^T att_src^0, W_1^T att_src^1, W_0^T att_dst^0, W_1^T att_dst^1] [4, 512]
 //   xagg_logits_kernel  a_src / a_dst [N, 2] = x . v (every row: the rank's neighbours are anywhere)
 //   xagg_fwd_kernel     own rows: softmax stats, then ONE gather pass over x_j accumulating
@@ -35,18 +35,24 @@
 
 namespace hicgat {
 
-// ---- v [4][512]: block b = (which, 256-column half); thread k sums 256 weights of its column ---
+// ---- v [4][512]: block b = (which, 64-column group); thread (q, k) sums the 64 weights c in
+// [64q, 64q + 64) of column k, the four quarters added in order (32 blocks: the 8-block form with a
+// 256-long chain per thread took 14 us, one launch on every step's critical path) -------------------
 __global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__ W, const float *__restrict__ att_s,
                                                        const float *__restrict__ att_d, float *__restrict__ v) {
-  const int which = blockIdx.x >> 1;                 // 0, 1: att_src heads 0, 1; 2, 3: att_dst heads 0, 1
-  const int k = (blockIdx.x & 1) * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int which = blockIdx.x >> 3;                 // 0, 1: att_src heads 0, 1; 2, 3: att_dst heads 0, 1
+  const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int k = (blockIdx.x & 7) * 64 + kl;
   const int hd = which & 1;
-  const float *att = (which < 2 ? att_s : att_d) + hd * 256;
-  const float *w = W + (size_t)hd * 256 * 512 + k;
+  const float *att = (which < 2 ? att_s : att_d) + hd * 256 + q * 64;
+  const float *w = W + ((size_t)hd * 256 + q * 64) * 512 + k;
   float s = 0.f;
 #pragma unroll 8
-  for (int c = 0; c < 256; ++c) s = fmaf(att[c], w[(size_t)c * 512], s);
-  v[which * 512 + k] = s;
+  for (int c = 0; c < 64; ++c) s = fmaf(att[c], w[(size_t)c * 512], s);
+  red[q][kl] = s;
+  __syncthreads();
+  if (q == 0) v[which * 512 + k] = ((red[0][kl] + red[1][kl]) + red[2][kl]) + red[3][kl];
 }
 
 // ---- a_src / a_dst for every row: lane l holds float4 #l and #64+l of x_n and of each v --------
@@ -73,35 +79,49 @@ __global__ __launch_bounds__(256) void xagg_logits_kernel(const float *__restric
 // ---- own rows: softmax statistics + one gather pass over x_j ---------------------------------
 // X4 [2 heads][2 kinds][rows][512]: kind 0 = xa (sum alpha x_j), kind 1 = xa2 (sum alpha lrelu' x_j);
 // row i of the launch range is local row i - row_begin.  row_stats (global rows): (max, sum) and S3.
+// One row per 4-wave block: wave w takes the row's 64-edge chunks w, w + 4, ... in every pass (max,
+// sum, gather); the partial sums meet in LDS and are added in wave order (deterministic).  A rank's
+// shard at P = 8 is ~2700 rows: one wave per row left ~2.6 waves per SIMD, each walking ~190 edges
+// serially (66 us, profiles/r03g_simprof_xa_timeline.txt).
 __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                        int row_begin, int row_end, const float *__restrict__ x,
                                                        const float *__restrict__ a_src,
                                                        const float *__restrict__ a_dst, float ns,
                                                        float *__restrict__ X4, float *__restrict__ row_stats) {
   constexpr int U = HICGAT_XAGG_U;
-  const int lane = lane_id();
-  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (i >= row_end) return;
+  __shared__ float4 part[3][8][64];      // waves 1..3: acc[hd][kd][half] per lane
+  __shared__ float red[4][4];            // per wave: (m0, m1) then (s0, s1), then (t0, t1)
+  const int lane = lane_id(), wv = wave_in_block();
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x);
+  if (i >= row_end) return;              // uniform over the block
   const int rows = row_end - row_begin, r = i - row_begin;
   const int beg = rowptr[i], end = rowptr[i + 1];
   const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
   const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
   float m0 = -INFINITY, m1 = -INFINITY;
-  for (int e = beg + lane; e < end; e += 64) {
+  for (int e = beg + 64 * wv + lane; e < end; e += 256) {
     const float2 s = as2[col[e]];
     m0 = fmaxf(m0, lrelu(s.x + ad.x, ns));
     m1 = fmaxf(m1, lrelu(s.y + ad.y, ns));
   }
   m0 = wave_max(m0);
   m1 = wave_max(m1);
+  if (lane == 0) { red[wv][0] = m0; red[wv][1] = m1; }
+  __syncthreads();
+  m0 = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+  m1 = fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1]));
   float s0 = 0.f, s1 = 0.f;
-  for (int e = beg + lane; e < end; e += 64) {
+  for (int e = beg + 64 * wv + lane; e < end; e += 256) {
     const float2 s = as2[col[e]];
     s0 += expf(lrelu(s.x + ad.x, ns) - m0);
     s1 += expf(lrelu(s.y + ad.y, ns) - m1);
   }
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
+  if (lane == 0) { red[wv][2] = s0; red[wv][3] = s1; }
+  __syncthreads();
+  s0 = ((red[0][2] + red[1][2]) + red[2][2]) + red[3][2];
+  s1 = ((red[0][3] + red[1][3]) + red[2][3]) + red[3][3];
   const float den0 = s0 + 1e-16f, den1 = s1 + 1e-16f;
   const float4 *x4 = reinterpret_cast<const float4 *>(x);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -112,7 +132,7 @@ __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ r
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b][0] = acc[a][b][1] = z4;
   float t0 = 0.f, t1 = 0.f;
-  for (int base = beg; base < end; base += 64) {
+  for (int base = beg + 64 * wv; base < end; base += 256) {
     const int e = base + lane;
     int j = i;
     float p0 = 0.f, p1 = 0.f, q0 = 0.f, q1 = 0.f;
@@ -151,6 +171,25 @@ __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ r
       }
     }
   }
+  t0 = wave_sum(t0);
+  t1 = wave_sum(t1);
+  if (wv > 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part[wv - 1][q][lane] = acc[q >> 2][(q >> 1) & 1][q & 1];
+    if (lane == 0) { red[wv][0] = t0; red[wv][1] = t1; }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 v = part[w][q][lane];
+      float4 &a = acc[q >> 2][(q >> 1) & 1][q & 1];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  t0 = ((t0 + red[1][0]) + red[2][0]) + red[3][0];
+  t1 = ((t1 + red[1][1]) + red[2][1]) + red[3][1];
   float4 *o4 = reinterpret_cast<float4 *>(X4);
 #pragma unroll
   for (int hd = 0; hd < 2; ++hd)
@@ -160,8 +199,6 @@ __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ r
       dst[lane] = acc[hd][kd][0];
       dst[64 + lane] = acc[hd][kd][1];
     }
-  t0 = wave_sum(t0);
-  t1 = wave_sum(t1);
   float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
   if (lane == 0) {
     rs4[2 * (size_t)i] = make_float4(m0, m1, s0, s1);
@@ -220,10 +257,16 @@ __global__ __launch_bounds__(256) void xagg_rows_bwd_kernel(int rows, const floa
 
 // ---- own rows: per-edge softmax-gradient terms (the destination pass of the aggregate-first form) --
 // dxa [rows][1024] (local rows): head h at columns 512h..; row_stats (global) holds delta at [4:6]
-// (agg_bwd_rows_kernel).  ds [nnz_own][2] in the rank's CSR order (rowptr[row_begin] = 0).
+// (xagg_rows_bwd).  ds [nnz_own][2] in the rank's CSR order (rowptr[row_begin] = 0).
 // xa2 != NULL (X4's kind-1 planes, local rows; the caller's forward skipped out2): the row's
 // da_dst^h = <dxa_i^h, xa2_i^h> - delta_i^h S3_i^h is formed here too, with S3 read from
 // row_stats[6:8] (xagg_rows_bwd put it there) and da_dst written over it.
+// One row per 4-wave block, the row's dxa (4 KiB) in LDS.  A wave takes 8 edges at a time, one per
+// 8-lane group: lane t of a group reads float4s t, t + 8, ..., t + 120 of its neighbour's x_j (each
+// load instruction is eight 128-B row segments, 16 loads of a lane in flight) against the LDS dxa
+// (the same address in every group: a broadcast), and the two head dots are summed over the 8 lanes
+// (3 xor-shuffle steps).  The one-wave-per-row form needed a 64-lane transposed reduction per 4
+// edges and ran at half the forward gather's rate (111 vs 64 us at P = 8, r03h_simprof_xa_timeline).
 __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                         int row_begin, int row_end, const float *__restrict__ x,
                                                         const float *__restrict__ a_src,
@@ -231,63 +274,54 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
                                                         float *__restrict__ row_stats,
                                                         const float *__restrict__ dxa, float ns,
                                                         float *__restrict__ ds, const float *__restrict__ xa2) {
-  constexpr int U = HICGAT_XAGG_U;
-  const int lane = lane_id();
-  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
-  if (i >= row_end) return;
+  __shared__ float4 dl4[256];          // dxa row: head 0 float4s 0..127, head 1 128..255
+  const int lane = lane_id(), wv = wave_in_block();
+  const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x);
+  if (i >= row_end) return;            // uniform over the block
   const int r = i - row_begin;
+  dl4[threadIdx.x] = reinterpret_cast<const float4 *>(dxa)[(size_t)r * 256 + threadIdx.x];
+  __syncthreads();
   const int beg = rowptr[i], end = rowptr[i + 1];
   const float4 *x4 = reinterpret_cast<const float4 *>(x);
-  const float4 *d4 = reinterpret_cast<const float4 *>(dxa) + (size_t)r * 256;
-  const float4 d00 = d4[lane], d01 = d4[64 + lane], d10 = d4[128 + lane], d11 = d4[192 + lane];
   const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
   const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
   const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
   const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
-  const int hh = lane >> 5;                       // after transpose_reduce<2U>: head of this lane's sum
-  constexpr int kShift = U == 8 ? 2 : U == 4 ? 3 : U == 2 ? 4 : 5;
-  const int kk = (lane >> kShift) & (U - 1);
-  const bool owner = (lane & ((1 << kShift) - 1)) == 0;
-  for (int base = beg; base < end; base += 64) {
-    const int e = base + lane;
-    int j = i;
-    float al0 = 0.f, al1 = 0.f, alp0 = 0.f, alp1 = 0.f;
-    if (e < end) {
-      j = col[e];
-      const float2 s = as2[j];
-      const float e0 = s.x + ad.x, e1 = s.y + ad.y;
-      al0 = expf(lrelu(e0, ns) - ms.x) / (ms.z + 1e-16f);
-      al1 = expf(lrelu(e1, ns) - ms.y) / (ms.w + 1e-16f);
-      alp0 = al0 * (e0 > 0.f ? 1.f : ns);
-      alp1 = al1 * (e1 > 0.f ? 1.f : ns);
+  const int g = lane >> 3, t = lane & 7;
+  for (int e0 = beg + 8 * wv; e0 < end; e0 += 32) {   // wave wv: edges e0 .. e0 + 7 of every 32
+    const int e = e0 + g;
+    const bool live = e < end;
+    const int j = live ? col[e] : i;
+    const float4 *xr = x4 + (size_t)j * 128 + t;
+    float4 xv[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) xv[c] = xr[8 * c];
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      s0 += f4_dot(xv[c], dl4[t + 8 * c]);
+      s1 += f4_dot(xv[c], dl4[128 + t + 8 * c]);
     }
-    const int cnt = min(64, end - base);
-    for (int k = 0; k < cnt; k += U) {
-      float4 va[U], vb[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const size_t jj = (size_t)readlane_i(j, k + u);   // k + u < 64: U divides 64
-        va[u] = x4[jj * 128 + lane];
-        vb[u] = x4[jj * 128 + 64 + lane];
-      }
-      float v[2 * U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        v[u] = f4_dot(d00, va[u]) + f4_dot(d01, vb[u]);
-        v[U + u] = f4_dot(d10, va[u]) + f4_dot(d11, vb[u]);
-      }
-      transpose_reduce<2 * U>(v, lane);
-      const int src = k + kk;
-      const float pa = __shfl(alp0, src), pb = __shfl(alp1, src);   // every lane shuffles (no divergence)
-      const float p = hh ? pb : pa;
-      if (owner && src < cnt) ds[2 * (size_t)(base + src) + hh] = p * (v[0] - (hh ? dl.y : dl.x));
+    for (int o = 1; o < 8; o <<= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 += __shfl_xor(s1, o);
+    }
+    if (live && t == 0) {
+      const float2 sv = as2[j];
+      const float ea = sv.x + ad.x, eb = sv.y + ad.y;
+      const float al0 = expf(lrelu(ea, ns) - ms.x) / (ms.z + 1e-16f);
+      const float al1 = expf(lrelu(eb, ns) - ms.y) / (ms.w + 1e-16f);
+      const float alp0 = al0 * (ea > 0.f ? 1.f : ns), alp1 = al1 * (eb > 0.f ? 1.f : ns);
+      reinterpret_cast<float2 *>(ds)[e] = make_float2(alp0 * (s0 - dl.x), alp1 * (s1 - dl.y));
     }
   }
-  if (xa2) {
+  if (xa2 && wv == 0) {
     const int rows = row_end - row_begin;
     const float4 *q0 = reinterpret_cast<const float4 *>(xa2) + (size_t)r * 128;                     // head 0
     const float4 *q1 = reinterpret_cast<const float4 *>(xa2) + ((size_t)2 * rows + r) * 128;         // head 1
-    float v[2] = {f4_dot(d00, q0[lane]) + f4_dot(d01, q0[64 + lane]), f4_dot(d10, q1[lane]) + f4_dot(d11, q1[64 + lane])};
+    float v[2] = {f4_dot(dl4[lane], q0[lane]) + f4_dot(dl4[64 + lane], q0[64 + lane]),
+                  f4_dot(dl4[128 + lane], q1[lane]) + f4_dot(dl4[192 + lane], q1[64 + lane])};
     transpose_reduce<2>(v, lane);
     const float p0 = readlane_f(v[0], 0), p1 = readlane_f(v[0], 32);
     if (lane == 0) {
@@ -298,9 +332,12 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
 }
 
 // ---- every row j: da_src_j = sum over the slab entries (j, i) of ds at the rank's edge (i, j), and
-// g_src^h += da_src_j^h x_j: persistent waves (wave w takes rows w, w + W, ...), lanes over a row's
-// entries (float2 wave sum), then x_j's 512 columns (8 per lane) into the wave's two 512-column
-// partial rows; part [W][2][512] is summed in wave order by xagg_colred_kernel (no atomics). ------
+// g_src^h += da_src_j^h x_j: persistent waves, each taking 4 rows at a time (rows 4w .. 4w + 3, then
+// + 4W): 16-lane group q sums row 4w + q's entries (float2, 4 xor-shuffle steps), then the four x_j
+// rows (8 columns per lane) go into the wave's two 512-column partial rows in row order; part
+// [W][2][512] is summed in wave order by xagg_colred_kernel (no atomics).  Four rows per pass
+// overlap their rowptr -> perm -> ds load chains (one row per pass: ~20 rows x 3 dependent loads per
+// wave, 31-46 us at P = 8, profiles/r03h_simprof_xa_timeline.txt). ------------------------------------
 constexpr int kSlabWaves = 1024;   // partial rows of g_src (256 workgroups x 4 waves)
 __global__ __launch_bounds__(256) void xagg_slab_sum_kernel(const int *__restrict__ rowptr_s,
                                                             const int *__restrict__ perm, int N,
@@ -309,25 +346,39 @@ __global__ __launch_bounds__(256) void xagg_slab_sum_kernel(const int *__restric
                                                             float *__restrict__ da_src, float *__restrict__ part) {
   const int lane = lane_id();
   const int w = blockIdx.x * 4 + wave_in_block(), W = gridDim.x * 4;
+  const int q = lane >> 4, t = lane & 15;
   const float2 *ds2 = reinterpret_cast<const float2 *>(ds);
   const float4 *x4 = reinterpret_cast<const float4 *>(x);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 g00 = z4, g01 = z4, g10 = z4, g11 = z4;   // head 0 / 1, columns 4l.. / 256+4l..
-  for (int j = w; j < N; j += W) {
+  for (int j0 = 4 * w; j0 < N; j0 += 4 * W) {
+    const int j = j0 + q;
     float a = 0.f, b = 0.f;
-    for (int k = rowptr_s[j] + lane; k < rowptr_s[j + 1]; k += 64) {
-      const float2 v = ds2[perm[k]];
-      a += v.x;
-      b += v.y;
+    if (j < N) {
+      const int k1 = rowptr_s[j + 1];
+      for (int k = rowptr_s[j] + t; k < k1; k += 16) {
+        const float2 v = ds2[perm[k]];
+        a += v.x;
+        b += v.y;
+      }
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) reinterpret_cast<float2 *>(da_src)[j] = make_float2(a, b);
-    const float4 xa = x4[(size_t)j * 128 + lane], xb = x4[(size_t)j * 128 + 64 + lane];
-    g00 = f4_fma(a, xa, g00);
-    g01 = f4_fma(a, xb, g01);
-    g10 = f4_fma(b, xa, g10);
-    g11 = f4_fma(b, xb, g11);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      a += __shfl_xor(a, o);
+      b += __shfl_xor(b, o);
+    }
+    if (t == 0 && j < N) reinterpret_cast<float2 *>(da_src)[j] = make_float2(a, b);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int jj = j0 + u;
+      if (jj >= N) break;
+      const float au = __shfl(a, 16 * u), bu = __shfl(b, 16 * u);
+      const float4 xa = x4[(size_t)jj * 128 + lane], xb = x4[(size_t)jj * 128 + 64 + lane];
+      g00 = f4_fma(au, xa, g00);
+      g01 = f4_fma(au, xb, g01);
+      g10 = f4_fma(bu, xa, g10);
+      g11 = f4_fma(bu, xb, g11);
+    }
   }
   float4 *p4 = reinterpret_cast<float4 *>(part) + (size_t)w * 256;
   p4[lane] = g00;
@@ -410,7 +461,7 @@ extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *a
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (!W || !att_src || !att_dst || !vec) return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(xagg_vec_kernel, dim3(8), dim3(256), 0, s, W, att_src, att_dst, vec);
+  hipLaunchKernelGGL(xagg_vec_kernel, dim3(32), dim3(256), 0, s, W, att_src, att_dst, vec);
   HICGAT_CHECK_LAUNCH();
   if (N == 0) return HICGAT_OK;
   if (!x || !a_src || !a_dst) return HICGAT_EINVAL;
@@ -426,7 +477,7 @@ extern "C" int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N,
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (row_end == row_begin) return HICGAT_OK;
   if (!rowptr || !col || !x || !a_src || !a_dst || !X4 || !row_stats) return HICGAT_EINVAL;
-  hipLaunchKernelGGL(xagg_fwd_kernel, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, (hipStream_t)stream, rowptr,
+  hipLaunchKernelGGL(xagg_fwd_kernel, dim3(row_end - row_begin), dim3(256), 0, (hipStream_t)stream, rowptr,
                      col, row_begin, row_end, x, a_src, a_dst, neg_slope, X4, row_stats);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
@@ -468,7 +519,7 @@ extern "C" int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (row_end == row_begin) return HICGAT_OK;
   if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !ds) return HICGAT_EINVAL;
-  hipLaunchKernelGGL(xagg_edge_kernel, dim3((row_end - row_begin + 3) / 4), dim3(256), 0, (hipStream_t)stream, rowptr,
+  hipLaunchKernelGGL(xagg_edge_kernel, dim3(row_end - row_begin), dim3(256), 0, (hipStream_t)stream, rowptr,
                      col, row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, ds, xa2);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;

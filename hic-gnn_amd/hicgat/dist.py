@@ -58,6 +58,9 @@ TILE = 128
 MODES = ("slab", "xagg", "allgather")
 # "xagg": head 1's GEMMs on a second stream beside head 0's (1, default) or both on one stream (0)
 HEAD_STREAM = os.environ.get("HICGAT_HEAD_STREAM", "1") != "0"
+# side streams for the MLP tail's queued parameter-gradient launches in the sharded step
+# (ops.side_flush lanes; 1 = one chain as on a single GPU)
+SIDE_LANES = int(os.environ.get("HICGAT_DIST_SIDE_LANES", "3"))
 
 
 def partition_rows(rowptr, P):
@@ -454,7 +457,7 @@ class ShardedTrainer:
             # dh_r / da_src_r (complete when summed over ranks -- through dW and datt below)
             K.agg_bwd_src(self.rowptr_s, self.col_s, 0, N, self.h, a_src, a_dst, self.rs, dout, al, ar, self.ns,
                           self.dh, self.da_src, round_robin=True)
-            ops.side_flush(after=fork)
+            ops.side_flush(after=fork, lanes=SIDE_LANES)
             tail_done = self._side_event()
             with torch.no_grad():
                 # lin_l's partial dW over all rows (x replicated) on a side stream of its own (lane 2:
@@ -513,25 +516,35 @@ class ShardedTrainer:
             coords_loc.backward(self.dcoords[r0:r1])
             rs_own = self.rs[r0:r1]
             K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
-            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
             # dxa^hd = dout^hd W_hd
             self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
                                           self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx"))
+            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
+            # dW_h += dout^h^T xa^h (K = own rows, split) and dbias on side lanes 2 / 3, forked after the
+            # dxa GEMMs so they run beside the edge pass and the slab sum (issued after the slab sum
+            # they were ~60 us of the critical path at P = 8, forked before the dxa GEMMs a captured
+            # step ran them first and delayed the dxa GEMMs by as much, profiles/r03g_*, r03h_*);
+            # joined before xagg_param_finish adds into dW
+            with torch.no_grad():
+                for hd in (0, 1):
+                    with ops._side(self.dout_l, self.X4, lane=2 + hd):
+                        K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
+                               self.W.grad[hd * C:(hd + 1) * C], accumulate=True, splits=ops._splits(C, F, Rl),
+                               name="gemm_dw")
+                if self.bias is not None:
+                    with ops._side(self.dout_l, lane=2):
+                        K.colsum(self.dout_l, self.bias.grad, accumulate=True)
             K.xagg_edge(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                         self.ds, xa2=self.X4[:, 1])
             K.xagg_slab_sum(self.rowptr_s, self.perm_s, self.ds, self.x, self.da_src, self.g_src)
-            ops.side_flush(after=fork)
+            ops.side_flush(after=fork, lanes=SIDE_LANES)
             tail_done = self._side_event()
             with torch.no_grad():
                 K.param_grad(self.x2[r0:r1], None, None, rs_own, H, out=(None, self.g_dst, None))
-                if self.bias is not None:
-                    K.colsum(self.dout_l, self.bias.grad, accumulate=True)
-                # dW_hd += dout^hd^T xa^hd (K = own rows, split)
-                self._heads(lambda hd: K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
-                                              self.W.grad[hd * C:(hd + 1) * C], accumulate=True,
-                                              splits=ops._splits(C, F, Rl), name="gemm_dw"))
-                K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
-                                    self.att_r.grad.view(-1))
+        # after the join: the side lanes' dW_h are in W.grad
+        with torch.no_grad():
+            K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
+                                self.att_r.grad.view(-1))
         return coords, tail_done
 
     def _step_allgather(self):
@@ -560,7 +573,7 @@ class ShardedTrainer:
             self.comm.all_gather_inplace(self.pack, self._own(self.pack))
             K.agg_bwd_src(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, rs_all, dout, al, ar, self.ns,
                           self.dh, self.da_src)
-            ops.side_flush(after=fork)
+            ops.side_flush(after=fork, lanes=SIDE_LANES)
             tail_done = self._side_event()
             dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
             with torch.no_grad():

@@ -41,6 +41,29 @@ class _timed:
 
 P = _lib.ptr
 
+# K-split of a node-row GEMM (Linear forward / input gradient: M = rows) that would leave the chip
+# mostly idle: a rank's shard of the multi-GPU step (M ~ 2700 rows at P = 8) gives the 64 x 128
+# kernel 43 x 4 = 172 workgroups with the whole K = 512 each, one per CU, latency-bound per K-step
+# (38 us for 1.4 GFLOP, profiles/r03f_simprof_*_timeline.txt; split in 3: 28 + 7 us for the slab
+# sum).  Split over K until ~512 workgroups are in flight (each split >= 128 deep), partial slabs
+# added in split order (deterministic).  The tall 160 x 128 kernel split the same way (a grid.y of
+# K-chunks into slabs) measured slower at these shapes (r03i: 23-33 + 8 us) and was not kept.
+# Shapes that fill the chip on their own -- every single-GPU shape at N = 20000 (the tall kernel,
+# or >= 256 tiles) -- keep splits = 1.  HICGAT_ROW_SPLIT=0: off (A/B).
+ROW_SPLIT = os.environ.get("HICGAT_ROW_SPLIT", "1") != "0"
+_TALL_MIN_TILES = int(os.environ.get("HICGAT_TALL_MIN_TILES", "192"))   # gemm.hip tall_min_tiles()
+
+
+def row_splits(M, N, K):
+    if not ROW_SPLIT or M < 1024 or K < 256:
+        return 1
+    if -(-M // 160) * (N // 128) >= _TALL_MIN_TILES:      # the tall kernel takes it (gemm.hip dispatch)
+        return 1
+    wgs = -(-M // 64) * -(-N // (128 if N >= 128 else 64))
+    if wgs >= 256:
+        return 1
+    return max(1, min(K // 128, -(-512 // wgs)))
+
 
 class HipKernels:
     """The MI355X implementation of the kernel interface."""
@@ -323,13 +346,17 @@ class HipKernels:
         return dc
 
     # -- a6: Linear layers on the MFMA GEMM (fp32, or the fp32-accurate x3 split) ------------------
-    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=1, name="gemm",
+    def gemm(self, a_kmajor, b_kmajor, M, N, K, A, B, C, bias=None, accumulate=False, splits=None, name="gemm",
              impl=None):
+        """``splits=None``: ``row_splits`` for node-row (row-major A) fp32 problems, else 1; an int is
+        taken as given."""
         dev = C.device
         ws = None
+        impl = self.gemm_impl if impl is None else impl
+        if splits is None:
+            splits = row_splits(M, N, K) if (not a_kmajor and impl == 1) else 1
         if splits > 1:
             ws = _lib.workspace(self.lib.hicgat_gemm_workspace_bytes(M, N, splits), dev)
-        impl = self.gemm_impl if impl is None else impl
         with _timed(name):
             _lib.check(self.lib.hicgat_gemm_ex(int(a_kmajor), int(b_kmajor), M, N, K, P(A), A.stride(0), P(B),
                                                B.stride(0), P(bias), P(C), C.stride(0), int(accumulate), int(splits),

@@ -83,14 +83,36 @@ def side_mark():
     return ev
 
 
-def side_flush(after=None):
+_FLUSH_LANES = (0, 4, 5, 6)
+
+
+def side_flush(after=None, lanes=1):
     """Issue the queued parameter-gradient launches on the side stream, forked from the current
     stream at this point, or from the earlier point ``after`` (an event from ``side_mark``): the
     caller can then enqueue its own next kernel first, so a captured graph lists that kernel
-    ahead of the side branch (they read only tensors produced before the fork point)."""
+    ahead of the side branch (they read only tensors produced before the fork point).
+
+    ``lanes`` > 1 spreads the launches over that many side streams (largest work first, each to the
+    least-loaded lane; every launch writes its own parameters' gradients, so they are independent):
+    a rank's shard of the multi-GPU step has a gather window too short for the tail's ~13 queued
+    launches in one chain (170 us at P = 8, profiles/r03i_simprof_xa_timeline.txt).  The
+    single-GPU step keeps one lane (a second one measured slower there)."""
     with _SIDE_LOCK:
         queue, _SIDE["queue"] = _SIDE["queue"], []
     if not queue:
+        return
+    if lanes > 1 and SIDE_BIG == 0:
+        n = min(lanes, len(_FLUSH_LANES))
+        load, parts = [0] * n, [[] for _ in range(n)]
+        for item in sorted(queue, key=lambda q: -q[2]):
+            k = min(range(n), key=lambda a: (load[a], len(parts[a])))
+            parts[k].append(item)
+            load[k] += item[2]
+        for lane, items in zip(_FLUSH_LANES, parts):
+            if items:
+                with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
+                    for fn, _, _ in items:
+                        fn()
         return
     if SIDE_ORDER == "size":
         queue.sort(key=lambda q: -q[2])

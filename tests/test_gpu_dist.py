@@ -123,12 +123,67 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
+# Graph sizes of the comparisons between the aggregate-first form and the h-first / float64 ones.
+# Their fp32 forwards differ by rounding (~1e-7 relative), so a relu input closer to 0 than that can
+# fall on the other side of the kink in the two runs, and that one element's gradient then differs
+# by its whole value (the reference's own arithmetic is discontinuous there).  At the first step
+# LayerNorm's beta is 0, so such an element sits at xhat ~ 0: the signature is a wrong dbeta / dW of
+# one block with dgamma exact.  n = 777 has a block-2 LN output at |z| = 6e-8 and showed exactly that
+# (profiles/r03_relu_margin.txt, tools/relu_margin.py); these sizes keep every LN input >= 4e-6
+# from 0 (test_xagg_comparison_sizes_are_kink_free checks it).
+XAGG_NS = (300, 700)
+LN_MARGIN = 1e-6
+
+
+def tail_margins(model, o):
+    """min |pre-relu| of the flagship's three LayerNorm blocks (models.py:637-655), float64, from
+    the tail input ``o`` (the relu'd GATConv output)."""
+    d = torch.float64
+    x = o.detach().to(d)
+
+    def lin(layer, v):
+        return v @ layer.weight.detach().to(d).t() + layer.bias.detach().to(d)
+
+    def ln(norm, v):
+        mu = v.mean(1, keepdim=True)
+        var = ((v - mu) ** 2).mean(1, keepdim=True)
+        return (v - mu) / torch.sqrt(var + norm.eps) * norm.weight.detach().to(d) + norm.bias.detach().to(d)
+
+    z1 = ln(model.norm_a, lin(model.densea, x))
+    x1 = torch.relu(z1) + lin(model.align_densea, x)
+    z2 = ln(model.norm1, lin(model.dense1, x1))
+    x2 = torch.relu(z2) + lin(model.align_dense1, x1)
+    z3 = ln(model.norm2, lin(model.dense2, x2))
+    return [float(z.abs().min()) for z in (z1, z2, z3)]
+
+
+def xagg_margins(n):
+    """One world-1 "xagg" step (SimComm: a single rank's collectives are identities); the LN margins
+    of its forward, from the seed-0 (step-1) weights."""
+    hicgat, adj, truth, x = _inputs(n, "cuda")
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+    tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode="xagg", comm=hicgat.dist.SimComm(1, 0))
+    tr.step()
+    torch.cuda.synchronize()
+    torch.manual_seed(0)
+    m0 = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+    return float(tr.Y0.abs().min()), tail_margins(m0, tr.O)
+
+
+def test_xagg_comparison_sizes_are_kink_free():
+    for n in XAGG_NS:
+        y0, ln = xagg_margins(n)
+        print(n, y0, ln)
+        assert min(ln) >= LN_MARGIN, (n, ln, "a LayerNorm input sits at the relu kink: pick another size")
+
+
 @pytest.mark.parametrize("mode", ["slab", "xagg"])
 def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode):
     """World 1 over RCCL vs the single-GPU step; the aggregate-first form ("xagg": out = W (sum
     alpha x) + b, gat_xagg.hip) rounds the GATConv differently: loss to the north star's 1e-5,
-    gradients to 1e-4 of their max (fp32 reassociation)."""
-    n = 777
+    gradients to 1e-4 of their max (fp32 reassociation), at a kink-free size (XAGG_NS)."""
+    n = 777 if mode == "slab" else XAGG_NS[1]
     res = _run(1, "nccl", n, tmp_path, mode)
     hicgat, adj, truth, x = _inputs(n, "cuda")
     torch.manual_seed(0)
@@ -185,8 +240,7 @@ def test_simulated_ranks_run_their_shares(mode):
     assert tot["srows"] == 777 and tot["tiles"] == tr.plan.tiles
 
 
-@pytest.mark.parametrize("n", [300, 777])
-@pytest.mark.parametrize("mode", ["slab", "xagg"])
+@pytest.mark.parametrize("mode,n", [("slab", 300), ("slab", 777), ("xagg", XAGG_NS[0]), ("xagg", XAGG_NS[1])])
 def test_world1_step_matches_float64_standin(mode, n):
     """One world-1 step of each form on the HIP kernels against the same step on the float64 torch
     stand-ins (tests/cpu_kernels.py, tied to the autograd oracle by tests/test_dist_gloo.py), per

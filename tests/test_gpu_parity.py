@@ -313,6 +313,34 @@ def test_tall_gemm_edges_and_accumulate(m, n, k):
         assert _rel(ys.cpu(), (xs.double() @ w.double().t() + b.double()).cpu()) < 5e-6
 
 
+@pytest.mark.parametrize("m,n,k", [(2701, 512, 512), (2479, 256, 512), (2701, 512, 256), (1601, 384, 272),
+                                   (3001, 192, 512)])
+def test_row_split_gemm_matches_fp64(m, n, k):
+    """Node-row GEMMs of a rank's shard (kernels.row_splits: the 64x128 kernel split over K into
+    slabs added in split order), both B layouts, into a column slice of a wider output (ldc > N), with
+    bias and accumulate, against fp64; and against the unsplit kernel (splits=1) to fp32 rounding."""
+    import hicgat
+    from hicgat import kernels as hk
+    K = hicgat.kernels.default()
+    assert hk.row_splits(m, n, k) > 1 and hk.row_splits(m, k, n) >= 1
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV)
+    w = torch.randn(n, k, device=DEV)
+    b = torch.randn(n, device=DEV)
+    big = torch.randn(m, n + 64, device=DEV)
+    ref = x.double() @ w.double().t() + b.double() + big[:, 32:32 + n].double()
+    out = big.clone()
+    K.gemm(0, 0, m, n, k, x, w, out[:, 32:32 + n], bias=b, accumulate=True)
+    assert _rel(out[:, 32:32 + n].cpu(), ref.cpu()) < 5e-6
+    assert torch.equal(out[:, :32], big[:, :32]) and torch.equal(out[:, 32 + n:], big[:, 32 + n:])
+    one = K.gemm(0, 0, m, n, k, x, w, torch.empty(m, n, device=DEV), bias=b, splits=1)
+    spl = K.gemm(0, 0, m, n, k, x, w, torch.empty(m, n, device=DEV), bias=b)
+    assert _rel(spl.cpu(), one.double().cpu()) < 5e-6
+    dy = torch.randn(m, n, device=DEV)
+    dx = K.gemm(0, 1, m, k, n, dy, w, torch.empty(m, k, device=DEV))
+    assert _rel(dx.cpu(), (dy.double() @ w.double()).cpu()) < 5e-6
+
+
 @pytest.mark.parametrize("m,n,k,splits", [(128, 128, 1001, 3), (512, 256, 17, 1), (256, 128, 20000, 1),
                                           (128, 384, 4099, 64), (512, 512, 20000, 32)])
 def test_wgrad_ragged_strided(m, n, k, splits):
