@@ -309,6 +309,7 @@ def simulate_world(args):
     import hicgat
     from hicgat import dist as hdist
     P = args.simulate_world
+    mode = hdist.resolve_mode(args.dist_mode, P)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     wl = build_workload(args.workload, args.seed, dev)
@@ -318,7 +319,7 @@ def simulate_world(args):
         torch.manual_seed(0)
         model = hicgat.MODELS[args.model]().to(dev)
         tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], truth, lr=1e-3, kind=args.loss,
-                                  mode=args.dist_mode, comm=hdist.SimComm(P, r))
+                                  mode=mode, comm=hdist.SimComm(P, r))
         step = tr.captured(warmup=max(1, args.warmup))
         torch.cuda.synchronize()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -343,7 +344,7 @@ def simulate_world(args):
             # the tail's bucket runs on the comm stream beside lin_l's dW GEMM: only the GATConv's
             # bucket (W 512x512 + att + bias) is on the critical path
             "grad_all_reduce_gat_bucket": _coll_us("all_reduce", 4 * (512 * 512 + 3 * 512), P)}
-    if args.dist_mode == "allgather":
+    if mode == "allgather":
         coll["h_all_gather"] = _coll_us("all_gather", P * R * D * 4, P)
         coll["pack_all_gather"] = _coll_us("all_gather", P * R * (D + 8) * 4, P)
     exposed_us = sum(coll.values())
@@ -354,8 +355,8 @@ def simulate_world(args):
         "ms_per_step": model_ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
         "config": {"workload": args.workload, "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz,
-                   "parallelism": f"dst-row shard x{P} ({args.dist_mode}), SIMULATED one rank at a time on 1 GPU"},
-        "simulated": {"world": P, "mode": args.dist_mode, "rank_ms": rank_ms, "rank_median_ms": rank_med,
+                   "parallelism": f"dst-row shard x{P} ({mode}), SIMULATED one rank at a time on 1 GPU"},
+        "simulated": {"world": P, "mode": mode, "rank_ms": rank_ms, "rank_median_ms": rank_med,
                       "shards": shards, "collectives_us": coll, "exposed_collectives_us": exposed_us,
                       "model_ms_per_step": model_ms,
                       "assumptions": {"rccl_latency_us": RCCL_LAT_US, "rccl_bus_GBps": RCCL_BUS_GBS,
@@ -376,9 +377,11 @@ def main():
                     choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
                     help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
                          "N > 1 shards the GAT models only")
-    ap.add_argument("--dist-mode", default="slab", choices=["slab", "xagg", "allgather"],
-                    help="N > 1: the slab form (default: x replicated, h recomputed per rank, source pass split by "
-                         "destination owner -- no h / dout all-gathers) or the all-gather of h before the layer")
+    ap.add_argument("--dist-mode", default="auto", choices=["auto", "slab", "xagg", "allgather"],
+                    help="N > 1: auto (default: slab at N = 2, xagg from N = 4 -- the faster per world size, "
+                         "hicgat.dist.resolve_mode), slab (x replicated, h recomputed per rank, source pass split by "
+                         "destination owner -- no h / dout all-gathers), xagg (aggregate-first GATConv: x replicated, "
+                         "every GEMM on own rows) or allgather (the RCCL all-gather of h before the layer)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="one GPU: time each rank's share of a P-rank sharded step, collectives left out")
     ap.add_argument("--sim-rank", type=int, default=None, help="--simulate-world: only this rank (profiling)")
@@ -579,7 +582,7 @@ def main():
         "config": {"workload": args.workload if not args.selftest_cpu else "selftest-400",
                    "n_nodes": n, "nnz_with_self_loops": nnz, "d": D_FEAT, "heads": HEADS,
                    "loss": args.loss,
-                   "parallelism": (f"dst-row shard x{world} (nnz-balanced, {args.dist_mode})" if sharded else "single"),
+                   "parallelism": (f"dst-row shard x{world} (nnz-balanced, {runner.mode})" if sharded else "single"),
                    "gemm": ({0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl]
                             if not args.selftest_cpu else "cpu stand-in")},
         "final_loss": loss_v,
@@ -588,7 +591,7 @@ def main():
         "kernels": kern_t,
     }
     if sharded:
-        result["shard"] = {"mode": args.dist_mode, "rows_per_rank": [int(v) for v in runner.plan.counts],
+        result["shard"] = {"mode": runner.mode, "rows_per_rank": [int(v) for v in runner.plan.counts],
                            "nnz_per_rank": [int(v) for v in runner.plan.nnz]}
     if graph_error is not None:
         result["graph_error"] = graph_error

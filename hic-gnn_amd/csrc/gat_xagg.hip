@@ -32,6 +32,9 @@
 #ifndef HICGAT_XAGG_U
 #define HICGAT_XAGG_U 4   // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
 #endif
+#ifndef HICGAT_XAGG_GL
+#define HICGAT_XAGG_GL 16   // edge pass: lanes per edge (8: 16 float4 per lane, 238 VGPRs, 2 waves per SIMD)
+#endif
 
 namespace hicgat {
 
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(256) void xagg_logits_kernel(const float *__restric
 // One row per 4-wave block: wave w takes the row's 64-edge chunks w, w + 4, ... in every pass (max,
 // sum, gather); the partial sums meet in LDS and are added in wave order (deterministic).  A rank's
 // shard at P = 8 is ~2700 rows: one wave per row left ~2.6 waves per SIMD, each walking ~190 edges
-// serially (66 us, profiles/r03g_simprof_xa_timeline.txt).
+// serially (66 us, profiles/r03g_simprof_xagg_P8_rank0_timeline.txt).
 __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                        int row_begin, int row_end, const float *__restrict__ x,
                                                        const float *__restrict__ a_src,
@@ -261,12 +264,15 @@ __global__ __launch_bounds__(256) void xagg_rows_bwd_kernel(int rows, const floa
 // xa2 != NULL (X4's kind-1 planes, local rows; the caller's forward skipped out2): the row's
 // da_dst^h = <dxa_i^h, xa2_i^h> - delta_i^h S3_i^h is formed here too, with S3 read from
 // row_stats[6:8] (xagg_rows_bwd put it there) and da_dst written over it.
-// One row per 4-wave block, the row's dxa (4 KiB) in LDS.  A wave takes 8 edges at a time, one per
-// 8-lane group: lane t of a group reads float4s t, t + 8, ..., t + 120 of its neighbour's x_j (each
-// load instruction is eight 128-B row segments, 16 loads of a lane in flight) against the LDS dxa
-// (the same address in every group: a broadcast), and the two head dots are summed over the 8 lanes
-// (3 xor-shuffle steps).  The one-wave-per-row form needed a 64-lane transposed reduction per 4
-// edges and ran at half the forward gather's rate (111 vs 64 us at P = 8, r03h_simprof_xa_timeline).
+// One row per 4-wave block, the row's dxa (4 KiB) in LDS.  A wave takes 64/GL edges at a time, one
+// per GL-lane group: lane t of a group reads float4s t, t + GL, ... of its neighbour's x_j (each load
+// instruction is 64/GL row segments of 16 GL bytes, 128/GL loads of a lane in flight) against the LDS
+// dxa (the same address in every group: a broadcast), and the two head dots are summed over the GL
+// lanes (log2 GL xor-shuffle steps), no 64-lane transposed reduction per 4 edges as in the former
+// one-wave-per-row form.  Measured at P = 8 beside the side lanes' dW GEMMs: 111 us (wave per row),
+// 100 (GL = 8, 238 VGPRs), 112 (GL = 16) -- against 64 us for the forward's gather of the same rows
+// alone (profiles/r03h_/r03i_/r03k_simprof_xagg_P8_rank0_timeline.txt): the pass shares the CUs
+// with the GEMMs there, so its time is not its own rate.
 __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                         int row_begin, int row_end, const float *__restrict__ x,
                                                         const float *__restrict__ a_src,
@@ -287,23 +293,24 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
   const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
   const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
   const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
-  const int g = lane >> 3, t = lane & 7;
-  for (int e0 = beg + 8 * wv; e0 < end; e0 += 32) {   // wave wv: edges e0 .. e0 + 7 of every 32
+  constexpr int GL = HICGAT_XAGG_GL, NG = 64 / GL, NC = 128 / GL;   // lanes per edge, edges per wave, float4s per lane
+  const int g = lane / GL, t = lane % GL;
+  for (int e0 = beg + NG * wv; e0 < end; e0 += 4 * NG) {   // wave wv: edges e0 .. e0 + NG - 1 of every 4 NG
     const int e = e0 + g;
     const bool live = e < end;
     const int j = live ? col[e] : i;
     const float4 *xr = x4 + (size_t)j * 128 + t;
-    float4 xv[16];
+    float4 xv[NC];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) xv[c] = xr[8 * c];
+    for (int c = 0; c < NC; ++c) xv[c] = xr[GL * c];
     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      s0 += f4_dot(xv[c], dl4[t + 8 * c]);
-      s1 += f4_dot(xv[c], dl4[128 + t + 8 * c]);
+    for (int c = 0; c < NC; ++c) {
+      s0 += f4_dot(xv[c], dl4[t + GL * c]);
+      s1 += f4_dot(xv[c], dl4[128 + t + GL * c]);
     }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
+    for (int o = 1; o < GL; o <<= 1) {
       s0 += __shfl_xor(s0, o);
       s1 += __shfl_xor(s1, o);
     }
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
 // rows (8 columns per lane) go into the wave's two 512-column partial rows in row order; part
 // [W][2][512] is summed in wave order by xagg_colred_kernel (no atomics).  Four rows per pass
 // overlap their rowptr -> perm -> ds load chains (one row per pass: ~20 rows x 3 dependent loads per
-// wave, 31-46 us at P = 8, profiles/r03h_simprof_xa_timeline.txt). ------------------------------------
+// wave, 31-46 us at P = 8, profiles/r03h_simprof_xagg_P8_rank0_timeline.txt). ------------------------------------
 constexpr int kSlabWaves = 1024;   // partial rows of g_src (256 workgroups x 4 waves)
 __global__ __launch_bounds__(256) void xagg_slab_sum_kernel(const int *__restrict__ rowptr_s,
                                                             const int *__restrict__ perm, int N,

@@ -9,7 +9,7 @@ rowptr is the prefix sum), every rank keeping at least one row; the upper-triang
 contiguous ranges; the loss's support rows (the contact set of cont2dist's target) in P blocks
 balanced by support nnz.
 
-Two step forms (``mode``):
+Three step forms (``mode``; "auto" picks slab at P = 2 and xagg from P = 4, ``resolve_mode``):
 
 ``"slab"`` (default) -- no per-step collective larger than the 2.4 MB gradient buffer.  The 512-d
   node embeddings x are constant, so they are all-gathered ONCE (every rank holds all of x, 41 MB)
@@ -56,6 +56,17 @@ from .optim import FlatAdam
 
 TILE = 128
 MODES = ("slab", "xagg", "allgather")
+# "auto" (bench.py's default): the form measured faster per world size on the N = 20000 graph
+# (bench.py --simulate-world, profiles/r03*_simrank_*): at P = 2 the slab form (1.37 vs 1.48 ms
+# modeled: 10000-row shards keep its replicated lin_l GEMMs cheap next to the xagg edge pass), from
+# P = 4 on the aggregate-first form (P = 8: 0.71 vs 0.84 ms: no replicated O(N d^2) work at all)
+AUTO_XAGG_MIN_P = int(os.environ.get("HICGAT_AUTO_XAGG_MIN_P", "4"))
+
+
+def resolve_mode(mode, P):
+    if mode == "auto":
+        return "xagg" if P >= AUTO_XAGG_MIN_P else "slab"
+    return mode
 # "xagg": head 1's GEMMs on a second stream beside head 0's (1, default) or both on one stream (0)
 HEAD_STREAM = os.environ.get("HICGAT_HEAD_STREAM", "1") != "0"
 # side streams for the MLP tail's queued parameter-gradient launches in the sharded step
@@ -241,11 +252,12 @@ class ShardedTrainer:
         if kern is None:
             from .kernels import default
             kern = default()
+        self.comm = comm if comm is not None else DistComm(group)
+        mode = resolve_mode(mode, self.comm.P)
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
         self.K = kern
         self.model = model
-        self.comm = comm if comm is not None else DistComm(group)
         self.group = group
         self.P = P = self.comm.P
         self.rank = rank = self.comm.rank
@@ -523,7 +535,7 @@ class ShardedTrainer:
             # dW_h += dout^h^T xa^h (K = own rows, split) and dbias on side lanes 2 / 3, forked after the
             # dxa GEMMs so they run beside the edge pass and the slab sum (issued after the slab sum
             # they were ~60 us of the critical path at P = 8, forked before the dxa GEMMs a captured
-            # step ran them first and delayed the dxa GEMMs by as much, profiles/r03g_*, r03h_*);
+            # step ran them first and delayed the dxa GEMMs by as much, profiles/r03g_* / r03h_simprof_xagg_*);
             # joined before xagg_param_finish adds into dW
             with torch.no_grad():
                 for hd in (0, 1):

@@ -44,7 +44,7 @@ P = _lib.ptr
 # K-split of a node-row GEMM (Linear forward / input gradient: M = rows) that would leave the chip
 # mostly idle: a rank's shard of the multi-GPU step (M ~ 2700 rows at P = 8) gives the 64 x 128
 # kernel 43 x 4 = 172 workgroups with the whole K = 512 each, one per CU, latency-bound per K-step
-# (38 us for 1.4 GFLOP, profiles/r03f_simprof_*_timeline.txt; split in 3: 28 + 7 us for the slab
+# (38 us for 1.4 GFLOP, profiles/r03f_simprof_*_P8_rank0_timeline.txt; split in 3: 28 + 7 us for the slab
 # sum).  Split over K until ~512 workgroups are in flight (each split >= 128 deep), partial slabs
 # added in split order (deterministic).  The tall 160 x 128 kernel split the same way (a grid.y of
 # K-chunks into slabs) measured slower at these shapes (r03i: 23-33 + 8 us) and was not kept.

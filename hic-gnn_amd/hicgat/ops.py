@@ -66,6 +66,8 @@ SIDE_BIG = float(os.environ.get("HICGAT_SIDE_BIG", "0"))
 # beside the gather slows it more than the 30 us it takes off the tail); 0 (default): all three
 # behind the source pass
 PG_SPLIT = os.environ.get("HICGAT_PG_SPLIT", "0") != "0"
+# side streams for the single-GPU step's deferred side work (side_flush lanes; 1 = one chain)
+SIDE_LANES = int(os.environ.get("HICGAT_SIDE_LANES", "1"))
 
 
 def side_begin():
@@ -95,7 +97,7 @@ def side_flush(after=None, lanes=1):
     ``lanes`` > 1 spreads the launches over that many side streams (largest work first, each to the
     least-loaded lane; every launch writes its own parameters' gradients, so they are independent):
     a rank's shard of the multi-GPU step has a gather window too short for the tail's ~13 queued
-    launches in one chain (170 us at P = 8, profiles/r03i_simprof_xa_timeline.txt).  The
+    launches in one chain (170 us at P = 8, profiles/r03i_simprof_xagg_P8_rank0_timeline.txt).  The
     single-GPU step keeps one lane (a second one measured slower there)."""
     with _SIDE_LOCK:
         queue, _SIDE["queue"] = _SIDE["queue"], []
@@ -315,7 +317,7 @@ class _GATConvFn(torch.autograd.Function):
             else:
                 K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
             if c == 0:
-                side_flush(after=fork)
+                side_flush(after=fork, lanes=SIDE_LANES)
             rows = slice(r0, r1)
             if use_sinks:
                 # on a second side stream (PG_SIDE), beside lin_l's dW GEMM on this one, or in front of it

@@ -14,7 +14,8 @@
 #   pmc_traffic  two PMC passes (FETCH_SIZE, WRITE_SIZE) of an eager bench -> <tag>_pmc_traffic.json
 #   pmc_mfma     one PMC pass (MFMA busy cycles, F32 MFMA MOPs, GRBM_GUI_ACTIVE) -> <tag>_pmc_mfma.json
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
-#   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world; _ag: allgather form)
+#   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world; _ag: allgather
+#                form, _xa: aggregate-first form, _au: bench.py's default "auto")
 #   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
 #   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
@@ -76,8 +77,8 @@ for S in "$@"; do
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json $W \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager" \
         "$COMMIT" || exit $? ;;
-    simrank|simrank_ag|simrank_xa)
-      M=slab; [ "$S" = simrank_ag ] && M=allgather; [ "$S" = simrank_xa ] && M=xagg
+    simrank|simrank_ag|simrank_xa|simrank_au)
+      M=slab; [ "$S" = simrank_ag ] && M=allgather; [ "$S" = simrank_xa ] && M=xagg; [ "$S" = simrank_au ] && M=auto
       for P in 2 4 8; do
         timeout -k 10 240 python bench.py --simulate-world $P --dist-mode $M --steps 50 --warmup 5 \
           > gpurun_out/${T}_simrank_${M}_P$P.json 2> gpurun_out/${T}_simrank_${M}_P$P.err || exit $?
