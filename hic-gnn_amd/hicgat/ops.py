@@ -180,11 +180,17 @@ def overlapped_param_grads(enabled=None):
         side_join()
 
 
+# deferred side work of at least this many multiply-adds runs at once on the backward's own stream
+# instead (A/B knob, 0 = off): the first tail block's 512 x 512 dW ahead of the GAT backward, so that
+# after the source gather only lin_l's dW is left
+BIG_MAIN = float(os.environ.get("HICGAT_BIG_MAIN", "0"))
+
+
 def _param_launch(fn, *keep, small=False, work=0):
     """Launch a sink-bound parameter-gradient kernel ``fn()``: now on the current stream when not
     overlapping; queued for ``side_flush`` when deferring (``work``: its size, the issue order);
     else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join)."""
-    if not _SIDE["on"]:
+    if not _SIDE["on"] or (BIG_MAIN > 0 and work >= BIG_MAIN):
         fn()
     elif DEFER_DEFAULT:
         with _SIDE_LOCK:
