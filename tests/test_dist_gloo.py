@@ -147,6 +147,23 @@ def test_three_uneven_ranks_equal_single_rank(tmp_path, mode):
         assert int(held[:, 4].sum()) == int(full[4]) == int(full[0])     # the slabs partition the CSR
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_auto_form_at_four_and_eight_ranks_equals_single_rank(tmp_path, world):
+    """bench.py's default form at the driver's larger world sizes ("auto" = xagg from 4 ranks,
+    hicgat.dist.resolve_mode): 4 and 8 gloo ranks on a 301-node graph equal world 1 of the same
+    form, and the shards still partition the rows, edges, slabs, tiles and support rows."""
+    from hicgat import dist as hdist
+    assert hdist.resolve_mode("auto", world) == "xagg" and hdist.resolve_mode("auto", 2) == "slab"
+    one = _run(1, 301, "combined", tmp_path, mode="xagg")
+    many = _run(world, 301, "combined", tmp_path, mode="auto")
+    _close(one, many)
+    held, full = many["held"], one["held"][0]
+    assert held.shape[0] == world
+    assert int(held[:, 0].sum()) == int(full[0]) and int(held[:, 1].sum()) == 301
+    assert int(held[:, 2].sum()) == 301 and int(held[:, 3].sum()) == int(full[3])
+    assert int(held[:, 4].sum()) == int(full[4]) == int(full[0]) and int(held[:, 5].sum()) == int(full[5])
+
+
 def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
     """The manual backward of ShardedTrainer (CpuKernels, P = 1) vs the oracle model trained by
     autograd + torch Adam with exact distances: same losses, same parameters."""

@@ -201,10 +201,11 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode):
 
 
 @pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "xagg"), (2, "allgather"), (3, "slab"), (3, "xagg"),
-                                        (3, "allgather")])
+                                        (3, "allgather"), (4, "xagg"), (8, "xagg")])
 def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
-    """nnz-balanced shards over gloo on the one GPU, every step form, 2 and 3 (uneven) ranks, against
-    world 1 of the same form."""
+    """nnz-balanced shards over gloo on the one GPU, every step form, 2 and 3 (uneven) ranks, and the
+    form bench.py's "auto" runs at the driver's 4 and 8 ranks (xagg), against world 1 of the same
+    form."""
     n = 777
     one = _run(1, "gloo", n, tmp_path, mode)
     many = _run(world, "gloo", n, tmp_path, mode)
