@@ -32,8 +32,11 @@
 #ifndef HICGAT_XAGG_U
 #define HICGAT_XAGG_U 4   // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
 #endif
+#ifndef HICGAT_XAGG_DXA_LDS
+#define HICGAT_XAGG_DXA_LDS 1   // edge pass: dxa operands read from LDS every pass (0: the compiler keeps them in VGPRs)
+#endif
 #ifndef HICGAT_XAGG_GL
-#define HICGAT_XAGG_GL 16   // edge pass: lanes per edge (8: 16 float4 per lane, 238 VGPRs, 2 waves per SIMD)
+#define HICGAT_XAGG_GL 8   // edge pass: lanes per edge (16 float4 of x_j per lane in flight)
 #endif
 
 namespace hicgat {
@@ -270,9 +273,11 @@ __global__ __launch_bounds__(256) void xagg_rows_bwd_kernel(int rows, const floa
 // dxa (the same address in every group: a broadcast), and the two head dots are summed over the GL
 // lanes (log2 GL xor-shuffle steps), no 64-lane transposed reduction per 4 edges as in the former
 // one-wave-per-row form.  Measured at P = 8 beside the side lanes' dW GEMMs: 111 us (wave per row),
-// 100 (GL = 8, 238 VGPRs), 112 (GL = 16) -- against 64 us for the forward's gather of the same rows
-// alone (profiles/r03h_/r03i_/r03k_simprof_xagg_P8_rank0_timeline.txt): the pass shares the CUs
-// with the GEMMs there, so its time is not its own rate.
+// 100 (GL = 8, dxa kept in 128 VGPRs: 238, 2 waves per SIMD), 112 (GL = 16, 130 VGPRs) -- against
+// 64 us for the forward's gather of the same rows alone (profiles/r03h_/r03i_/r03k_simprof_xagg_P8_
+// rank0_timeline.txt).  dxa re-read from LDS every pass (100 VGPRs, 4 waves per SIMD): rank 0's
+// whole step at P = 2 1.372 ms with GL = 8 against 1.42-1.43 (GL = 16) and 1.448 (GL = 16, dxa in
+// VGPRs); even at P = 8 (profiles/r03p_sim_ab_edge.txt).
 __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ rowptr, const int *__restrict__ col,
                                                         int row_begin, int row_end, const float *__restrict__ x,
                                                         const float *__restrict__ a_src,
@@ -296,6 +301,9 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
   constexpr int GL = HICGAT_XAGG_GL, NG = 64 / GL, NC = 128 / GL;   // lanes per edge, edges per wave, float4s per lane
   const int g = lane / GL, t = lane % GL;
   for (int e0 = beg + NG * wv; e0 < end; e0 += 4 * NG) {   // wave wv: edges e0 .. e0 + NG - 1 of every 4 NG
+#if HICGAT_XAGG_DXA_LDS
+    asm volatile("" ::: "memory");   // re-read dxa from LDS each pass: no 64-128 VGPR copy, more waves
+#endif
     const int e = e0 + g;
     const bool live = e < end;
     const int j = live ? col[e] : i;
