@@ -1,0 +1,206 @@
+// The flagship's MLP tail forward (GATNetSelectiveResidualsUpdated, models.py:637-659, after the
+// GATConv's relu) as ONE kernel: 16 node rows per 4-wave workgroup go through
+//   block 1   Y1 = x [W_a; W_al]^T + [b_a; b_al]          (512 -> 512, fp32 MFMA)
+//             z1 = relu(LN_a(Y1[:, :256])) + Y1[:, 256:]
+//   block 2   Y2 = z1 [W_1; W_1al]^T + [b_1; b_1al]       (256 -> 256)
+//             z2 = relu(LN_1(Y2[:, :128])) + Y2[:, 128:]
+//   block 3   y3 = z2 W_2^T + b_2                          (128 -> 64)
+//             z3 = relu(LN_2(y3))
+//   dense3    coords = z3 W_3^T + b_3                       (64 -> 3)
+// with every intermediate in LDS, instead of 10 launches (4 GEMMs, 3 LayerNorm passes, 3 split-K
+// slab sums on a rank's shard) whose every output makes a round trip through HBM.  The backward
+// still needs Y1, z1, Y2, z2, y3, z3 and the LN statistics (the unfused autograd functions save
+// exactly these), so they are written once on the way.
+//
+// GEMMs: v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).  Lane l supplies
+// A[l & 15][k] and B[k][l & 15]; the four k slots of one instruction are taken as k = 16g + 4(l >> 4)
+// + s for step s of the 16-deep group g, so a lane's four values of a group are ONE float4 -- a
+// ds_read_b128 of the activations (LDS) and a global float4 of the weight row (L2) -- and the next
+// group's weights are loaded before the current group's MFMAs.  C/D: col = l & 15, row = 4(l >> 4)
+// + r.  The k order is fixed (deterministic); it differs from the tiled GEMMs' by fp32 rounding.
+// LayerNorm: one wave per row, the arithmetic of ln_relu_res_fwd_kernel (layernorm.hip) on the row
+// held in LDS (torch.nn.LayerNorm: biased variance, eps 1e-5 inside the square root).
+#include "common.hpp"
+
+namespace hicgat {
+
+constexpr int TR = 16;          // rows per workgroup
+constexpr int XS = 516;         // LDS row stride (floats) of the 512-wide buffers
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// acc[t] (t < NT) += A[16 x K] (LDS, row stride lda) x B^T, B = W rows n0 + 16t + (l & 15), K cols
+template <int NT, int K>
+__device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
+                                          f32x4 (&acc)[NT], int lane) {
+  constexpr int G = K / 16;
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  const float *wrow = W + (size_t)(n0 + li) * K + kq;
+  const float *arow = As + li * lda + kq;
+  float4 b[NT], bn[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) b[t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K);
+  for (int g = 0; g < G; ++g) {
+    if (g + 1 < G) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bn[t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + 1));
+    }
+    const float4 a = *reinterpret_cast<const float4 *>(arow + 16 * g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[t].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[t].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[t].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[t].w, acc[t], 0, 0, 0);
+    }
+    if (g + 1 < G) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[t] = bn[t];
+    }
+  }
+}
+
+// acc + bias -> LDS rows (stride lds) and the global output (rows < M, row stride ldo)
+template <int NT>
+__device__ __forceinline__ void store_tiles(const f32x4 (&acc)[NT], int n0, const float *__restrict__ bias,
+                                            float *__restrict__ Ls, int lds, float *__restrict__ out, int ldo,
+                                            int m0, int M, int lane) {
+  const int li = lane & 15, r0 = 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = n0 + 16 * t + li;
+    const float bb = bias[c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[t][r] + bb;
+      Ls[(r0 + r) * lds + c] = v;
+      if (m0 + r0 + r < M) out[(size_t)(m0 + r0 + r) * ldo + c] = v;
+    }
+  }
+}
+
+// one wave per row: z = relu((y - mean) rstd gamma + beta) (+ y[W + c] when RES), y = the row in LDS
+template <int W, bool RES>
+__device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, const float *__restrict__ gamma,
+                                        const float *__restrict__ beta, float eps, float *__restrict__ Zs, int ldz,
+                                        float *__restrict__ z, float2 *__restrict__ stats, int m0, int M, int wv,
+                                        int lane) {
+  constexpr int V = W / 64;
+  for (int rr = wv; rr < TR; rr += 4) {
+    const float *y = Ys + rr * lds;
+    float v[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = y[q * 64 + lane];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) s += v[q];
+    const float mean = wave_sum(s) / (float)W;
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const float d = v[q] - mean;
+      ss = fmaf(d, d, ss);
+    }
+    const float rstd = 1.0f / sqrt_rn_f32(wave_sum(ss) / (float)W + eps);
+    const bool live = m0 + rr < M;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c = q * 64 + lane;
+      float o = fmaxf(fmaf((v[q] - mean) * rstd, gamma[c], beta[c]), 0.f);
+      if (RES) o += y[W + c];
+      Zs[rr * ldz + c] = o;
+      if (live) z[(size_t)(m0 + rr) * W + c] = o;
+    }
+    if (live && lane == 0) stats[m0 + rr] = make_float2(mean, rstd);
+  }
+}
+
+__global__ __launch_bounds__(256) void tail_fwd_kernel(
+    const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
+    const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
+    const float *__restrict__ b2c, const float *__restrict__ g2, const float *__restrict__ be2,
+    const float *__restrict__ W3, const float *__restrict__ b3, const float *__restrict__ g3,
+    const float *__restrict__ be3, const float *__restrict__ W4, const float *__restrict__ b4, float eps,
+    float *__restrict__ Y1, float2 *__restrict__ st1, float *__restrict__ z1, float *__restrict__ Y2,
+    float2 *__restrict__ st2, float *__restrict__ z2, float *__restrict__ y3, float2 *__restrict__ st3,
+    float *__restrict__ z3, float *__restrict__ coords) {
+  __shared__ __attribute__((aligned(16))) float As[TR * XS];   // x rows, then z1 / z2 / z3 rows
+  __shared__ __attribute__((aligned(16))) float Bs[TR * XS];   // Y1, then Y2 / y3 rows
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int m0 = blockIdx.x * TR;
+  // x rows -> LDS (rows past M: zeros)
+  for (int e = tid; e < TR * 128; e += 256) {
+    const int r = e >> 7, c4 = e & 127;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + (size_t)(m0 + r) * ldx)[c4];
+    *reinterpret_cast<float4 *>(&As[r * XS + 4 * c4]) = v;
+  }
+  __syncthreads();
+  // ---- block 1: 512 -> 512, wave wv: columns 128 wv .. 128 wv + 127 ----
+  {
+    f32x4 acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<8, 512>(As, XS, W1c, 128 * wv, acc, lane);
+    store_tiles<8>(acc, 128 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
+  }
+  __syncthreads();
+  ln_rows<256, true>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
+  __syncthreads();
+  // ---- block 2: 256 -> 256, wave wv: columns 64 wv .. 64 wv + 63 ----
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<4, 256>(As, XS, W2c, 64 * wv, acc, lane);
+    store_tiles<4>(acc, 64 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
+  }
+  __syncthreads();
+  ln_rows<128, true>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
+  __syncthreads();
+  // ---- block 3: 128 -> 64, wave wv: columns 16 wv .. 16 wv + 15 ----
+  {
+    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    mfma_rows<1, 128>(As, XS, W3, 16 * wv, acc, lane);
+    store_tiles<1>(acc, 16 * wv, b3, Bs, XS, y3, 64, m0, M, lane);
+  }
+  __syncthreads();
+  ln_rows<64, false>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
+  __syncthreads();
+  // ---- dense3: 64 -> 3, thread t < 48: row t / 3, output t % 3 (fp32 fma chain over k) ----
+  if (tid < TR * 3) {
+    const int r = tid / 3, j = tid % 3;
+    if (m0 + r < M) {
+      const float *zr = As + r * XS;
+      const float *w = W4 + j * 64;
+      float s = 0.f;
+#pragma unroll 16
+      for (int k = 0; k < 64; ++k) s = fmaf(zr[k], w[k], s);
+      coords[(size_t)(m0 + r) * 3 + j] = s + b4[j];
+    }
+  }
+}
+
+}  // namespace hicgat
+
+using namespace hicgat;
+
+extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c,
+                                     const float *g1, const float *be1, const float *W2c, const float *b2c,
+                                     const float *g2, const float *be2, const float *W3, const float *b3,
+                                     const float *g3, const float *be3, const float *W4, const float *b4, float eps,
+                                     float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2, float *y3,
+                                     float *st3, float *z3, float *coords, hicgat_stream_t stream) {
+  if (M < 0 || ldx < 512 || (ldx & 3)) return HICGAT_EINVAL;
+  if (M == 0) return HICGAT_OK;
+  const void *ps[] = {x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4,
+                      Y1, st1, z1, Y2, st2, z2, y3, st3, z3, coords};
+  for (const void *p : ps)
+    if (!p) return HICGAT_EINVAL;
+  // float4 rows: x, the weight rows and the LDS images need 16-B alignment
+  if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3) & 15) return HICGAT_EUNSUPPORTED;
+  hipLaunchKernelGGL(tail_fwd_kernel, dim3((M + TR - 1) / TR), dim3(256), 0, (hipStream_t)stream, x, ldx, M, W1c, b1c,
+                     g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1,
+                     Y2, reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

@@ -67,7 +67,10 @@ class GATNetSelectiveResidualsUpdated(_CoordsModel):
     def post_act(self, x):
         """models.py:638-659 (after the relu): each residual block relu(norm(dense(x))) +
         align_dense(x) as one fused op (one GEMM over [W; W_align], one row pass);
-        relu(norm2(dense2(.))); dense3."""
+        relu(norm2(dense2(.))); dense3.  On graphs of >= ops.FUSED_TAIL_MIN_M rows the whole forward
+        is one kernel (ops.fused_tail, tail_fused.hip) with the same backward."""
+        if ops.fused_tail_ok(self, x):
+            return ops.fused_tail(self, x)
         x = ops.dual_ln_relu_res(x, self.densea, self.align_densea, self.norm_a)
         x = ops.dual_ln_relu_res(x, self.dense1, self.align_dense1, self.norm1)
         x = ops.ln_relu_res(_lin(self.dense2, x), self.norm2)

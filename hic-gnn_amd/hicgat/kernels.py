@@ -405,6 +405,25 @@ class HipKernels:
                                                    P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
                                                    _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
 
+    def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps):
+        """The flagship's MLP tail forward in one launch (tail_fused.hip): returns (coords, saved)
+        with saved = (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)."""
+        M = x.shape[0]
+        dev = x.device
+        f = dict(dtype=torch.float32, device=dev)
+        Y1, z1 = torch.empty((M, 512), **f), torch.empty((M, 256), **f)
+        Y2, z2 = torch.empty((M, 256), **f), torch.empty((M, 128), **f)
+        y3, z3 = torch.empty((M, 64), **f), torch.empty((M, 64), **f)
+        st1, st2, st3 = (torch.empty((M, 2), **f) for _ in range(3))
+        coords = torch.empty((M, 3), **f)
+        ws = [W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4]
+        assert all(t.is_contiguous() for t in ws) and x.stride(1) == 1
+        with _timed("tail_fwd_fused"):
+            _lib.check(self.lib.hicgat_tail_fwd_fused(P(x), x.stride(0), M, *[P(t) for t in ws], float(eps), P(Y1), P(st1),
+                                                      P(z1), P(Y2), P(st2), P(z2), P(y3), P(st3), P(z3), P(coords),
+                                                      _lib.stream(dev)), "hicgat_tail_fwd_fused")
+        return coords, (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)
+
     def ln_workspace(self, W, device):
         return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)
 

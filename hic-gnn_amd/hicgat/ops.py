@@ -646,6 +646,77 @@ def dual_ln_relu_res(x, lin1, lin2, norm):
                                   norm.eps)
 
 
+# The flagship's MLP tail forward as ONE launch (tail_fused.hip) for row counts in [MIN_M, MAX_M]
+# (HICGAT_FUSED_TAIL=0: off).  Measured (profiles/r03q_ab_fused_tail.txt): a rank's shard at P = 8
+# (2 700 rows) 0.629 vs 0.644 ms per rank step, P = 4 (5 000) 0.877 vs 0.896, synth-2000 0.662 vs
+# 0.668 ms per step; slower above: P = 2 (10 000 rows) 1.39 vs 1.37 and the single-GPU N = 20000
+# step 1.987 vs 1.915 ms -- its 16-row workgroups stream the 1.3 MB of tail weights from L2 once per
+# 16 rows (1.6 GB at N = 20000), where the tiled GEMMs reuse each weight tile over 160 rows.
+# Graphs below MIN_M (chr19: 58 / 114 loci) keep the per-layer kernels.
+FUSED_TAIL = os.environ.get("HICGAT_FUSED_TAIL", "1") != "0"
+FUSED_TAIL_MIN_M = int(os.environ.get("HICGAT_FUSED_TAIL_MIN_M", "1024"))
+FUSED_TAIL_MAX_M = int(os.environ.get("HICGAT_FUSED_TAIL_MAX_M", "6144"))
+
+
+class _FusedTailFn(torch.autograd.Function):
+    """models.py:638-659 after the relu (GATNetSelectiveResidualsUpdated.post_act): the forward in
+    one kernel (hicgat_tail_fwd_fused), which writes the tensors the per-layer autograd functions
+    would save; the backward runs those functions' own backward steps on them, in autograd's order
+    (dense3, norm2, dense2, block 2, block 1), so its kernels, side-stream parameter gradients and
+    sums are the per-layer path's."""
+
+    @staticmethod
+    def forward(ctx, x, Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3, eps):
+        K = kernels.default()
+        x = x.contiguous()
+        W1c, b1c = _joined(Wa, Wal).contiguous(), _joined(ba, bal).contiguous()
+        W2c, b2c = _joined(W1, W1al).contiguous(), _joined(b1, b1al).contiguous()
+        coords, saved = K.tail_fwd_fused(x, W1c, b1c, ga.contiguous(), bea.contiguous(), W2c, b2c, g1.contiguous(),
+                                         be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
+                                         be2.contiguous(), W3.contiguous(), b3.contiguous(), eps)
+        ctx.save_for_backward(x, *saved)
+        ctx.params = (Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3)
+        return coords
+
+    @staticmethod
+    def backward(ctx, dcoords):
+        import types
+        x, Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = ctx.saved_tensors
+        Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3 = ctx.params
+        T = (True,) * 8
+
+        def c(**kw):
+            return types.SimpleNamespace(needs_input_grad=T, **kw)
+
+        dz3, dW3, db3 = _LinearFn.backward(c(saved_tensors=(z3, W3), params=(W3, b3), has_bias=True), dcoords)
+        dy3, dg2, dbe2, _, _ = _LnReluResFn.backward(c(saved_tensors=(y3, st3, g2, be2), params=(g2, be2),
+                                                       has_res=False), dz3)
+        dz2, dW2, db2 = _LinearFn.backward(c(saved_tensors=(z2, W2), params=(W2, b2), has_bias=True), dy3)
+        dz1, dW1, db1, dW1al, db1al, dg1, dbe1, _ = _DualLnReluResFn.backward(
+            c(saved_tensors=(z1, Y2, st2, g1, be1), params=(W1, b1, W1al, b1al, g1, be1)), dz2)
+        ctx1 = types.SimpleNamespace(needs_input_grad=(ctx.needs_input_grad[0],) + T[1:],
+                                     saved_tensors=(x, Y1, st1, ga, bea), params=(Wa, ba, Wal, bal, ga, bea))
+        dx, dWa, dba, dWal, dbal, dga, dbea, _ = _DualLnReluResFn.backward(ctx1, dz1)
+        return (dx, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al, dg1, dbe1, dW2, db2, dg2, dbe2,
+                dW3, db3, None)
+
+
+def fused_tail_ok(model, x):
+    return (FUSED_TAIL and x.is_cuda and x.dim() == 2 and FUSED_TAIL_MIN_M <= x.shape[0] <= FUSED_TAIL_MAX_M
+            and x.shape[1] == 512
+            and x.dtype == torch.float32 and x.stride(1) == 1
+            and model.norm_a.eps == model.norm1.eps == model.norm2.eps)
+
+
+def fused_tail(model, x):
+    """GATNetSelectiveResidualsUpdated.post_act on the fused forward (``fused_tail_ok`` first)."""
+    m = model
+    return _FusedTailFn.apply(x, m.densea.weight, m.densea.bias, m.align_densea.weight, m.align_densea.bias,
+                              m.norm_a.weight, m.norm_a.bias, m.dense1.weight, m.dense1.bias, m.align_dense1.weight,
+                              m.align_dense1.bias, m.norm1.weight, m.norm1.bias, m.dense2.weight, m.dense2.bias,
+                              m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps)
+
+
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):
     """GATConv forward; ``act="relu"`` returns relu(GATConv(x)) with the relu fused."""
     if adj.rowptr32 is None or adj.rowptr32.device != x.device:

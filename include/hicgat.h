@@ -362,6 +362,20 @@ size_t hicgat_ln_relu_res_workspace_bytes(int W);
 int hicgat_ln_relu_res_bwd_params(int W, float *dgamma, float *dbeta, int accumulate, void *workspace,
                                   size_t workspace_bytes, hicgat_stream_t stream);
 
+/* ---- The flagship's MLP tail forward in one launch (tail_fused.hip; replaces the dual-Linear GEMMs,
+ * ln_relu_res passes and Linear GEMMs of models.py:637-659 for GATNetSelectiveResidualsUpdated) ----
+ * x [M][512] (ld ldx, 16-B aligned rows): the GATConv output after its relu.  W1c [512][512] = [W_densea;
+ * W_align_densea], b1c [512]; g1/be1 [256] = norm_a; W2c [256][256] = [W_dense1; W_align_dense1], b2c
+ * [256]; g2/be2 [128] = norm1; W3 [64][128] / b3 = dense2; g3/be3 [64] = norm2; W4 [3][64] / b4 = dense3.
+ * Writes what the backward reads: Y1 [M][512] (block-1 GEMM + bias), st1 [M][2] (mean, rstd), z1
+ * [M][256], Y2 [M][256], st2, z2 [M][128], y3 [M][64], st3, z3 [M][64], and coords [M][3].
+ * 16 rows per workgroup, fp32 MFMA (16x16x4), LayerNorm eps inside the square root. */
+int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c, const float *g1,
+                          const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2,
+                          const float *W3, const float *b3, const float *g3, const float *be3, const float *W4,
+                          const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2, float *st2,
+                          float *z2, float *y3, float *st3, float *z3, float *coords, hicgat_stream_t stream);
+
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --
  * the networkx weight utils.load_input assigns (utils.py:37-52): A[max(i,j), min(i,j)] when

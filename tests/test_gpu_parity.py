@@ -1360,3 +1360,72 @@ def test_gatconv_tiny_graphs_match_oracle(n):
     assert _rel(xm.grad.cpu(), xr.grad) < 1e-4
     for (name, pr), (_, pm) in zip(ref.named_parameters(), mine.named_parameters()):
         assert _rel(pm.grad.cpu(), pr.grad) < 1e-4 or pr.grad.abs().max() < 1e-30, name
+
+
+# ---------------------------------------------------------------- a6: the fused MLP-tail forward
+@pytest.mark.parametrize("m,sinks", [(2701, False), (2701, True), (20000, True), (1030, False)])
+def test_fused_tail_matches_per_layer_path(monkeypatch, m, sinks):
+    """GATNetSelectiveResidualsUpdated.post_act through the one-launch forward (tail_fused.hip) vs the
+    per-layer kernels: coords, the input gradient and every tail parameter's gradient (into FlatAdam's
+    gradient sinks, or autograd's .grad), and an fp64 torch evaluation of the forward.  Tolerances:
+    coords 1e-5 of their max (fp32 GEMM order), gradients 1e-4 of each tensor's max."""
+    import hicgat
+    from hicgat import ops
+    torch.manual_seed(7)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    with torch.no_grad():      # trained-looking LayerNorm affine parameters (beta != 0 moves the kinks)
+        for nm in ("norm_a", "norm1", "norm2"):
+            getattr(model, nm).weight.add_(0.1 * torch.randn_like(getattr(model, nm).weight))
+            getattr(model, nm).bias.add_(0.1 * torch.randn_like(getattr(model, nm).bias))
+    x0 = torch.relu(torch.randn(m, 512, device=DEV))
+    g = torch.randn(m, 3, device=DEV)
+    # the tail is row-wise: rows holding a relu input within 1e-5 of the kink (where the two fp32 GEMM
+    # orders may take different sides, tests/test_gpu_dist.py XAGG_NS) get no upstream gradient, so
+    # neither path's backward sees them
+    d = torch.float64
+
+    def lin(layer, v):
+        return v @ layer.weight.detach().to(d).t() + layer.bias.detach().to(d)
+
+    def ln(norm, v):
+        return torch.nn.functional.layer_norm(v, v.shape[1:], norm.weight.detach().to(d), norm.bias.detach().to(d),
+                                              norm.eps)
+
+    with torch.no_grad():
+        v = x0.to(d)
+        p1 = ln(model.norm_a, lin(model.densea, v))
+        v = torch.relu(p1) + lin(model.align_densea, v)
+        p2 = ln(model.norm1, lin(model.dense1, v))
+        v = torch.relu(p2) + lin(model.align_dense1, v)
+        p3 = ln(model.norm2, lin(model.dense2, v))
+        ref = lin(model.dense3, torch.relu(p3))
+        kink = torch.cat([p1, p2, p3], 1).abs().amin(1) < 1e-5
+    g[kink] = 0.0
+    assert kink.float().mean().item() < 0.02
+    tail = [p for n, p in model.named_parameters() if not n.startswith("conv.")]
+    res = {}
+    monkeypatch.setattr(ops, "FUSED_TAIL_MAX_M", max(m, ops.FUSED_TAIL_MAX_M))   # the kernel at N = 20000 too
+    for fused in (False, True):
+        monkeypatch.setattr(ops, "FUSED_TAIL", fused)
+        assert ops.fused_tail_ok(model, x0) == fused
+        opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3) if sinks else None
+        if opt is not None:
+            opt.zero_grad()
+        else:
+            for p in model.parameters():
+                p.grad = None
+        x = x0.clone().requires_grad_(True)
+        with ops.overlapped_param_grads(sinks):
+            c = model.post_act(x)
+            c.backward(g)
+        torch.cuda.synchronize()
+        res[fused] = (c.detach().clone(), x.grad.clone(), [p.grad.detach().clone() for p in tail])
+    (c0, dx0, gp0), (c1, dx1, gp1) = res[False], res[True]
+    assert _rel(c1.cpu(), c0.cpu()) < 1e-5
+    assert (dx1 - dx0).abs().max().item() <= 1e-4 * dx0.abs().max().item()
+    names = [n for n, _ in model.named_parameters() if not n.startswith("conv.")]
+    for nm, a, b in zip(names, gp0, gp1):
+        if nm == "dense3.bias":
+            continue      # exactly 0 up to rounding when the upstream gradient sums to ~0
+        assert (b - a).abs().max().item() <= 1e-4 * a.abs().max().item(), nm
+    assert _rel(c1.double().cpu(), ref.cpu()) < 1e-5      # the fp64 forward of models.py:638-659

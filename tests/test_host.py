@@ -29,6 +29,29 @@ def test_library_exports_every_header_symbol():
     assert b"unsupported" in lib.hicgat_strerror(-3)
 
 
+def _header_arity():
+    """{symbol: number of parameters} of every prototype in include/hicgat.h (comments stripped)."""
+    with open(os.path.join(ROOT, "include", "hicgat.h")) as fh:
+        text = re.sub(r"/\*.*?\*/", "", fh.read(), flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    out = {}
+    for m in re.finditer(r"\b(hicgat_\w+)\s*\(([^;{]*?)\)\s*;", text, re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes signature has as many arguments as the header's prototype (a miscounted
+    signature fails only at call time, on a GPU)."""
+    from hicgat import _lib
+    arity = _header_arity()
+    assert len(arity) >= 20
+    for name, (_, args) in _lib.SIGNATURES.items():
+        assert name in arity, name
+        assert len(args) == arity[name], (name, len(args), arity[name])
+
+
 def test_query_functions_need_no_gpu():
     from hicgat import _lib
     lib = _lib.load()
