@@ -15,8 +15,8 @@
 // GEMMs: v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).  Lane l supplies
 // A[l & 15][k] and B[k][l & 15]; the four k slots of one instruction are taken as k = 16g + 4(l >> 4)
 // + s for step s of the 16-deep group g, so a lane's four values of a group are ONE float4 -- a
-// ds_read_b128 of the activations (LDS) and a global float4 of the weight row (L2) -- and the next
-// group's weights are loaded before the current group's MFMAs.  C/D: col = l & 15, row = 4(l >> 4)
+// ds_read_b128 of the activations (LDS) and a global float4 of the weight row (L2) -- and the
+// weights of group g + 4 are loaded right after group g's MFMAs.  C/D: col = l & 15, row = 4(l >> 4)
 // + r.  The k order is fixed (deterministic); it differs from the tiled GEMMs' by fp32 rounding.
 // LayerNorm: one wave per row, the arithmetic of ln_relu_res_fwd_kernel (layernorm.hip) on the row
 // held in LDS (torch.nn.LayerNorm: biased variance, eps 1e-5 inside the square root).
@@ -24,44 +24,52 @@
 
 namespace hicgat {
 
-constexpr int TR = 16;          // rows per workgroup
 constexpr int XS = 516;         // LDS row stride (floats) of the 512-wide buffers
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// acc[t] (t < NT) += A[16 x K] (LDS, row stride lda) x B^T, B = W rows n0 + 16t + (l & 15), K cols
-template <int NT, int K>
+// acc[h][t] (h < RB/16 row halves, t < NT) += A[RB x K] (LDS, row stride lda) x B^T, B = the weight
+// rows n0 + 16t + (l & 15) (K columns).  The weights of group g + 4 are loaded right after group g's
+// MFMAs, so three groups of MFMAs cover every load (a ring of 4 float4 sets).
+template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
-                                          f32x4 (&acc)[NT], int lane) {
-  constexpr int G = K / 16;
+                                          f32x4 (&acc)[RB / 16][NT], int lane) {
+  constexpr int G = K / 16, H = RB / 16;
+  static_assert(G % 4 == 0, "K: a multiple of 64");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
   const float *arow = As + li * lda + kq;
-  float4 b[NT], bn[NT];
+  float4 b[4][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) b[t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K);
-  for (int g = 0; g < G; ++g) {
-    if (g + 1 < G) {
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) bn[t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + 1));
-    }
-    const float4 a = *reinterpret_cast<const float4 *>(arow + 16 * g);
+    for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * q);
+  for (int g0 = 0; g0 < G; g0 += 4) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[t].x, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[t].y, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[t].z, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[t].w, acc[t], 0, 0, 0);
-    }
-    if (g + 1 < G) {
+    for (int q = 0; q < 4; ++q) {
+      const int g = g0 + q;
+      float4 a[H];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b[t] = bn[t];
+      for (int h = 0; h < H; ++h) a[h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].x, b[q][t].x, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].y, b[q][t].y, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t].z, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t].w, acc[h][t], 0, 0, 0);
+        }
+      if (g + 4 < G) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + 4));
+      }
     }
   }
 }
 
 // acc + bias -> LDS rows (stride lds) and the global output (rows < M, row stride ldo)
-template <int NT>
-__device__ __forceinline__ void store_tiles(const f32x4 (&acc)[NT], int n0, const float *__restrict__ bias,
+template <int RB, int NT>
+__device__ __forceinline__ void store_tiles(const f32x4 (&acc)[RB / 16][NT], int n0, const float *__restrict__ bias,
                                             float *__restrict__ Ls, int lds, float *__restrict__ out, int ldo,
                                             int m0, int M, int lane) {
   const int li = lane & 15, r0 = 4 * (lane >> 4);
@@ -70,22 +78,25 @@ __device__ __forceinline__ void store_tiles(const f32x4 (&acc)[NT], int n0, cons
     const int c = n0 + 16 * t + li;
     const float bb = bias[c];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = acc[t][r] + bb;
-      Ls[(r0 + r) * lds + c] = v;
-      if (m0 + r0 + r < M) out[(size_t)(m0 + r0 + r) * ldo + c] = v;
-    }
+    for (int h = 0; h < RB / 16; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * h + r0 + r;
+        const float v = acc[h][t][r] + bb;
+        Ls[row * lds + c] = v;
+        if (m0 + row < M) out[(size_t)(m0 + row) * ldo + c] = v;
+      }
   }
 }
 
 // one wave per row: z = relu((y - mean) rstd gamma + beta) (+ y[W + c] when RES), y = the row in LDS
-template <int W, bool RES>
+template <int RB, int W, bool RES>
 __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, const float *__restrict__ gamma,
                                         const float *__restrict__ beta, float eps, float *__restrict__ Zs, int ldz,
                                         float *__restrict__ z, float2 *__restrict__ stats, int m0, int M, int wv,
                                         int lane) {
   constexpr int V = W / 64;
-  for (int rr = wv; rr < TR; rr += 4) {
+  for (int rr = wv; rr < RB; rr += 4) {
     const float *y = Ys + rr * lds;
     float v[V];
 #pragma unroll
@@ -114,6 +125,8 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
   }
 }
 
+// RB rows per workgroup (the launch uses 16).
+template <int RB>
 __global__ __launch_bounds__(256) void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
@@ -123,12 +136,14 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
     float *__restrict__ Y1, float2 *__restrict__ st1, float *__restrict__ z1, float *__restrict__ Y2,
     float2 *__restrict__ st2, float *__restrict__ z2, float *__restrict__ y3, float2 *__restrict__ st3,
     float *__restrict__ z3, float *__restrict__ coords) {
-  __shared__ __attribute__((aligned(16))) float As[TR * XS];   // x rows, then z1 / z2 / z3 rows
-  __shared__ __attribute__((aligned(16))) float Bs[TR * XS];   // Y1, then Y2 / y3 rows
+  extern __shared__ __attribute__((aligned(16))) float lds_tail[];
+  float *As = lds_tail;              // x rows, then z1 / z2 / z3 rows
+  float *Bs = lds_tail + RB * XS;    // Y1, then Y2 / y3 rows
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * TR;
+  const int m0 = blockIdx.x * RB;
+  constexpr int H = RB / 16;
   // x rows -> LDS (rows past M: zeros)
-  for (int e = tid; e < TR * 128; e += 256) {
+  for (int e = tid; e < RB * 128; e += 256) {
     const int r = e >> 7, c4 = e & 127;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + (size_t)(m0 + r) * ldx)[c4];
@@ -137,37 +152,43 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   __syncthreads();
   // ---- block 1: 512 -> 512, wave wv: columns 128 wv .. 128 wv + 127 ----
   {
-    f32x4 acc[8];
+    f32x4 acc[H][8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<8, 512>(As, XS, W1c, 128 * wv, acc, lane);
-    store_tiles<8>(acc, 128 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, 8, 512>(As, XS, W1c, 128 * wv, acc, lane);
+    store_tiles<RB, 8>(acc, 128 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<256, true>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
+  ln_rows<RB, 256, true>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
   __syncthreads();
   // ---- block 2: 256 -> 256, wave wv: columns 64 wv .. 64 wv + 63 ----
   {
-    f32x4 acc[4];
+    f32x4 acc[H][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<4, 256>(As, XS, W2c, 64 * wv, acc, lane);
-    store_tiles<4>(acc, 64 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, 4, 256>(As, XS, W2c, 64 * wv, acc, lane);
+    store_tiles<RB, 4>(acc, 64 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<128, true>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
+  ln_rows<RB, 128, true>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
   __syncthreads();
   // ---- block 3: 128 -> 64, wave wv: columns 16 wv .. 16 wv + 15 ----
   {
-    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
-    mfma_rows<1, 128>(As, XS, W3, 16 * wv, acc, lane);
-    store_tiles<1>(acc, 16 * wv, b3, Bs, XS, y3, 64, m0, M, lane);
+    f32x4 acc[H][1];
+#pragma unroll
+    for (int h = 0; h < H; ++h) acc[h][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, 1, 128>(As, XS, W3, 16 * wv, acc, lane);
+    store_tiles<RB, 1>(acc, 16 * wv, b3, Bs, XS, y3, 64, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<64, false>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
+  ln_rows<RB, 64, false>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
   __syncthreads();
-  // ---- dense3: 64 -> 3, thread t < 48: row t / 3, output t % 3 (fp32 fma chain over k) ----
-  if (tid < TR * 3) {
+  // ---- dense3: 64 -> 3, thread t < 3 RB: row t / 3, output t % 3 (fp32 fma chain over k) ----
+  if (tid < RB * 3) {
     const int r = tid / 3, j = tid % 3;
     if (m0 + r < M) {
       const float *zr = As + r * XS;
@@ -198,9 +219,19 @@ extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const f
     if (!p) return HICGAT_EINVAL;
   // float4 rows: x, the weight rows and the LDS images need 16-B alignment
   if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3) & 15) return HICGAT_EUNSUPPORTED;
-  hipLaunchKernelGGL(tail_fwd_kernel, dim3((M + TR - 1) / TR), dim3(256), 0, (hipStream_t)stream, x, ldx, M, W1c, b1c,
-                     g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1,
-                     Y2, reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords);
+  // 16 rows per workgroup (66 KiB of dynamic LDS: two workgroups per CU).  A 32-row form (132 KiB,
+  // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
+  // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
+  // with one workgroup per CU every phase's latency is exposed.
+  constexpr int RB = 16;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
+  if (!attr) return HICGAT_ELAUNCH;
+  hipLaunchKernelGGL(tail_fwd_kernel<RB>, dim3((M + RB - 1) / RB), dim3(256), (size_t)2 * RB * XS * sizeof(float),
+                     (hipStream_t)stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps,
+                     Y1, reinterpret_cast<float2 *>(st1), z1, Y2, reinterpret_cast<float2 *>(st2), z2, y3,
+                     reinterpret_cast<float2 *>(st3), z3, coords);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -647,11 +647,12 @@ def dual_ln_relu_res(x, lin1, lin2, norm):
 
 
 # The flagship's MLP tail forward as ONE launch (tail_fused.hip) for row counts in [MIN_M, MAX_M]
-# (HICGAT_FUSED_TAIL=0: off).  Measured (profiles/r03q_ab_fused_tail.txt): a rank's shard at P = 8
-# (2 700 rows) 0.629 vs 0.644 ms per rank step, P = 4 (5 000) 0.877 vs 0.896, synth-2000 0.662 vs
-# 0.668 ms per step; slower above: P = 2 (10 000 rows) 1.39 vs 1.37 and the single-GPU N = 20000
-# step 1.987 vs 1.915 ms -- its 16-row workgroups stream the 1.3 MB of tail weights from L2 once per
-# 16 rows (1.6 GB at N = 20000), where the tiled GEMMs reuse each weight tile over 160 rows.
+# (HICGAT_FUSED_TAIL=0: off).  Measured (profiles/r03r_ab_fused_tail.txt, 4-deep weight prefetch):
+# a rank's shard at P = 8 (2 700 rows) 0.613 vs 0.650 ms per rank step, P = 4 (5 000) 0.877 vs
+# 0.896, synth-2000 0.641 vs 0.664 ms per step; slower on big graphs: the single-GPU N = 20000 step
+# 1.977 vs 1.913 ms (r03q: P = 2, 10 000 rows, 1.39 vs 1.37) -- 16-row workgroups stream the 1.3 MB
+# of tail weights from L2 once per 16 rows (1.6 GB at N = 20000) where the tiled GEMMs reuse each
+# weight tile over 160 rows, and a 32-row form (one workgroup per CU) exposed every phase's latency.
 # Graphs below MIN_M (chr19: 58 / 114 loci) keep the per-layer kernels.
 FUSED_TAIL = os.environ.get("HICGAT_FUSED_TAIL", "1") != "0"
 FUSED_TAIL_MIN_M = int(os.environ.get("HICGAT_FUSED_TAIL_MIN_M", "1024"))
