@@ -22,6 +22,8 @@
 // held in LDS (torch.nn.LayerNorm: biased variance, eps 1e-5 inside the square root).
 #include "common.hpp"
 
+extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W);   // layernorm.hip
+
 namespace hicgat {
 
 constexpr int XS = 516;         // LDS row stride (floats) of the 512-wide buffers
@@ -201,6 +203,200 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   }
 }
 
+// ---- the tail's backward (the input-gradient chain) in one kernel ----------------------------------
+// acc[h][t] += A[RB x K] (LDS) x B, B[k][n] = W[k][n] (W [K][ldw] row-major: dx = dy W): lane l reads
+// W[16g + 4(l >> 4) + s][n0 + 16t + (l & 15)] -- 16 consecutive floats per k across the lanes -- with
+// the weights of group g + 4 loaded after group g's MFMAs (ring of 4).
+template <int RB, int NT, int K>
+__device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int lda, const float *__restrict__ W, int ldw,
+                                            int n0, f32x4 (&acc)[RB / 16][NT], int lane) {
+  constexpr int G = K / 16, H = RB / 16;
+  static_assert(G % 4 == 0, "K: a multiple of 64");
+  const int li = lane & 15, kq = 4 * (lane >> 4);
+  const float *wcol = W + (size_t)kq * ldw + n0 + li;
+  const float *arow = As + li * lda + kq;
+  float b[4][NT][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * q + j) * ldw + 16 * t];
+  for (int g0 = 0; g0 < G; g0 += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int g = g0 + q;
+      float4 a[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) a[h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].x, b[q][t][0], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].y, b[q][t][1], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t][2], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t][3], acc[h][t], 0, 0, 0);
+        }
+      if (g + 4 < G) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * (g + 4) + j) * ldw + 16 * t];
+      }
+    }
+  }
+}
+
+// acc -> LDS rows (no bias), and optionally the global output
+template <int RB, int NT>
+__device__ __forceinline__ void put_tiles(const f32x4 (&acc)[RB / 16][NT], int n0, float *__restrict__ Ls, int lds,
+                                          float *__restrict__ out, int ldo, int m0, int M, int lane) {
+  const int li = lane & 15, r0 = 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c = n0 + 16 * t + li;
+#pragma unroll
+    for (int h = 0; h < RB / 16; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * h + r0 + r;
+        if (Ls) Ls[row * lds + c] = acc[h][t][r];
+        if (out && m0 + row < M) out[(size_t)(m0 + row) * ldo + c] = acc[h][t][r];
+      }
+  }
+}
+
+// LayerNorm + ReLU (+ residual) backward of rows wv, wv + 4, ... (ln_relu_res_bwd_kernel's
+// arithmetic): dz from LDS (Dz, stride ldd), y / stats from global; dy (and dres = dz beside it when
+// RES) into LDS (Gs, stride lds: [dy | dres]) and the global dY rows ([M][W or 2W]); the wave's
+// dgamma / dbeta partials into its slot of part ([slots][2][W], hicgat_ln_relu_res_bwd_params).
+template <int RB, int W, bool RES>
+__device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ldd, const float *__restrict__ y,
+                                            int64_t ldy, const float2 *__restrict__ stats,
+                                            const float *__restrict__ gamma, const float *__restrict__ beta,
+                                            float *__restrict__ Gs, int lds, float *__restrict__ dY,
+                                            float *__restrict__ part, int slot, int m0, int M, int wv, int lane) {
+  constexpr int V = W / 64, LDY = RES ? 2 * W : W;
+  float g_[V], b_[V], pg[V], pb[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) {
+    g_[q] = gamma[q * 64 + lane];
+    b_[q] = beta[q * 64 + lane];
+    pg[q] = pb[q] = 0.f;
+  }
+  for (int rr = wv; rr < RB; rr += 4) {
+    const int row = m0 + rr;
+    const bool live = row < M;
+    const float2 st = live ? stats[row] : make_float2(0.f, 0.f);
+    float yh[V], dh[V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c = q * 64 + lane;
+      yh[q] = live ? (y[(size_t)row * ldy + c] - st.x) * st.y : 0.f;
+      const float pre = fmaf(yh[q], g_[q], b_[q]);
+      const float dzv = live ? Dz[rr * ldd + c] : 0.f;
+      if (RES) {
+        Gs[rr * lds + W + c] = dzv;
+        if (live) dY[(size_t)row * LDY + W + c] = dzv;
+      }
+      const float g = pre > 0.f ? dzv : 0.f;
+      pg[q] = fmaf(g, yh[q], pg[q]);
+      pb[q] += g;
+      dh[q] = g * g_[q];
+      s1 += dh[q];
+      s2 = fmaf(dh[q], yh[q], s2);
+    }
+    const float m1 = wave_sum(s1) / (float)W, m2 = wave_sum(s2) / (float)W;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const float v = st.y * (dh[q] - m1 - yh[q] * m2);
+      Gs[rr * lds + q * 64 + lane] = v;
+      if (live) dY[(size_t)row * LDY + q * 64 + lane] = v;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < V; ++q) {
+    part[((size_t)slot * 2 + 0) * W + q * 64 + lane] = pg[q];
+    part[((size_t)slot * 2 + 1) * W + q * 64 + lane] = pb[q];
+  }
+}
+
+constexpr int kTailBwdSlots = 4096;   // = kLnWaves (layernorm.hip): the partial slots of each LN workspace
+
+template <int RB>
+__global__ __launch_bounds__(256) void tail_bwd_kernel(
+    const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
+    const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
+    const float2 *__restrict__ st3, const float *__restrict__ W4, const float *__restrict__ W3,
+    const float *__restrict__ W2c, const float *__restrict__ W1c, const float *__restrict__ g1,
+    const float *__restrict__ be1, const float *__restrict__ g2, const float *__restrict__ be2,
+    const float *__restrict__ g3, const float *__restrict__ be3, float *__restrict__ dx, float *__restrict__ dY1,
+    float *__restrict__ dY2, float *__restrict__ dy3, float *__restrict__ p1, float *__restrict__ p2,
+    float *__restrict__ p3) {
+  extern __shared__ __attribute__((aligned(16))) float lds_tail[];
+  float *As = lds_tail;              // dz3, dz2, dz1 rows
+  float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int slot = blockIdx.x * 4 + wv;
+  const int m0 = blockIdx.x * RB;
+  constexpr int H = RB / 16;
+  if (m0 >= M) {   // the grid covers every partial slot: the waves past the rows write zeros
+    for (int c = lane; c < 2 * 256; c += 64) p1[(size_t)slot * 512 + c] = 0.f;
+    for (int c = lane; c < 2 * 128; c += 64) p2[(size_t)slot * 256 + c] = 0.f;
+    for (int c = lane; c < 2 * 64; c += 64) p3[(size_t)slot * 128 + c] = 0.f;
+    return;
+  }
+  // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
+  for (int e = tid; e < RB * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    float s = 0.f;
+    if (m0 + r < M) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) s = fmaf(dc[(size_t)(m0 + r) * 3 + j], W4[j * 64 + c], s);
+    }
+    As[r * XS + c] = s;
+  }
+  __syncthreads();
+  ln_bwd_rows<RB, 64, false>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, m0, M, wv, lane);
+  __syncthreads();
+  // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 32 wv ..
+  {
+    f32x4 acc[H][2];
+#pragma unroll
+    for (int h = 0; h < H; ++h) acc[h][0] = acc[h][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, 2, 64>(Bs, XS, W3, 128, 32 * wv, acc, lane);
+    put_tiles<RB, 2>(acc, 32 * wv, As, XS, nullptr, 0, m0, M, lane);
+  }
+  __syncthreads();
+  ln_bwd_rows<RB, 128, true>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, m0, M, wv, lane);
+  __syncthreads();
+  // block 2 backward: dz1 = [dy2 | dres2] [W_1; W_1al] ([RB x 256] [256 x 256]), wave wv: columns 64 wv ..
+  {
+    f32x4 acc[H][4];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, 4, 256>(Bs, XS, W2c, 256, 64 * wv, acc, lane);
+    put_tiles<RB, 4>(acc, 64 * wv, As, XS, nullptr, 0, m0, M, lane);
+  }
+  __syncthreads();
+  ln_bwd_rows<RB, 256, true>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, m0, M, wv, lane);
+  __syncthreads();
+  // block 1 backward: dx = [dy1 | dres1] [W_a; W_al] ([RB x 512] [512 x 512]), wave wv: columns 128 wv ..
+  {
+    f32x4 acc[H][8];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, 8, 512>(Bs, XS, W1c, 512, 128 * wv, acc, lane);
+    put_tiles<RB, 8>(acc, 128 * wv, nullptr, 0, dx, 512, m0, M, lane);
+  }
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -232,6 +428,38 @@ extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const f
                      (hipStream_t)stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps,
                      Y1, reinterpret_cast<float2 *>(st1), z1, Y2, reinterpret_cast<float2 *>(st2), z2, y3,
                      reinterpret_cast<float2 *>(st3), z3, coords);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
+                                     const float *st2, const float *y3, const float *st3, const float *W4,
+                                     const float *W3, const float *W2c, const float *W1c, const float *g1,
+                                     const float *be1, const float *g2, const float *be2, const float *g3,
+                                     const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
+                                     size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
+                                     hicgat_stream_t stream) {
+  constexpr int RB = 16;
+  if (M < 0) return HICGAT_EINVAL;
+  if (M == 0) return HICGAT_OK;
+  // every workgroup owns four partial slots of each LN workspace: rows up to 4 slots x 16 rows each
+  if ((M + RB - 1) / RB > kTailBwdSlots / 4) return HICGAT_EUNSUPPORTED;
+  const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                      dx, dY1, dY2, dy3, ws1, ws2, ws3};
+  for (const void *p : ps)
+    if (!p) return HICGAT_EINVAL;
+  if (ws1_bytes < hicgat_ln_relu_res_workspace_bytes(256) || ws2_bytes < hicgat_ln_relu_res_workspace_bytes(128) ||
+      ws3_bytes < hicgat_ln_relu_res_workspace_bytes(64))
+    return HICGAT_EINVAL;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
+  if (!attr) return HICGAT_ELAUNCH;
+  hipLaunchKernelGGL(tail_bwd_kernel<RB>, dim3(kTailBwdSlots / 4), dim3(256), (size_t)2 * RB * XS * sizeof(float),
+                     (hipStream_t)stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1), Y2,
+                     reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c, W1c,
+                     g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1), static_cast<float *>(ws2),
+                     static_cast<float *>(ws3));
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

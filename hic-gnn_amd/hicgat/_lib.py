@@ -92,6 +92,7 @@ SIGNATURES = {
     "hicgat_ln_relu_res_workspace_bytes": (c_sz, [c_int]),
     "hicgat_ln_relu_res_bwd_params": (c_int, [c_int, c_p, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_tail_fwd_fused": (c_int, [c_p, c_i64, c_int] + [c_p] * 14 + [c_f] + [c_p] * 10 + [c_p]),
+    "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p]),
     "hicgat_sage_weights": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_agg": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_int, c_int, c_p, c_i64,
                                 c_p]),

@@ -424,6 +424,25 @@ class HipKernels:
                                                       _lib.stream(dev)), "hicgat_tail_fwd_fused")
         return coords, (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)
 
+    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3):
+        """The tail's input-gradient chain in one launch (tail_fused.hip): returns (dx, dY1, dY2, dy3,
+        (ws1, ws2, ws3)) -- the LayerNorm dgamma/dbeta partials stay in the workspaces
+        (``ln_relu_res_bwd_params``)."""
+        Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = saved
+        M = dcoords.shape[0]
+        dev = dcoords.device
+        f = dict(dtype=torch.float32, device=dev)
+        dx, dY1, dY2, dy3 = (torch.empty((M, w), **f) for w in (512, 512, 256, 64))
+        ws = [self.ln_workspace(w, dev) for w in (256, 128, 64)]
+        ts = [W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3]
+        assert all(t.is_contiguous() for t in ts) and dcoords.is_contiguous()
+        with _timed("tail_bwd_fused"):
+            _lib.check(self.lib.hicgat_tail_bwd_fused(
+                P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dx), P(dY1), P(dY2),
+                P(dy3), P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), P(ws[2]), ws[2].numel(), _lib.stream(dev)),
+                "hicgat_tail_bwd_fused")
+        return dx, dY1, dY2, dy3, ws
+
     def ln_workspace(self, W, device):
         return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)
 

@@ -616,27 +616,48 @@ class _DualLnReluResFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, M, x.shape[1], 2 * w, dY, _joined(W1, W2).contiguous(), torch.empty_like(x),
                         name="gemm_dx")
-        sW1, sW2, sb1, sb2 = _sink(W1), _sink(W2), _sink(b1), _sink(b2)
-        dW1 = dW2 = db1 = db2 = None
-        w_pair = sW1 is not None and sW2 is not None and _adjacent(sW1, sW2)
-        b_pair = sb1 is not None and sb2 is not None and _adjacent(sb1, sb2)
-        if w_pair and b_pair and K.gemm_impl == 1:
-            # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
-            gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
-            _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x,
-                          work=M * 2 * w * x.shape[1])
-        else:
-            if w_pair:
-                _param_launch(lambda: weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True), dY, x)
-            else:
-                dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
-                dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
-            if b_pair:
-                _param_launch(lambda: K.colsum(dY, _joined(sb1, sb2), accumulate=True), dY, small=True)
-            else:
-                db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
-                db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
+        dW1, db1, dW2, db2 = _dual_param_grads(K, W1, b1, W2, b2, dY, x)
         return dx, dW1, db1, dW2, db2, dgamma, dbeta, None
+
+
+def _dual_param_grads(K, W1, b1, W2, b2, dY, x):
+    """dW / db of a dual-Linear pair from its packed output gradient dY = [dy1 | dy2] and input x:
+    into the parameters' sinks (queued side work; returns Nones) or new tensors (returned)."""
+    M, w = dY.shape[0], W1.shape[0]
+    sW1, sW2, sb1, sb2 = _sink(W1), _sink(W2), _sink(b1), _sink(b2)
+    dW1 = dW2 = db1 = db2 = None
+    w_pair = sW1 is not None and sW2 is not None and _adjacent(sW1, sW2)
+    b_pair = sb1 is not None and sb2 is not None and _adjacent(sb1, sb2)
+    if w_pair and b_pair and K.gemm_impl == 1:
+        # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
+        gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
+        _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x,
+                      work=M * 2 * w * x.shape[1])
+    else:
+        if w_pair:
+            _param_launch(lambda: weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True), dY, x)
+        else:
+            dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
+            dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
+        if b_pair:
+            _param_launch(lambda: K.colsum(dY, _joined(sb1, sb2), accumulate=True), dY, small=True)
+        else:
+            db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
+            db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
+    return dW1, db1, dW2, db2
+
+
+def _ln_param_grads(K, gamma, beta, ws):
+    """A LayerNorm's dgamma / dbeta from the per-wave partials a backward pass left in ``ws``: into
+    the sinks (queued side work, as the per-layer path with LN_SIDE) or new tensors (returned)."""
+    W = gamma.shape[0]
+    sg, sb = _sink(gamma), _sink(beta)
+    if sg is not None and sb is not None:
+        _param_launch(lambda: K.ln_relu_res_bwd_params(W, sg, sb, ws, accumulate=True), ws)
+        return None, None
+    dg, db = torch.empty_like(gamma), torch.empty_like(beta)
+    K.ln_relu_res_bwd_params(W, dg, db, ws)
+    return dg, db
 
 
 def dual_ln_relu_res(x, lin1, lin2, norm):
@@ -657,6 +678,9 @@ def dual_ln_relu_res(x, lin1, lin2, norm):
 FUSED_TAIL = os.environ.get("HICGAT_FUSED_TAIL", "1") != "0"
 FUSED_TAIL_MIN_M = int(os.environ.get("HICGAT_FUSED_TAIL_MIN_M", "1024"))
 FUSED_TAIL_MAX_M = int(os.environ.get("HICGAT_FUSED_TAIL_MAX_M", "6144"))
+# ... and its backward input-gradient chain in one launch too (tail_fused.hip; 0: the per-layer
+# functions' backward steps on the fused forward's tensors)
+FUSED_TAIL_BWD = os.environ.get("HICGAT_FUSED_TAIL_BWD", "1") != "0"
 
 
 class _FusedTailFn(torch.autograd.Function):
@@ -684,6 +708,25 @@ class _FusedTailFn(torch.autograd.Function):
         import types
         x, Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = ctx.saved_tensors
         Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3 = ctx.params
+        if FUSED_TAIL_BWD:
+            # the input-gradient chain in one launch; the parameter gradients from its dY tensors
+            # and LN partials, issued in the per-layer path's order (dense3, norm2, dense2, block 2,
+            # block 1)
+            K = kernels.default()
+            dc = dcoords.contiguous()
+            dx, dY1, dY2, dy3, (ws1, ws2, ws3) = K.tail_bwd_fused(
+                dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
+                _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
+                g2.contiguous(), be2.contiguous())
+            dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
+            dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3)
+            dW2, db2 = _wb_grad_to(K, W2, b2, dy3, z2)
+            dg1, dbe1 = _ln_param_grads(K, g1, be1, ws2)
+            dW1, db1, dW1al, db1al = _dual_param_grads(K, W1, b1, W1al, b1al, dY2, z1)
+            dga, dbea = _ln_param_grads(K, ga, bea, ws1)
+            dWa, dba, dWal, dbal = _dual_param_grads(K, Wa, ba, Wal, bal, dY1, x)
+            return (dx if ctx.needs_input_grad[0] else None, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al,
+                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None)
         T = (True,) * 8
 
         def c(**kw):

@@ -375,6 +375,20 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
                           const float *W3, const float *b3, const float *g3, const float *be3, const float *W4,
                           const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2, float *st2,
                           float *z2, float *y3, float *st3, float *z3, float *coords, hicgat_stream_t stream);
+/* The same tail's backward input-gradient chain in one launch: from dcoords [M][3] and the forward's
+ * Y1, st1, Y2, st2, y3, st3 (hicgat_tail_fwd_fused), with W4 = dense3.weight [3][64], W3 = dense2.weight
+ * [64][128], W2c = [W_dense1; W_align_dense1] [256][256], W1c = [W_densea; W_align_densea] [512][512],
+ * g1/be1 = norm_a, g2/be2 = norm1, g3/be3 = norm2: writes dx [M][512] (the gradient of the tail's
+ * input), dY1 [M][512] = [dy | dres] of block 1, dY2 [M][256] of block 2, dy3 [M][64] (dense2's output
+ * gradient) -- the inputs of the weight-gradient GEMMs -- and each LayerNorm's dgamma/dbeta partials
+ * into ws1 / ws2 / ws3 (workspaces of hicgat_ln_relu_res_workspace_bytes(256 / 128 / 64); reduce them
+ * with hicgat_ln_relu_res_bwd_params).  M <= 16384. */
+int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
+                          const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
+                          const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
+                          const float *be2, const float *g3, const float *be3, float *dx, float *dY1, float *dY2,
+                          float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
+                          size_t ws3_bytes, hicgat_stream_t stream);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --

@@ -1363,14 +1363,17 @@ def test_gatconv_tiny_graphs_match_oracle(n):
 
 
 # ---------------------------------------------------------------- a6: the fused MLP-tail forward
-@pytest.mark.parametrize("m,sinks", [(2701, False), (2701, True), (20000, True), (1030, False)])
-def test_fused_tail_matches_per_layer_path(monkeypatch, m, sinks):
-    """GATNetSelectiveResidualsUpdated.post_act through the one-launch forward (tail_fused.hip) vs the
-    per-layer kernels: coords, the input gradient and every tail parameter's gradient (into FlatAdam's
-    gradient sinks, or autograd's .grad), and an fp64 torch evaluation of the forward.  Tolerances:
-    coords 1e-5 of their max (fp32 GEMM order), gradients 1e-4 of each tensor's max."""
+@pytest.mark.parametrize("m,sinks,bwd", [(2701, False, True), (2701, True, True), (2701, True, False),
+                                         (16000, True, True), (1030, False, True)])
+def test_fused_tail_matches_per_layer_path(monkeypatch, m, sinks, bwd):
+    """GATNetSelectiveResidualsUpdated.post_act through the one-launch forward and backward
+    (tail_fused.hip; bwd=False: the per-layer backward steps on the fused forward's tensors) vs the
+    per-layer kernels: coords, the input gradient and every tail parameter's gradient (into
+    FlatAdam's gradient sinks, or autograd's .grad), and an fp64 torch evaluation of the forward.
+    Tolerances: coords 1e-5 of their max (fp32 GEMM order), gradients 1e-4 of each tensor's max."""
     import hicgat
     from hicgat import ops
+    monkeypatch.setattr(ops, "FUSED_TAIL_BWD", bwd)
     torch.manual_seed(7)
     model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
     with torch.no_grad():      # trained-looking LayerNorm affine parameters (beta != 0 moves the kinks)
