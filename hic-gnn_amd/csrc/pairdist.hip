@@ -782,6 +782,30 @@ extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, flo
   return HICGAT_OK;
 }
 
+// finalize + a rank's rows of the all-reduced fp64 dcoords narrowed to fp32 (one launch after the
+// multi-GPU loss all-reduce instead of two)
+__global__ __launch_bounds__(256) void finalize_rows_kernel(int N, int loss_kind, double *__restrict__ stats,
+                                                            float *__restrict__ loss, const double *__restrict__ dc64,
+                                                            int64_t n3, float *__restrict__ dcoords) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t == 0) finalize_stats(N, loss_kind, stats, loss);
+  if (t < n3) dcoords[t] = (float)dc64[t];
+}
+
+extern "C" int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64,
+                                             int row_begin, int row_end, float *dcoords, hicgat_stream_t stream) {
+  if (N <= 0 || !stats || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  const int64_t n3 = 3 * (int64_t)(row_end - row_begin);
+  if (n3 > 0 && (!dc64 || !dcoords)) return HICGAT_EINVAL;
+  const int64_t off = 3 * (int64_t)row_begin;
+  hipLaunchKernelGGL(finalize_rows_kernel, dim3((unsigned)((n3 + 255) / 256 + (n3 == 0))), dim3(256), 0,
+                     (hipStream_t)stream, N, loss_kind, stats, loss, n3 ? dc64 + off : nullptr, n3,
+                     n3 ? dcoords + off : nullptr);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 // ---- background form: T = bg except at a sorted symmetric CSR support + the diagonal -----------
 static int64_t pd_support_blocks(int N) { return (N + 3) / 4; }
 

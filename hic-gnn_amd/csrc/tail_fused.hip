@@ -342,12 +342,6 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   const int slot = blockIdx.x * 4 + wv;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16;
-  if (m0 >= M) {   // the grid covers every partial slot: the waves past the rows write zeros
-    for (int c = lane; c < 2 * 256; c += 64) p1[(size_t)slot * 512 + c] = 0.f;
-    for (int c = lane; c < 2 * 128; c += 64) p2[(size_t)slot * 256 + c] = 0.f;
-    for (int c = lane; c < 2 * 64; c += 64) p3[(size_t)slot * 128 + c] = 0.f;
-    return;
-  }
   // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
   for (int e = tid; e < RB * 64; e += 256) {
     const int r = e >> 6, c = e & 63;
@@ -455,7 +449,7 @@ extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL(tail_bwd_kernel<RB>, dim3(kTailBwdSlots / 4), dim3(256), (size_t)2 * RB * XS * sizeof(float),
+  hipLaunchKernelGGL(tail_bwd_kernel<RB>, dim3((M + RB - 1) / RB), dim3(256), (size_t)2 * RB * XS * sizeof(float),
                      (hipStream_t)stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1), Y2,
                      reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c, W1c,
                      g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1), static_cast<float *>(ws2),

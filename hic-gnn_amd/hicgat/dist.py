@@ -388,8 +388,9 @@ class ShardedTrainer:
                          row0=self.trow0, col0=self.tcol0)
             self.dc64.copy_(self.dcoords)
         self.comm.all_reduce(self.red)
-        K.loss_finalize(N, self.kind, self.stats, self.loss)
-        self.dcoords[self.r0:self.r1].copy_(self.dc64[self.r0:self.r1])
+        # finalize + this rank's rows of dcoords narrowed to fp32, one launch
+        K.loss_finalize(N, self.kind, self.stats, self.loss, dc64=self.dc64, r0=self.r0, r1=self.r1,
+                        dcoords=self.dcoords)
         return self.dcoords[self.r0:self.r1]
 
     def _tail(self, o=None):

@@ -647,17 +647,19 @@ def _dual_param_grads(K, W1, b1, W2, b2, dY, x):
     return dW1, db1, dW2, db2
 
 
-def _ln_param_grads(K, gamma, beta, ws):
-    """A LayerNorm's dgamma / dbeta from the per-wave partials a backward pass left in ``ws``: into
-    the sinks (queued side work, as the per-layer path with LN_SIDE) or new tensors (returned)."""
+def _ln_param_grads(K, gamma, beta, ws, rows):
+    """A LayerNorm's dgamma / dbeta = the column sums of the first ``rows`` per-wave partial rows
+    [dgamma | dbeta] that hicgat_tail_bwd_fused left in ``ws``: into the (adjacent) sinks as queued
+    side work (ONE colsum launch over the live rows, its size as the lane-balancing work) or new
+    tensors (returned)."""
     W = gamma.shape[0]
+    part = ws.view(torch.float32)[:rows * 2 * W].view(rows, 2 * W)
     sg, sb = _sink(gamma), _sink(beta)
-    if sg is not None and sb is not None:
-        _param_launch(lambda: K.ln_relu_res_bwd_params(W, sg, sb, ws, accumulate=True), ws)
+    if sg is not None and sb is not None and _adjacent(sg, sb):
+        _param_launch(lambda: K.colsum(part, _joined(sg, sb), accumulate=True), ws, work=rows * 2 * W)
         return None, None
-    dg, db = torch.empty_like(gamma), torch.empty_like(beta)
-    K.ln_relu_res_bwd_params(W, dg, db, ws)
-    return dg, db
+    out = K.colsum(part, torch.empty(2 * W, dtype=torch.float32, device=part.device))
+    return out[:W], out[W:]
 
 
 def dual_ln_relu_res(x, lin1, lin2, norm):
@@ -709,7 +711,7 @@ class _FusedTailFn(torch.autograd.Function):
         import types
         x, Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = ctx.saved_tensors
         Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3 = ctx.params
-        if FUSED_TAIL_BWD:
+        if FUSED_TAIL_BWD and dcoords.shape[0] <= 16384:   # hicgat_tail_bwd_fused's row limit
             # the input-gradient chain in one launch; the parameter gradients from its dY tensors
             # and LN partials, issued in the per-layer path's order (dense3, norm2, dense2, block 2,
             # block 1)
@@ -719,12 +721,13 @@ class _FusedTailFn(torch.autograd.Function):
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
                 g2.contiguous(), be2.contiguous())
+            rows = 4 * (-(-dc.shape[0] // 16))      # the kernel's partial rows: 4 waves per 16 node rows
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
-            dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3)
+            dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)
             dW2, db2 = _wb_grad_to(K, W2, b2, dy3, z2)
-            dg1, dbe1 = _ln_param_grads(K, g1, be1, ws2)
+            dg1, dbe1 = _ln_param_grads(K, g1, be1, ws2, rows)
             dW1, db1, dW1al, db1al = _dual_param_grads(K, W1, b1, W1al, b1al, dY2, z1)
-            dga, dbea = _ln_param_grads(K, ga, bea, ws1)
+            dga, dbea = _ln_param_grads(K, ga, bea, ws1, rows)
             dWa, dba, dWal, dbal = _dual_param_grads(K, Wa, ba, Wal, bal, dY1, x)
             return (dx if ctx.needs_input_grad[0] else None, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al,
                     dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None)

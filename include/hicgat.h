@@ -264,6 +264,10 @@ int hicgat_pairdist_mse_fused_band(const float *coords, const float *T, int N, i
                                    float *dcoords, void *workspace, size_t workspace_bytes,
                                    hicgat_stream_t stream);
 int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, hicgat_stream_t stream);
+/* hicgat_pairdist_finalize + dcoords[r][c] = (float)dc64[r][c] for rows [row_begin, row_end) of the
+ * (all-reduced) fp64 coordinate gradient [N][3], in one launch (a rank's rows for its tail backward). */
+int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64, int row_begin,
+                                  int row_end, float *dcoords, hicgat_stream_t stream);
 /* Tile count and workspace of the two tilings, mode HICGAT_PD_TRI (the fused loss: upper-triangle
  * 128x128 tiles, nb(nb+1)/2) or HICGAT_PD_SQUARE (hicgat_pairdist_bwd: nb*nb), nb = ceil(N/128). */
 enum { HICGAT_PD_SQUARE = 0, HICGAT_PD_TRI = 1 };
@@ -381,8 +385,9 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
  * g1/be1 = norm_a, g2/be2 = norm1, g3/be3 = norm2: writes dx [M][512] (the gradient of the tail's
  * input), dY1 [M][512] = [dy | dres] of block 1, dY2 [M][256] of block 2, dy3 [M][64] (dense2's output
  * gradient) -- the inputs of the weight-gradient GEMMs -- and each LayerNorm's dgamma/dbeta partials
- * into ws1 / ws2 / ws3 (workspaces of hicgat_ln_relu_res_workspace_bytes(256 / 128 / 64); reduce them
- * with hicgat_ln_relu_res_bwd_params).  M <= 16384. */
+ * into ws1 / ws2 / ws3 (workspaces of hicgat_ln_relu_res_workspace_bytes(256 / 128 / 64)): rows
+ * [0, 4 ceil(M/16)) of a [.][2W] = [dgamma | dbeta] matrix, one per wave (their column sums, e.g.
+ * hicgat_colsum, are dgamma / dbeta).  M <= 16384. */
 int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
                           const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
                           const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,

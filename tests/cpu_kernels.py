@@ -345,7 +345,9 @@ class CpuKernels:
         dcoords.copy_(gf.to(dcoords.dtype).view_as(dcoords))
         self.loss_finalize(n, kind, stats, loss)
 
-    def loss_finalize(self, n, kind, stats, loss):
+    def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None):
+        if dc64 is not None:
+            dcoords[r0:r1].copy_(dc64[r0:r1])
         s = stats.double()
         mse = (2 * float(s[0]) + float(s[6])) / (n * n)
         M = n * (n - 1) / 2
