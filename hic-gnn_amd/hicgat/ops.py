@@ -86,6 +86,7 @@ def side_mark():
 
 
 _FLUSH_LANES = (0, 4, 5, 6)
+SMALL_WORK = 4e6   # side_flush(lanes > 1): items below this many multiply-adds go first in their lane
 
 
 def side_flush(after=None, lanes=1):
@@ -111,6 +112,12 @@ def side_flush(after=None, lanes=1):
             parts[k].append(item)
             load[k] += item[2]
         for lane, items in zip(_FLUSH_LANES, parts):
+            # reductions without a GEMM (the LayerNorm dgamma/dbeta column sums: inputs ready, a few
+            # us each) first in their lane, then the GEMMs (behind the GEMMs they were the last ~30 us
+            # of a P = 8 rank step in profiles/r03v_simprof_xagg_P8_rank0_timeline.txt; the rank step
+            # measured even, 0.581 / 0.564 vs 0.569 / 0.584 ms: streams beyond the box's 4 hardware
+            # queues share one, and a stream waiting on an event stalls the others behind it)
+            items = [q for q in items if q[2] < SMALL_WORK] + [q for q in items if q[2] >= SMALL_WORK]
             if items:
                 with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
                     for fn, _, _ in items:
