@@ -5,7 +5,9 @@
 
 One step = zero_grad + GATConv (MFMA lin_l + fused logits, edge-softmax aggregation) + MLP tail
 + fused distance/MSE loss + backward + Adam, over the whole synthetic Hi-C graph, inputs resident
-in HBM, replayed as one captured hipGraph (``--eager``: kernel by kernel).
+in HBM, replayed as one captured hipGraph (``--eager``: kernel by kernel).  The W warm-up steps are
+real training steps: W - 1 eager ones before the capture and the graph's first replay (which also
+uploads the graph), then the K timed replays.
 
 N > 1: one rank per GPU over RCCL (hicgat.dist: destination rows sharded by an nnz prefix sum;
 "slab" form by default -- the 512-d embeddings gathered once, h recomputed per rank, the source
@@ -320,7 +322,9 @@ def simulate_world(args):
         model = hicgat.MODELS[args.model]().to(dev)
         tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], truth, lr=1e-3, kind=args.loss,
                                   mode=mode, comm=hdist.SimComm(P, r))
-        step = tr.captured(warmup=max(1, args.warmup))
+        step = tr.captured(warmup=max(1, args.warmup - 1) if args.warmup >= 2 else max(1, args.warmup))
+        if args.warmup >= 2:
+            step()       # the last warm-up step: the graph's first replay
         torch.cuda.synchronize()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         evs[0].record()
@@ -453,9 +457,13 @@ def main():
             return hicgat.train.train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss, stats)
 
     eager_step = step
+    # graph mode: the W untimed warm-up steps are W - 1 eager steps (before the capture) and the graph's
+    # first replay (its upload to the device), so the timed region replays a resident graph
+    n_eager = max(1, args.warmup - 1) if args.warmup >= 2 else max(1, args.warmup)
+    replay_warm = args.warmup >= 2
     if args.graph and world > 1:
         try:
-            step = runner.captured(warmup=max(1, args.warmup))   # kernels + RCCL collectives in one graph
+            step = runner.captured(warmup=n_eager)   # kernels + RCCL collectives in one graph
         except RuntimeError as exc:   # recorded in the JSON line ("graph": false, "graph_error")
             graph_error = f"{type(exc).__name__}: {exc}"
             log(f"[bench] rank {rank}: GRAPH CAPTURE OF THE SHARDED STEP FAILED ({exc}); timing eager steps")
@@ -463,9 +471,13 @@ def main():
             args.graph = False
             for w in range(args.warmup):
                 step()
+        if args.graph and replay_warm:
+            step()
     elif args.graph:
         step = hicgat.graphs.captured_train_step(model, opt, wl["x"], wl["adj"], wl["truth"], args.loss,
-                                                 warmup=max(1, args.warmup))
+                                                 warmup=n_eager)
+        if replay_warm:
+            step()
     else:
         for w in range(args.warmup):
             step()
