@@ -200,13 +200,13 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode):
     assert (g - res["grad1"]).abs().max().item() <= gt * g.abs().max().item(), per
 
 
-@pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "xagg"), (2, "allgather"), (3, "slab"), (3, "xagg"),
-                                        (3, "allgather"), (4, "xagg"), (8, "xagg")])
-def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,n", [(2, "slab", 777), (2, "xagg", 777), (2, "allgather", 777), (3, "slab", 777),
+                                          (3, "xagg", 777), (3, "allgather", 777), (4, "xagg", 777), (8, "xagg", 777),
+                                          (2, "xagg", 3000)])
+def test_sharded_ranks_equal_one_rank(tmp_path, world, mode, n):
     """nnz-balanced shards over gloo on the one GPU, every step form, 2 and 3 (uneven) ranks, and the
     form bench.py's "auto" runs at the driver's 4 and 8 ranks (xagg), against world 1 of the same
-    form."""
-    n = 777
+    form; n = 3000 puts 1 500 / 3 000 rows on a rank: the one-kernel tail on both sides."""
     one = _run(1, "gloo", n, tmp_path, mode)
     many = _run(world, "gloo", n, tmp_path, mode)
     # the MLP tail runs on shards of the rows and the partial sums (dW, dcoords, loss moments) are
@@ -218,16 +218,20 @@ def test_sharded_ranks_equal_one_rank(tmp_path, world, mode):
     np.testing.assert_allclose(many["loss"], one["loss"], rtol=1e-3)
 
 
-@pytest.mark.parametrize("mode", ["slab", "xagg"])
-def test_simulated_ranks_run_their_shares(mode):
-    """bench.py --simulate-world: each rank's share of a 3-rank step runs captured on one GPU with
-    the collectives left out; the shards partition the edges, slabs, tiles and support rows."""
-    hicgat, adj, truth, x = _inputs(777, "cuda")
+@pytest.mark.parametrize("mode,n,world", [("slab", 777, 3), ("xagg", 777, 3), ("xagg", 3000, 2)])
+def test_simulated_ranks_run_their_shares(mode, n, world):
+    """bench.py --simulate-world: each rank's share of a sharded step runs captured on one GPU with
+    the collectives left out; the shards partition the edges, slabs, tiles and support rows.  n = 3000
+    over 2 ranks puts 1 500 rows on a rank: the one-kernel tail forward / backward (ops.fused_tail)
+    inside the captured sharded step."""
+    from hicgat import ops
+    hicgat, adj, truth, x = _inputs(n, "cuda")
     tot = {"nnz": 0, "slab": 0, "tiles": 0, "srows": 0}
-    for r in range(3):
+    for r in range(world):
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
-        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(3, r), mode=mode)
+        tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(world, r), mode=mode)
+        assert ops.fused_tail_ok(model, torch.empty(tr.local_rows, 512, device="cuda")) == (n == 3000)
         step = tr.captured(warmup=1)
         for _ in range(2):
             loss = step()[0]
@@ -238,7 +242,7 @@ def test_simulated_ranks_run_their_shares(mode):
         tot["tiles"] += tr.t1 - tr.t0
         tot["srows"] += tr.s1 - tr.s0
     assert tot["nnz"] == tot["slab"] == adj.device_nnz
-    assert tot["srows"] == 777 and tot["tiles"] == tr.plan.tiles
+    assert tot["srows"] == n and tot["tiles"] == tr.plan.tiles
 
 
 @pytest.mark.parametrize("mode,n", [("slab", 300), ("slab", 777), ("xagg", XAGG_NS[0]), ("xagg", XAGG_NS[1])])
