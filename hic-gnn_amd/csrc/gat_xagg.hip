@@ -27,7 +27,7 @@
 //                       through the column slab (the transpose, by a precomputed permutation),
 //                       and g_src^h = sum_j da_src_j^h x_j in the same pass (+ xagg_colred)
 //   xagg_param_finish   dW += att (x) g terms, datt_src / datt_dst = W_h g
-#include "mfma16.hpp"
+#include "common.hpp"
 
 #ifndef HICGAT_XAGG_U
 #define HICGAT_XAGG_U 4   // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
@@ -463,78 +463,6 @@ __global__ __launch_bounds__(256) void xagg_param_finish_kernel(const float *__r
   }
 }
 
-// ---- the per-head GEMMs in one launch each (16 own rows per workgroup; mfma16.hpp) -----------------
-// forward: Y0[:, 256h + c] = xa^h W_h^T + b (the columns of head h), O = relu(Y0); waves 0, 1 take
-// head 0's columns 128w .., waves 2, 3 head 1's, each from its head's xa rows in LDS.  Replaces two
-// K-split GEMMs on two streams, their slab sums and the bias / relu pass (5 launches + a join).
-__global__ __launch_bounds__(256) void xagg_out_kernel(const float *__restrict__ X4, int R,
-                                                       const float *__restrict__ W, const float *__restrict__ bias,
-                                                       float *__restrict__ y0, float *__restrict__ o) {
-  constexpr int RB = 16;
-  extern __shared__ __attribute__((aligned(16))) float lds_x[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * RB;
-  for (int e = tid; e < 2 * RB * 128; e += 256) {   // xa rows of both heads -> LDS (rows past R: 0)
-    const int hd = e / (RB * 128), r = (e >> 7) % RB, c4 = e & 127;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m0 + r < R) v = reinterpret_cast<const float4 *>(X4 + ((size_t)(hd * 2) * R + m0 + r) * 512)[c4];
-    *reinterpret_cast<float4 *>(&lds_x[(hd * RB + r) * XS + 4 * c4]) = v;
-  }
-  __syncthreads();
-  const int hd = wv >> 1, n0 = 256 * hd + 128 * (wv & 1);
-  f32x4 acc[1][8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows<RB, 8, 512>(lds_x + hd * RB * XS, XS, W, n0, acc, lane);
-  const int li = lane & 15, r0 = 4 * (lane >> 4);
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int c = n0 + 16 * t + li;
-    const float bb = bias[c];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + r0 + r;
-      if (row < R) {
-        const float v = acc[0][t][r] + bb;
-        y0[(size_t)row * 512 + c] = v;
-        o[(size_t)row * 512 + c] = relu_t(v);
-      }
-    }
-  }
-}
-
-// backward: dxa[:, 512h + n] = dout[:, 256h ..] W_h (K = 256, the head's output columns); block y:
-// the 256-column half of both heads' 512 outputs, wave w: head w >> 1, columns 256y + 128 (w & 1) ..
-__global__ __launch_bounds__(256) void xagg_dxa_kernel(const float *__restrict__ dout, int R,
-                                                       const float *__restrict__ W, float *__restrict__ dxa) {
-  constexpr int RB = 16;
-  extern __shared__ __attribute__((aligned(16))) float lds_x[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * RB;
-  for (int e = tid; e < RB * 128; e += 256) {        // dout rows [RB][512] -> LDS
-    const int r = e >> 7, c4 = e & 127;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m0 + r < R) v = reinterpret_cast<const float4 *>(dout + (size_t)(m0 + r) * 512)[c4];
-    *reinterpret_cast<float4 *>(&lds_x[r * XS + 4 * c4]) = v;
-  }
-  __syncthreads();
-  const int hd = wv >> 1, n0 = 256 * blockIdx.y + 128 * (wv & 1);
-  f32x4 acc[1][8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows_t<RB, 8, 256>(lds_x + 256 * hd, XS, W + (size_t)256 * hd * 512, 512, n0, acc, lane);
-  const int li = lane & 15, r0 = 4 * (lane >> 4);
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int c = 512 * hd + n0 + 16 * t + li;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + r0 + r;
-      if (row < R) dxa[(size_t)row * 1024 + c] = acc[0][t][r];
-    }
-  }
-}
-
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -637,35 +565,6 @@ extern "C" int hicgat_xagg_param_finish(const float *W, const float *att_src, co
   if (!W || !att_src || !att_dst || !g_src || !g_dst || !dW || !datt_src || !datt_dst) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_param_finish_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, W, att_src, att_dst,
                      g_src, g_dst, dW, datt_src, datt_dst);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
-}
-
-extern "C" int hicgat_xagg_out_fused(const float *X4, int R, int F, int H, int C, const float *W, const float *bias,
-                                     float *y0, float *o, hicgat_stream_t stream) {
-  if (R < 0) return HICGAT_EINVAL;
-  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (R == 0) return HICGAT_OK;
-  if (!X4 || !W || !bias || !y0 || !o) return HICGAT_EINVAL;
-  if (((uintptr_t)X4 | (uintptr_t)W) & 15) return HICGAT_EUNSUPPORTED;
-  constexpr size_t lds = (size_t)2 * 16 * XS * sizeof(float);
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&xagg_out_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
-  if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL(xagg_out_kernel, dim3((R + 15) / 16), dim3(256), lds, (hipStream_t)stream, X4, R, W, bias, y0, o);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
-}
-
-extern "C" int hicgat_xagg_dxa_fused(const float *dout, int R, int F, int H, int C, const float *W, float *dxa,
-                                     hicgat_stream_t stream) {
-  if (R < 0) return HICGAT_EINVAL;
-  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (R == 0) return HICGAT_OK;
-  if (!dout || !W || !dxa) return HICGAT_EINVAL;
-  if ((uintptr_t)dout & 15) return HICGAT_EUNSUPPORTED;
-  constexpr size_t lds = (size_t)16 * XS * sizeof(float);
-  hipLaunchKernelGGL(xagg_dxa_kernel, dim3((R + 15) / 16, 2), dim3(256), lds, (hipStream_t)stream, dout, R, W, dxa);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

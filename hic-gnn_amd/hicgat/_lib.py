@@ -73,8 +73,6 @@ SIGNATURES = {
                                  c_f, c_p, c_p]),
     "hicgat_xagg_slab_workspace_bytes": (c_sz, []),
     "hicgat_xagg_slab_sum": (c_int, [c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
-    "hicgat_xagg_out_fused": (c_int, [c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p]),
-    "hicgat_xagg_dxa_fused": (c_int, [c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p]),
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_pairdist_mse_fused_support_range": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64, c_int,
                                                         c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),

@@ -72,9 +72,6 @@ HEAD_STREAM = os.environ.get("HICGAT_HEAD_STREAM", "1") != "0"
 # side streams for the MLP tail's queued parameter-gradient launches in the sharded step
 # (ops.side_flush lanes; 1 = one chain as on a single GPU)
 SIDE_LANES = int(os.environ.get("HICGAT_DIST_SIDE_LANES", "3"))
-# "xagg": the per-head GEMMs in one launch each (gat_xagg.hip xagg_out_fused / xagg_dxa_fused: both
-# heads, bias and relu; 0: K-split GEMMs per head on two streams + slab sums + the bias/relu pass)
-XAGG_FUSED = os.environ.get("HICGAT_XAGG_FUSED", "1") != "0"
 
 
 def partition_rows(rowptr, P):
@@ -518,17 +515,12 @@ class ShardedTrainer:
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
         Y0 = self.Y0
         # out (head hd columns) = xa^hd W_hd^T; the forward needs no out2 (da_dst comes from dxa . xa2)
-        if self.cuda and XAGG_FUSED and self.act:
-            K.xagg_out_fused(self.X4, W.contiguous(), bias, Y0, self.O)      # both heads + bias + relu
-            o, coords_loc, coords = self._tail(self.O)
-        elif self.act:
-            self._heads(lambda hd: K.gemm(0, 0, Rl, C, F, self.X4[hd, 0], W[hd * C:(hd + 1) * C],
-                                          Y0[:, hd * C:(hd + 1) * C], name="gemm_fwd"))
+        self._heads(lambda hd: K.gemm(0, 0, Rl, C, F, self.X4[hd, 0], W[hd * C:(hd + 1) * C],
+                                      Y0[:, hd * C:(hd + 1) * C], name="gemm_fwd"))
+        if self.act:
             K.xagg_bias_relu(Y0, bias, self.O)
             o, coords_loc, coords = self._tail(self.O)
         else:
-            self._heads(lambda hd: K.gemm(0, 0, Rl, C, F, self.X4[hd, 0], W[hd * C:(hd + 1) * C],
-                                          Y0[:, hd * C:(hd + 1) * C], name="gemm_fwd"))
             Y0.add_(bias)
             o, coords_loc, coords = self._tail(Y0)
         # ---- backward -----------------------------------------------------------------------
@@ -538,12 +530,8 @@ class ShardedTrainer:
             rs_own = self.rs[r0:r1]
             K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
             # dxa^hd = dout^hd W_hd
-            if self.cuda and XAGG_FUSED:
-                K.xagg_dxa_fused(self.dout_l, W.contiguous(), self.dxa)
-            else:
-                self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C],
-                                              W[hd * C:(hd + 1) * C], self.dxa[:, hd * F:(hd + 1) * F],
-                                              name="gemm_dx"))
+            self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
+                                          self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx"))
             fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
             # dW_h += dout^h^T xa^h (K = own rows, split) and dbias on side lanes 2 / 3, forked after the
             # dxa GEMMs so they run beside the edge pass and the slab sum (issued after the slab sum

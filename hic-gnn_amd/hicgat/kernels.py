@@ -266,22 +266,6 @@ class HipKernels:
             _lib.check(self.lib.hicgat_xagg_slab_sum(P(rowptr_s), P(perm), N, P(ds), P(x), P(da_src), P(g_src), P(ws),
                                                      ws.numel(), _lib.stream(ds.device)), "hicgat_xagg_slab_sum")
 
-    def xagg_out_fused(self, X4, W, bias, y0, o):
-        """y0 = per head xa^h W_h^T + bias, o = relu(y0), one launch (gat_xagg.hip)."""
-        R = X4.shape[2]
-        assert X4.is_contiguous() and W.is_contiguous() and y0.is_contiguous() and o.is_contiguous()
-        with _timed("gemm_fwd"):
-            _lib.check(self.lib.hicgat_xagg_out_fused(P(X4), R, 512, 2, 256, P(W), P(bias), P(y0), P(o),
-                                                      _lib.stream(X4.device)), "hicgat_xagg_out_fused")
-
-    def xagg_dxa_fused(self, dout, W, dxa):
-        """dxa = per head dout^h W_h, one launch (gat_xagg.hip)."""
-        R = dout.shape[0]
-        assert dout.is_contiguous() and W.is_contiguous() and dxa.is_contiguous() and dxa.shape == (R, 1024)
-        with _timed("gemm_dx"):
-            _lib.check(self.lib.hicgat_xagg_dxa_fused(P(dout), R, 512, 2, 256, P(W), P(dxa), _lib.stream(dout.device)),
-                       "hicgat_xagg_dxa_fused")
-
     def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
         H, C = att_l.shape[-2], att_l.shape[-1]
         _lib.check(self.lib.hicgat_xagg_param_finish(P(W), P(att_l), P(att_r), P(g_src), P(g_dst), W.shape[1], H, C,

@@ -179,14 +179,6 @@ size_t hicgat_xagg_slab_workspace_bytes(void);
 int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, const float *x,
                          float *da_src, float *g_src, void *workspace, size_t workspace_bytes,
                          hicgat_stream_t stream);
-/* The per-head GEMMs of the xagg step in one launch each (16 own rows per workgroup, fp32 16x16x4
- * MFMA): hicgat_xagg_out_fused: y0 [R][512] = per head h xa^h W_h^T + bias (columns 256h..), o = relu(y0),
- * xa^h = X4 [2][2][R][512] kind 0; hicgat_xagg_dxa_fused: dxa [R][1024] = per head dout[:, 256h..] W_h
- * (columns 512h..).  F = 512, H = 2, C = 256; X4 / dout 16-B aligned. */
-int hicgat_xagg_out_fused(const float *X4, int R, int F, int H, int C, const float *W, const float *bias, float *y0,
-                          float *o, hicgat_stream_t stream);
-int hicgat_xagg_dxa_fused(const float *dout, int R, int F, int H, int C, const float *W, float *dxa,
-                          hicgat_stream_t stream);
 int hicgat_xagg_param_finish(const float *W, const float *att_src, const float *att_dst, const float *g_src,
                              const float *g_dst, int F, int H, int C, float *dW, float *datt_src, float *datt_dst,
                              hicgat_stream_t stream);

@@ -145,26 +145,3 @@ def test_xagg_gemm_calls_match_float64(shape):
     err = _rel(got, ref)
     print(shape, f"{err:.2e}")
     assert err < 1e-5
-
-
-@pytest.mark.parametrize("R", [2701, 1030, 37])
-def test_xagg_fused_head_gemms_match_float64(R):
-    """The one-launch per-head GEMMs of the xagg step (xagg_out_fused: both heads + bias + relu;
-    xagg_dxa_fused) against float64 torch, ragged row counts (R not a multiple of the 16-row block)."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import hicgat
-    K = hicgat.kernels.default()
-    g = torch.Generator().manual_seed(R)
-    W = (0.05 * torch.randn((512, 512), generator=g)).cuda()
-    b = torch.randn(512, generator=g).cuda()
-    X4 = torch.randn((2, 2, R, 512), generator=g).cuda()
-    y0, o = torch.full((R, 512), float("nan")).cuda(), torch.full((R, 512), float("nan")).cuda()
-    K.xagg_out_fused(X4, W, b, y0, o)
-    ref = torch.cat([X4[hd, 0].double() @ W[hd * 256:(hd + 1) * 256].double().t() for hd in range(2)], 1) + b.double()
-    assert _rel(y0, ref) < 1e-5 and torch.equal(o, torch.relu(y0))
-    dout = torch.randn((R, 512), generator=g).cuda()
-    dxa = torch.full((R, 1024), float("nan")).cuda()
-    K.xagg_dxa_fused(dout, W, dxa)
-    ref = torch.cat([dout[:, hd * 256:(hd + 1) * 256].double() @ W[hd * 256:(hd + 1) * 256].double() for hd in range(2)], 1)
-    assert _rel(dxa, ref) < 1e-5
