@@ -52,6 +52,28 @@ def test_ctypes_signatures_match_header_arity():
         assert len(args) == arity[name], (name, len(args), arity[name])
 
 
+def test_row_split_policy():
+    """kernels.row_splits: the single-GPU N = 20000 GEMM shapes are never K-split; a rank's shard
+    (N = 20000 over P = 2..8) is split only as far as ~512 workgroups and never below 128-deep
+    K chunks."""
+    from hicgat import kernels as hk
+    dims = (3, 64, 128, 256, 512, 1024)
+    for n_out in dims:
+        for k in dims:
+            assert hk.row_splits(20000, n_out, k) == 1
+            assert hk.row_splits(20000, k, n_out) == 1
+    for p in range(2, 9):
+        m = -(-20000 // p)
+        for n_out in (64, 128, 256, 512):
+            for k in (256, 512, 1024):
+                s = hk.row_splits(m, n_out, k)
+                wgs = -(-m // 64) * -(-n_out // (128 if n_out >= 128 else 64))
+                assert 1 <= s <= k // 128
+                if s > 1:
+                    assert wgs < 256 and wgs * (s - 1) < 512
+    assert hk.row_splits(2500, 512, 128) == 1 and hk.row_splits(512, 512, 512) == 1
+
+
 def test_query_functions_need_no_gpu():
     from hicgat import _lib
     lib = _lib.load()
