@@ -98,6 +98,8 @@ def main(argv=None):
     p.add_argument("--weights", default=None, help="trained state_dict (.pt); trained here when missing")
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--out", default=None, help="prefix for the weights / PDB / log files")
+    p.add_argument("-print_interval", "--print_interval", type=int, default=10,
+                   help="print MSE and dSCC every this many steps (:87)")
     a = p.parse_args(argv)
     l1, l2 = np.loadtxt(a.list_trained), np.loadtxt(a.list_untrained)
     normed, emb = [], []
@@ -117,8 +119,12 @@ def main(argv=None):
     else:
         data = graph.load_input(normed[0], e1.astype(np.float32))
         truth = graph.Truth.from_contacts(data.y, a.conversion)
-        _, hist = train.train(model, data, truth, a.learningrate, a.loss_diff_threshold, a.steps, "combined")
+        dscc_hist = []      # the per-step dSCC of :242-247 (the forward's coordinates before the update)
+        _, hist = train.train(model, data, truth, a.learningrate, a.loss_diff_threshold, a.steps, "combined",
+                              dscc_history=dscc_hist, print_interval=a.print_interval)
         print(f"trained {len(hist)} steps, final loss {hist[-1]:.6g}")
+        print(f"\nOptimal dSCC after training: {dscc_hist[-1]}")                          # :273
+        print(f"dSCC Loss - Mean: {np.mean(dscc_hist)}, Max: {np.max(dscc_hist)}")         # :278-280
         if a.weights:
             torch.save(train.cpu_state_dict(model), a.weights)
     rho, coords = generalize(model, l1, l2, e1, e2, normed[1], a.conversion)

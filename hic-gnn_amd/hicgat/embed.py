@@ -78,15 +78,19 @@ def vocab_tables(counts, sample=1e-3, ns_exponent=0.75):
 
 def initial_vectors(walks, n_words, dimensions, w2v_seed=1):
     """gensim 4's initial input vectors: ``prep_vectors`` draws ``default_rng(seed).random((V, D))``
-    mapped to U(-1/D, 1/D) for the vocabulary in its order -- ``sort_by_descending_frequency``, a
-    stable sort of the words in first-appearance order of the corpus -- so node n gets row
-    rank(n).  The reference's ``.fit(window=25, min_count=1, batch_words=4)`` passes no seed, so
-    Word2Vec's default seed 1 applies."""
+    mapped to U(-1/D, 1/D) for the vocabulary in its order, so node n gets row rank(n).  The order:
+    ``prepare_vocab`` adds the words in first-appearance order of the corpus scan (the raw vocabulary
+    dict), then ``sort_by_descending_frequency`` permutes them by ``np.argsort(count)[::-1]`` --
+    numpy's default (unstable) sort, reversed, so tied words are NOT in first-appearance order; the
+    same expression is applied here to the same count array.  The reference's
+    ``.fit(window=25, min_count=1, batch_words=4)`` passes no seed, so Word2Vec's default seed 1
+    applies.  (gensim is absent here: the rule is restated from its published source, unpinned.)"""
     flat = walks.reshape(-1)
     flat = flat[flat >= 0].cpu().numpy().astype(np.int64)
     counts = np.bincount(flat, minlength=n_words)
     words, first = np.unique(flat, return_index=True)
-    order = words[np.lexsort((first, -counts[words]))]          # descending count, then first appearance
+    scan = words[np.argsort(first)]                             # first-appearance order
+    order = scan[np.argsort(counts[scan])[::-1]]                # gensim 4 sort_by_descending_frequency
     init = np.random.default_rng(seed=w2v_seed).random((len(order), dimensions), dtype=np.float32)
     init *= 2.0
     init -= 1.0
@@ -96,12 +100,16 @@ def initial_vectors(walks, n_words, dimensions, w2v_seed=1):
     return vec
 
 
+SMALL_VOCAB = 1024
+
+
 def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, alpha=0.025, min_alpha=1e-4,
              sample=1e-3, seed=42, max_waves=None, w2v_seed=1):
     """Word2Vec(sg=1, hs=0) over the walks: returns the input vectors syn0 [n_words, dimensions].
-    ``max_waves`` bounds the walks trained concurrently (default n_words // 64, within [1, 4096]):
-    on a Hi-C-sized vocabulary (58 loci for chr19 1 mb) concurrent Hogwild writers to the same
-    rows would lose updates, so small vocabularies train sequentially."""
+    ``max_waves`` bounds the walks trained concurrently: on a Hi-C-sized vocabulary (58 loci for
+    chr19 1 mb) concurrent Hogwild writers to the same rows would lose updates, so vocabularies
+    below ``SMALL_VOCAB`` words train near-sequentially (n_words // 64 walks at once); larger ones
+    keep n_words // 4 walks in flight (at most 4096)."""
     lib = _lib.lib()
     dev = walks.device
     nwalks, L = walks.shape
@@ -117,7 +125,7 @@ def skipgram(walks, n_words, dimensions=512, window=25, epochs=5, negative=5, al
         # a Hi-C chromosome at 1 mb / 500 kb (58 / 114 loci); measured on chr19 1 mb, 1 vs 14
         # concurrent walks give the same embedding structure (common-component share 0.984 vs
         # 0.980, profiles/r03b_n2v_study.json) at 20 vs 5 s
-        max_waves = max(1, min(4096, n_words // 64))
+        max_waves = max(1, n_words // 64) if n_words < SMALL_VOCAB else max(1, min(4096, n_words // 4))
     for ep in range(epochs):
         _lib.check(lib.hicgat_n2v_sgns_epoch(P(walks), nwalks, L, P(t_keep), P(t_cum), n_words, dimensions, window,
                                              negative, float(alpha), float(min_alpha), ep, epochs,

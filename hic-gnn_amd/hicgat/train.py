@@ -33,22 +33,45 @@ def train_step(model, opt, x, edge_index, truth, kind="mse", stats=None):
     return loss, stats, coords
 
 
+GRAPH_WARMUP = 2   # eager steps before the step is captured (real training steps, in the history)
+
+
 def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_steps=1_000_000,
-          on_step=None):
-    """Returns (optimizer, per-step loss list).  ``truth`` is a ``graph.Truth``."""
+          on_step=None, graph=None, dscc_history=None, print_interval=0):
+    """Returns (optimizer, per-step loss list).  ``truth`` is a ``graph.Truth``.
+
+    ``graph`` (default: on for device tensors): after ``GRAPH_WARMUP`` eager steps the step is
+    captured once (``graphs.CapturedStep``) and replayed; the loss is still read on the host every
+    step for the ``lossdiff`` rule (HiC-GNN_main.py:128) -- replays give the same bits as eager steps.
+    ``dscc_history`` (a list): the dSCC of every step's forward coordinates against the target, as
+    HiC_GAT_generalize_directly.py:242-247 appends it; ``print_interval`` > 0 prints its progress line
+    (:256) every that many steps."""
+    from .graphs import CapturedStep
     opt = FlatAdam(model.flat_parameters(), lr=lr)
+    use_graph = data.x.is_cuda if graph is None else bool(graph)
+    if use_graph:
+        opt.enable_device_step()
     old, diff, hist = 1.0, 1.0, []
     stats = torch.empty(12, dtype=torch.float64, device=data.x.device)
+    score = truth.scoring() if dscc_history is not None else None
+
+    def step():
+        return train_step(model, opt, data.x, data.edge_index, truth, loss, stats)
+
+    replay = None
     while (diff > thresh if steps is None else len(hist) < steps) and len(hist) < max_steps:
-        model.train()
-        opt.zero_grad()
-        val, stats, _ = model.loss(data.x, data.edge_index, truth, loss, stats=stats)
-        lv = float(val.item())
+        if use_graph and replay is None and len(hist) >= GRAPH_WARMUP:
+            replay = CapturedStep(step, warmup=0)     # captured, not run: the replay below is this step
+        val, _, coords = replay() if replay is not None else step()
+        lv = float(val.item())                        # the one device -> host read per step
         diff = abs(old - lv)
-        val.backward()
-        opt.step()
         old = lv
         hist.append(lv)
+        if score is not None:
+            dscc_history.append(metrics.dscc(coords, score))
+            if print_interval and (len(hist) - 1) % print_interval == 0:
+                print(f"Iteration [{len(hist) - 1}], Total Loss: {float(stats[7]):.6g}, dSCC: {dscc_history[-1]}, "
+                      f"Loss Diff: {diff}")
         if on_step is not None:
             on_step(len(hist), lv)
     return opt, hist

@@ -1221,7 +1221,60 @@ def test_config5_generalisation_matches_oracle():
           f"vs oracle {float(band['loss'][ref_i]):.6e}")
     assert abs(rho_tf - g_ref) <= 1e-3, (rho_tf, g_ref)
     assert abs(rho_tr - float(tb[ref_i])) <= 0.005, (rho_tr, tb)
-    assert gb.min() - 0.02 <= rho_gen <= gb.max() + 0.02, (rho_gen, gb)
+    # the generalised dSCC of ONE free run moves by ~0.04 under a rounding change (the oracle's own
+    # seed 0 at 1/2/4/8 threads: 0.339-0.376): checked on the seed median, test below
+    assert 0.0 < rho_gen < 1.0, rho_gen
+
+
+def _config5_inputs():
+    import hicgat
+    band = load_golden("config5_band_chr19.npz")
+    al = load_golden("align_chr19_f512.npz")
+    scale = float(band["feature_scale"])
+    e1 = (scale * al["emb1"]).astype(np.float32)
+    e2 = (scale * al["emb2"]).astype(np.float32)
+    normed = {}
+    for tag in ("1mb", "500kb"):
+        a = np.array(load_golden(f"graph_chr19_{tag}.npz")["matrix"], dtype=np.float64)
+        np.fill_diagonal(a, 0)
+        normed[tag] = hicgat.kr.KRnorm(a)[0].cpu().numpy()
+    return al, e1, e2, normed
+
+
+@pytest.mark.timeout(900)
+def test_config5_generalisation_seed_median_matches_oracle():
+    """BASELINE configs[4] free-running, on the seed protocol of the chr19 1 mb north-star check:
+    train on 1 mb (combined loss, K = 1000, initial-weight seeds 0..23), generalise to 500 kb
+    (HiC_GAT_generalize_directly.py:312-336); the MEDIAN generalised dSCC over the seeds within
+    +-0.01 of the oracle's median over the same seeds at 1 thread (tests/golden/make_config5_seeds.py).
+    The same fixture holds the oracle at 2 threads -- another fp32 summation order of the same
+    arithmetic, i.e. what a rounding change alone does: its median sits 2.1e-3 from the 1-thread one,
+    so +-0.01 is ~5x the rounding-level movement of the statistic, while one seed's value moves by up
+    to 0.04 (seed 0: 0.346 / 0.380)."""
+    import hicgat
+    fx = load_golden("config5_seeds_chr19.npz")
+    K = int(fx["steps"])
+    one = fx["threads"] == 1
+    seeds = [int(v) for v in fx["seeds"][one]]
+    ref = np.asarray(fx["dscc_generalised"][one], dtype=np.float64)
+    ref2 = np.asarray(fx["dscc_generalised"][fx["threads"] == 2], dtype=np.float64)
+    al, e1, e2, normed = _config5_inputs()
+    data = hicgat.load_input(normed["1mb"], e1)
+    truth = hicgat.Truth.from_contacts(data.y, 1)
+    dev = []
+    for sd in seeds:
+        torch.manual_seed(sd)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+        hicgat.train.train(model, data, truth, steps=K, loss="combined")
+        rho, _ = hicgat.align.generalize(model, al["list1"], al["list2"], e1, e2, normed["500kb"], 1)
+        dev.append(rho)
+    dev = np.asarray(dev)
+    with np.printoptions(precision=4):
+        print(f"[config5 seeds] K={K} generalised 500 kb dSCC, seeds {seeds[0]}..{seeds[-1]}: device median "
+              f"{np.median(dev):.6f} (mean {dev.mean():.6f}); oracle 1 thread median {np.median(ref):.6f} (mean "
+              f"{ref.mean():.6f}), 2 threads {np.median(ref2):.6f}; |diff of medians| "
+              f"{abs(np.median(dev) - np.median(ref)):.2e}; device {dev}; oracle {ref}")
+    assert abs(np.median(dev) - np.median(ref)) <= 0.01, (np.median(dev), np.median(ref))
 
 
 # ---------------------------------------------------------------- north star: dSCC band
@@ -1383,7 +1436,7 @@ def test_fused_tail_matches_per_layer_path(monkeypatch, m, sinks, bwd):
     x0 = torch.relu(torch.randn(m, 512, device=DEV))
     g = torch.randn(m, 3, device=DEV)
     # the tail is row-wise: rows holding a relu input within 1e-5 of the kink (where the two fp32 GEMM
-    # orders may take different sides, tests/test_gpu_dist.py XAGG_NS) get no upstream gradient, so
+    # orders may take different sides, tests/kinks.py) get no upstream gradient, so
     # neither path's backward sees them
     d = torch.float64
 

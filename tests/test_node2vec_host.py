@@ -61,14 +61,17 @@ def test_second_step_table_factors():
 
 def test_initial_vectors_follow_gensim4_prep_vectors():
     """gensim 4 ``prep_vectors``: default_rng(seed).random((V, D)) * 2 - 1, / D, rows in the
-    vocabulary order (descending count, ties by first appearance); Word2Vec's default seed 1."""
+    vocabulary order of sort_by_descending_frequency (np.argsort(count)[::-1] over the words in
+    first-appearance order: ties come out reversed); Word2Vec's default seed 1."""
     import torch
     from hicgat import embed
     walks = torch.tensor([[2, 0, 2, 1, -1], [3, 2, 0, 0, 2]], dtype=torch.int32)   # counts 0:3 1:1 2:4 3:1
     v = embed.initial_vectors(walks, 5, 8, w2v_seed=1)
     ref = np.random.default_rng(seed=1).random((4, 8), dtype=np.float32) * 2.0 - 1.0
     ref /= 8
-    order = [2, 0, 1, 3]                  # 2 (4x), 0 (3x), then 1 and 3 (1x each) by first appearance
+    scan, cnt = np.array([2, 0, 1, 3]), np.array([4, 3, 1, 1])     # first appearance; counts 4, 3, 1, 1
+    order = list(scan[np.argsort(cnt)[::-1]])
+    assert order[:2] == [2, 0]            # 2 (4x), 0 (3x), then the tie 1 / 3 in numpy's argsort order
     for rank, node in enumerate(order):
         assert np.array_equal(v[node], ref[rank])
     assert not v[4].any()                 # never visited: not in the vocabulary

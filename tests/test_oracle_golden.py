@@ -248,3 +248,38 @@ def test_domain_alignment_oracle_matches_reference(golden, f):
     fit, R, A, B = align.domain_alignment(fx["list1"], fx["list2"], fx["emb1"], fx["emb2"])
     np.testing.assert_array_equal(fit, fx["fitembed"])
     assert np.abs(R.T @ R - np.eye(f)).max() < 1e-5
+
+
+# the reference's own parameter counts (code comments above the classes in models.py): the one
+# reference-held number that fixes GATConv's layout -- lin_l without bias and shared with lin_r,
+# att_l / att_r [1, 2, 256], bias [512]
+REF_PARAM_COUNTS = {"GATNetHeadsChanged3LayersLeakyReLUv2": 411651,   # /root/reference/models.py:1009
+                    "GATNetSelectiveResidualsUpdated": 601475}        # 263 680 (GATConv) + the tail of :619-632
+GATCONV_512_256_H2 = 512 * 512 + 2 * (2 * 256) + 512                   # lin_l + att_l + att_r + bias
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_parameter_count_matches_reference(golden, name):
+    """Unique parameters of the product class (hicgat), the oracle class and the reference-composed
+    class (its gradients in the make_golden fixture: one per registered parameter, lin_r aliased) ==
+    the count models.py states for GATNetHeadsChanged3LayersLeakyReLUv2 (411 651); the flagship's
+    601 475 follows from the same GATConv layout plus its tail."""
+    import hicgat
+    want = REF_PARAM_COUNTS[name]
+    fx = golden(f"model_{name}.npz")
+    ref_count = sum(int(np.prod(fx[k].shape)) for k in fx if k.startswith("grad::"))
+    assert ref_count == want
+    # lin_r is in the state_dict (PyG 1.7.2 keys) but is the same tensor as lin_l
+    assert np.array_equal(fx["state::conv.lin_l.weight"], fx["state::conv.lin_r.weight"])
+    torch.manual_seed(0)
+    mine = getattr(hicgat, name)()
+    torch.manual_seed(0)
+    ora = getattr(gat, name)()
+    for m in (mine, ora):
+        assert sum(p.numel() for p in m.parameters()) == want, type(m)
+        conv = m.conv
+        assert conv.lin_r.weight is conv.lin_l.weight and getattr(conv.lin_l, "bias", None) is None
+        assert tuple(conv.att_l.shape) == tuple(conv.att_r.shape) == (1, 2, 256) and tuple(conv.bias.shape) == (512,)
+        assert sum(p.numel() for p in conv.parameters()) == GATCONV_512_256_H2
+    tail = {k: v for k, v in mine.state_dict().items() if not k.startswith("conv.")}
+    assert GATCONV_512_256_H2 + sum(v.numel() for v in tail.values()) == want

@@ -20,7 +20,6 @@
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
 #   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
 #   n2vfix       node2vec embeddings of chr19 1 mb, seeds 43 and 42 (fixtures for the oracle collapse check)
-#   margin       relu-kink margins of the xagg forward per graph size (tools/relu_margin.py)
 #   cli          the reference driver's flow (python -m hicgat.train) on chr19 1 mb with GPU node2vec
 #                features, the default conversion sweep, 1000 steps each -> gpurun_out/<tag>_cli/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -120,9 +119,6 @@ np.savetxt('$D/emb_500kb.txt', 0.1 * a['emb2'].astype(np.float64), fmt='%.9g')" 
       (cd hic-gnn_amd && timeout -k 10 500 python -m hicgat.train ../gpurun_out/${T}_cli/GM12878_1mb_chr19_list.txt node2vec \
         --steps 1000 --out ../gpurun_out/${T}_cli/GM12878_1mb_chr19 > ../gpurun_out/${T}_cli/run.log 2>&1); rc=$?
       tail -5 gpurun_out/${T}_cli/run.log; [ $rc -eq 0 ] || exit $rc ;;
-    margin)
-      timeout -k 10 300 python tools/relu_margin.py 300 700 760 777 800 > gpurun_out/${T}_relu_margin.log 2>&1 || exit $?
-      cat gpurun_out/${T}_relu_margin.log | grep '^{' ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
