@@ -346,6 +346,140 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
   }
 }
 
+// ---- own rows, the edge pass with the source-side sum folded in (no slab pass) ----------------------
+// The source side enters the parameters only through g_src^h = sum_j da_src_j^h x_j, and
+// da_src_j = sum over the rank's edges (i, j) of ds_ij, so g_src^h = sum_i sum_j ds_ij^h x_j: the
+// edge pass that forms ds_ij has x_j in registers and adds ds_ij^h x_j into the block's running sum
+// -- no per-edge ds array, no transposed (slab) structure, no second gather.
+// Persistent blocks: logical block b (XCD-aware map) takes own rows [b R / G, (b+1) R / G) in order;
+// per row its dxa (4 KiB) goes to LDS; 16-lane groups take the row's edges g, g + 16, ... (lane t of a
+// group holds float4 t, t + 16, ..., t + 112 of x_j); the two head dots are summed over the group by
+// DPP (sum16), then y^h += ds^h x_j per lane (64 accumulators).  At the end the 16 group sums are
+// added in fixed order (xor 16, xor 32 within a wave, then the 4 waves in order through LDS) into the
+// block's partial row gpart[b][0:1024] (head 0 | head 1); their column sum (a grouped column-sum job,
+// hicgat_param_grads_grouped) is g_src.  With xa2 the row's da_dst is formed as in xagg_edge_kernel.
+template <int CTRL>
+__device__ __forceinline__ float dpp_row(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {   // every lane of a 16-lane DPP row: the row's sum
+  v += dpp_row<0x128>(v);   // row_ror:8
+  v += dpp_row<0x124>(v);   // row_ror:4
+  v += dpp_row<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_row<0xB1>(v);    // quad_perm [1,0,3,2]
+  return v;
+}
+constexpr int kEdgeAccBlocks = 512;   // persistent blocks (partial rows of g_src)
+__global__ __launch_bounds__(256) void xagg_edge_acc_kernel(const int *__restrict__ rowptr,
+                                                            const int *__restrict__ col, int row_begin,
+                                                            int row_end, const float *__restrict__ x,
+                                                            const float *__restrict__ a_src,
+                                                            const float *__restrict__ a_dst,
+                                                            float *__restrict__ row_stats,
+                                                            const float *__restrict__ dxa, float ns,
+                                                            const float *__restrict__ xa2,
+                                                            float *__restrict__ gpart) {
+  __shared__ float4 dl4[256];          // dxa row: head 0 float4s 0..127, head 1 128..255
+  __shared__ float4 wred[3][256];      // waves 1..3: their group sums (float4 q of head h at [h*128 + q])
+  const int lane = lane_id(), wv = wave_in_block();
+  const int g = wv * 4 + (lane >> 4), t = lane & 15;   // 16 groups per block
+  const int rows = row_end - row_begin, G = gridDim.x;
+  const int b = xcd_remap(blockIdx.x, G);
+  const int rb = (int)((int64_t)rows * b / G), re = (int)((int64_t)rows * (b + 1) / G);
+  const float4 *x4 = reinterpret_cast<const float4 *>(x);
+  const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 y0[8], y1[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) y0[c] = y1[c] = z4;
+  for (int r = rb; r < re; ++r) {
+    const int i = row_begin + r;
+    __syncthreads();                                   // the previous row's dl4 readers are done
+    dl4[threadIdx.x] = reinterpret_cast<const float4 *>(dxa)[(size_t)r * 256 + threadIdx.x];
+    __syncthreads();
+    const int beg = rowptr[i], end = rowptr[i + 1];
+    const float2 ad = *reinterpret_cast<const float2 *>(a_dst + 2 * (size_t)i);
+    const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
+    const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
+    const float den0 = ms.z + 1e-16f, den1 = ms.w + 1e-16f;
+    for (int e = beg + g; e < end; e += 16) {           // group-uniform trip count
+      asm volatile("" ::: "memory");   // dxa re-read from LDS every edge: no 128-VGPR copy, more waves
+      const int j = col[e];
+      const float4 *xr = x4 + (size_t)j * 128 + t;
+      float4 xv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) xv[c] = xr[16 * c];
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        s0 += f4_dot(xv[c], dl4[t + 16 * c]);
+        s1 += f4_dot(xv[c], dl4[128 + t + 16 * c]);
+      }
+      s0 = row_sum16(s0);
+      s1 = row_sum16(s1);
+      const float2 sv = as2[j];
+      const float ea = sv.x + ad.x, eb = sv.y + ad.y;
+      const float al0 = expf(lrelu(ea, ns) - ms.x) / den0;
+      const float al1 = expf(lrelu(eb, ns) - ms.y) / den1;
+      const float ds0 = al0 * (ea > 0.f ? 1.f : ns) * (s0 - dl.x);
+      const float ds1 = al1 * (eb > 0.f ? 1.f : ns) * (s1 - dl.y);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        y0[c] = f4_fma(ds0, xv[c], y0[c]);
+        y1[c] = f4_fma(ds1, xv[c], y1[c]);
+      }
+    }
+    if (xa2 && wv == 0) {
+      const float4 *q0 = reinterpret_cast<const float4 *>(xa2) + (size_t)r * 128;                     // head 0
+      const float4 *q1 = reinterpret_cast<const float4 *>(xa2) + ((size_t)2 * rows + r) * 128;         // head 1
+      float v[2] = {f4_dot(dl4[lane], q0[lane]) + f4_dot(dl4[64 + lane], q0[64 + lane]),
+                    f4_dot(dl4[128 + lane], q1[lane]) + f4_dot(dl4[192 + lane], q1[64 + lane])};
+      transpose_reduce<2>(v, lane);
+      const float p0 = readlane_f(v[0], 0), p1 = readlane_f(v[0], 32);
+      if (lane == 0) {
+        const float2 s3 = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 6);
+        *reinterpret_cast<float2 *>(row_stats + 8 * (size_t)i + 6) = make_float2(fmaf(-dl.x, s3.x, p0), fmaf(-dl.y, s3.y, p1));
+      }
+    }
+  }
+  // the 4 groups of a wave (its 4 DPP rows), lanes t of rows 0..3: (0 + 1) + (2 + 3)
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float *a = reinterpret_cast<float *>(&y0[c]), *bq = reinterpret_cast<float *>(&y1[c]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] += __shfl_xor(a[k], 16);
+      a[k] += __shfl_xor(a[k], 32);
+      bq[k] += __shfl_xor(bq[k], 16);
+      bq[k] += __shfl_xor(bq[k], 32);
+    }
+  }
+  __syncthreads();
+  if (wv > 0 && lane < 16) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      wred[wv - 1][t + 16 * c] = y0[c];
+      wred[wv - 1][128 + t + 16 * c] = y1[c];
+    }
+  }
+  __syncthreads();
+  if (wv == 0 && lane < 16) {
+    float4 *o = reinterpret_cast<float4 *>(gpart) + (size_t)blockIdx.x * 256;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float4 a = y0[c], bq = y1[c];
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        const float4 u = wred[w][t + 16 * c], v = wred[w][128 + t + 16 * c];
+        a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+        bq.x += v.x; bq.y += v.y; bq.z += v.z; bq.w += v.w;
+      }
+      o[t + 16 * c] = a;
+      o[128 + t + 16 * c] = bq;
+    }
+  }
+}
+
 // ---- every row j: da_src_j = sum over the slab entries (j, i) of ds at the rank's edge (i, j), and
 // g_src^h += da_src_j^h x_j: persistent waves, each taking 4 rows at a time (rows 4w .. 4w + 3, then
 // + 4W): 16-lane group q sums row 4w + q's entries (float2, 4 xor-shuffle steps), then the four x_j
@@ -536,6 +670,22 @@ extern "C" int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N
   if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !ds) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_edge_kernel, dim3(row_end - row_begin), dim3(256), 0, (hipStream_t)stream, rowptr,
                      col, row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, ds, xa2);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_edge_acc_blocks(void) { return kEdgeAccBlocks; }
+
+extern "C" int hicgat_xagg_edge_acc(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C,
+                                    int row_begin, int row_end, const float *x, const float *a_src,
+                                    const float *a_dst, float *row_stats, const float *dxa, const float *xa2,
+                                    float neg_slope, float *gpart, hicgat_stream_t stream) {
+  if (N < 0 || row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !gpart) return HICGAT_EINVAL;
+  // rows == 0 still writes the (zero) partial rows: the column sum that follows reads all of them
+  hipLaunchKernelGGL(xagg_edge_acc_kernel, dim3(kEdgeAccBlocks), dim3(256), 0, (hipStream_t)stream, rowptr, col,
+                     row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, xa2, gpart);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

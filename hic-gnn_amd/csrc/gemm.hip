@@ -16,6 +16,7 @@
 // K-step is prefetched into registers under the current step's MFMAs.  K can be split over
 // gridDim.z: each split writes an fp32 partial slab and a second kernel adds the slabs in split
 // order (deterministic, no float atomics; reduce.hip).
+#include <algorithm>
 #include <cstdlib>
 
 #include "reduce.hpp"
@@ -43,13 +44,14 @@ template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB, bool CS = fal
 #ifndef HICGAT_GEMM_OCC128
 #define HICGAT_GEMM_OCC128 1   // the same for the 128 x 128 tile (A/B builds)
 #endif
-__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64
-                                  : (BM == 128 && BN == 128 && VEC) ? HICGAT_GEMM_OCC128 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
-                                                   const float *__restrict__ B, int64_t ldb,
-                                                   float *__restrict__ C, int64_t ldc, int M, int N,
-                                                   int K, int kchunk, const float *__restrict__ bias,
-                                                   float *__restrict__ slab, int64_t slab_stride, int accumulate,
-                                                   float *__restrict__ csum) {
+// One BM x BN output tile (block coordinates bx, by, split bz) of the kernel below; also the body of
+// the grouped weight-gradient kernel (several GEMMs in one launch).
+__device__ __forceinline__ void gemm_tile(const float *__restrict__ A, int64_t lda,
+                                          const float *__restrict__ B, int64_t ldb,
+                                          float *__restrict__ C, int64_t ldc, int M, int N,
+                                          int K, int kchunk, const float *__restrict__ bias,
+                                          float *__restrict__ slab, int64_t slab_stride, int accumulate,
+                                          float *__restrict__ csum, int bx, int by, int bz) {
   static_assert(!CS || A_KM, "column sums of A need the K-major (weight-gradient) layout");
   constexpr int WM = BM / 2, WN = BN / 2;        // wave tile (4 waves in 2 x 2)
   constexpr int TM = WM / 32, TN = WN / 32;      // 32x32 MFMA tiles per wave
@@ -64,8 +66,8 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
   __shared__ __attribute__((aligned(16))) float Bs[NB][GK][BN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  const int m0 = bx * BM, n0 = by * BN;
+  const int kb = bz * kchunk, ke = min(K, kb + kchunk);
 
   float ra[AE][W], rb[BE][W];
   // piece p of a tile: K-major operands walk the contiguous m (n) dim first, the others the
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
     }
   };
   // CS: thread t < BM adds column t of every staged A tile, k in order (deterministic)
-  const bool cs_on = CS && blockIdx.y == 0 && tid < BM;
+  const bool cs_on = CS && csum != nullptr && by == 0 && tid < BM;
   float cs = 0.f;
   auto colacc = [&](int cb) {
     if (cs_on) {
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
   }
   if (cs_on && m0 + tid < M) {
     if (slab) {
-      csum[(size_t)blockIdx.z * slab_stride + tid + m0] = cs;      // csum = this launch's slab + M*N
+      csum[(size_t)bz * slab_stride + tid + m0] = cs;      // csum = this launch's slab + M*N
     } else {
       float *o = csum + m0 + tid;
       *o = cs + (accumulate ? *o : 0.f);
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
   }
 
   // C/D map of a 32x32 f32 tile: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float *out = slab ? slab + (size_t)blockIdx.z * slab_stride : C;
+  float *out = slab ? slab + (size_t)bz * slab_stride : C;
   const int64_t ldo = slab ? N : ldc;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
@@ -217,6 +219,18 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
       }
     }
   }
+}
+
+template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB, bool CS = false>
+__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64
+                                  : (BM == 128 && BN == 128 && VEC) ? HICGAT_GEMM_OCC128 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
+                                                   const float *__restrict__ B, int64_t ldb,
+                                                   float *__restrict__ C, int64_t ldc, int M, int N,
+                                                   int K, int kchunk, const float *__restrict__ bias,
+                                                   float *__restrict__ slab, int64_t slab_stride, int accumulate,
+                                                   float *__restrict__ csum) {
+  gemm_tile<BM, BN, A_KM, B_KM, VEC, DB, CS>(A, lda, B, ldb, C, ldc, M, N, K, kchunk, bias, slab, slab_stride, accumulate,
+                                             csum, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // ---- "x3": the same GEMM on the bf16 matrix cores by an exact three-way operand split ------------
@@ -575,9 +589,219 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
   return launch<64, 64, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
 }
 
+// ---- grouped parameter gradients (hicgat_param_grads_grouped) -------------------------------------
+// Launch 1: the 128 x 128 weight-gradient tiles of every job (K-major dY and X, db from the staged dY
+// of the first column tile: gemm_tile's CS path) -- workgroup b finds its job by the prefix of
+// workgroup counts, then (tile row, tile column, K chunk).  One K-chunk depth for all jobs, so every
+// workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
+// takes the scalar-staged path of the same tile in the same launch.
+constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
+struct WJob {
+  const float *dy;
+  const float *x;
+  float *dw;
+  float *db;
+  float *slab;        // [splits][M*N + M] partials, or null (splits == 1: straight into dw / db)
+  int64_t ldy, ldx, lddw;
+  int M, N, K, kchunk, tm, tn, wg0, accumulate, vec;
+};
+struct WJobs {
+  WJob j[kMaxWJobs];
+  int n;
+};
+__global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(const WJobs jobs) {
+  int q = 0;
+  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].wg0) ++q;   // block-uniform scalar scan
+  const WJob &J = jobs.j[q];
+  const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
+  const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
+  const int64_t stride = (int64_t)J.M * J.N + J.M;
+  float *cs = J.db ? (J.slab ? J.slab + (int64_t)J.M * J.N : J.db) : nullptr;
+  if (J.vec)
+    gemm_tile<kGroupTile, kGroupTile, true, true, true, false, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
+                                                                     J.K, J.kchunk, nullptr, J.slab, stride,
+                                                                     J.accumulate, cs, bx, by, bz);
+  else
+    gemm_tile<kGroupTile, kGroupTile, true, true, false, false, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
+                                                                      J.K, J.kchunk, nullptr, J.slab, stride,
+                                                                      J.accumulate, cs, bx, by, bz);
+}
+
+// Launch 2: column sums dst[c] (+)= sum_{r < rows} src[r * ld + c] of every job -- the slab sums of
+// the split weight gradients first, then the caller's jobs.  A block takes 64 columns (VEC: 64 float4
+// = 256 columns) of one job; its 4 waves sum 4 contiguous row ranges in row order (8 loads in flight
+// per lane), combined in wave order through LDS: one fixed order, bitwise reproducible.
+struct CJob {
+  const float *src;
+  float *dst;
+  int64_t ld, rows, cols;
+  int blk0, accumulate, vec;
+};
+struct CJobs {
+  CJob j[kMaxCJobs];
+  int n;
+};
+__device__ __forceinline__ float4 ld4(const float *p, bool vec, int64_t c, int64_t cols) {
+  if (vec) return *reinterpret_cast<const float4 *>(p);
+  return make_float4(p[0], c + 1 < cols ? p[1] : 0.f, c + 2 < cols ? p[2] : 0.f, c + 3 < cols ? p[3] : 0.f);
+}
+__global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
+  __shared__ float4 red[4][64];
+  int q = 0;
+  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].blk0) ++q;
+  const CJob &J = jobs.j[q];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t c = ((int64_t)(blockIdx.x - J.blk0) * 64 + lane) * 4;   // first of this lane's 4 columns
+  const int64_t r0 = J.rows * g / 4, r1 = J.rows * (g + 1) / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < J.cols) {
+    const bool vec = J.vec;
+    const float *p = J.src + c;
+    int64_t r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(p + (r + u) * J.ld, vec, c, J.cols);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; r < r1; ++r) {
+      const float4 v = ld4(p + r * J.ld, vec, c, J.cols);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[g][lane] = s;
+  __syncthreads();
+  if (g != 0 || c >= J.cols) return;
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    const float4 v = red[w][lane];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float *d = J.dst + c;
+  const float o[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (c + e < J.cols) d[e] = o[e] + (J.accumulate ? d[e] : 0.f);
+}
+
+// The common K-chunk depth: about target_wgs workgroups over the union of the jobs' tiles, a multiple
+// of the 16-deep K-step, at least 128 deep (shorter chunks spend more on the slab traffic than the
+// tiles gain).  Returns per-job splits into `splits`.
+static int group_kchunk(const hicgat_wgrad_job *w, int nw, int target, int *splits) {
+  int64_t tk = 0;
+  for (int i = 0; i < nw; ++i)
+    tk += (int64_t)((w[i].M + kGroupTile - 1) / kGroupTile) * ((w[i].N + kGroupTile - 1) / kGroupTile) * w[i].K;
+  int64_t kc = target > 0 ? (tk + target - 1) / target : tk;
+  kc = std::max<int64_t>(128, (kc + GK - 1) / GK * GK);
+  for (int i = 0; i < nw; ++i) {
+    // a job whose dW is not one contiguous [M, N] block is not split (its slab sum writes contiguous rows)
+    const bool can = w[i].lddw == w[i].N;
+    splits[i] = can ? (int)std::max<int64_t>(1, (w[i].K + kc - 1) / kc) : 1;
+  }
+  return (int)kc;
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
+
+extern "C" size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *w, int nw, int target_wgs) {
+  if (nw <= 0 || nw > kMaxWJobs || !w) return 0;
+  int splits[kMaxWJobs];
+  group_kchunk(w, nw, target_wgs, splits);
+  size_t tot = 0;
+  for (int i = 0; i < nw; ++i)
+    if (splits[i] > 1) tot += (size_t)splits[i] * ((size_t)w[i].M * w[i].N + w[i].M) * sizeof(float);
+  return tot;
+}
+
+extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, int nc,
+                                          int target_wgs, void *workspace, size_t workspace_bytes,
+                                          hicgat_stream_t stream) {
+  if (nw < 0 || nc < 0 || (nw && !w) || (nc && !c)) return HICGAT_EINVAL;
+  if (nw > kMaxWJobs) return HICGAT_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  int splits[kMaxWJobs];
+  const int kc = nw ? group_kchunk(w, nw, target_wgs, splits) : 0;
+  WJobs wj;
+  CJobs cj;
+  wj.n = 0;
+  cj.n = 0;
+  int wg = 0, blk = 0;
+  float *slab = static_cast<float *>(workspace);
+  size_t used = 0;
+  auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc) {
+    if (cols <= 0) return HICGAT_OK;
+    if (cj.n == kMaxCJobs) return HICGAT_EUNSUPPORTED;
+    CJob &J = cj.j[cj.n++];
+    J.src = src;
+    J.dst = dst;
+    J.ld = ld;
+    J.rows = rows;
+    J.cols = cols;
+    J.accumulate = acc;
+    J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
+    J.blk0 = blk;
+    blk += (int)((cols + 255) / 256);
+    return HICGAT_OK;
+  };
+  for (int i = 0; i < nw; ++i) {
+    const hicgat_wgrad_job &a = w[i];
+    if (a.M < 0 || a.N < 0 || a.K < 0 || a.lddw < a.N) return HICGAT_EINVAL;
+    if (a.M == 0 || a.N == 0) continue;
+    if (!a.dy || !a.x || !a.dw) return HICGAT_EINVAL;
+    WJob &J = wj.j[wj.n++];
+    J.dy = a.dy;
+    J.x = a.x;
+    J.dw = a.dw;
+    J.db = a.db;
+    J.ldy = a.ldy;
+    J.ldx = a.ldx;
+    J.lddw = a.lddw;
+    J.M = a.M;
+    J.N = a.N;
+    J.K = a.K;
+    J.kchunk = kc;
+    J.tm = (a.M + kGroupTile - 1) / kGroupTile;
+    J.tn = (a.N + kGroupTile - 1) / kGroupTile;
+    J.accumulate = a.accumulate;
+    J.vec = (a.M % 4 == 0 && a.ldy % 4 == 0 && a.N % 4 == 0 && a.ldx % 4 == 0 &&
+             ((reinterpret_cast<uintptr_t>(a.dy) | reinterpret_cast<uintptr_t>(a.x)) & 15) == 0);
+    const int sp = a.K > 0 ? splits[i] : 1;
+    J.slab = nullptr;
+    if (sp > 1) {
+      const size_t need = (size_t)sp * ((size_t)a.M * a.N + a.M) * sizeof(float);
+      if (!workspace || used + need > workspace_bytes) return HICGAT_EINVAL;
+      J.slab = slab + used / sizeof(float);
+      used += need;
+    }
+    J.wg0 = wg;
+    wg += J.tm * J.tn * sp;
+    if (sp > 1) {
+      const int64_t stride = (int64_t)a.M * a.N + a.M;
+      int rc = add_col(J.slab, stride, sp, (int64_t)a.M * a.N, a.dw, a.accumulate);
+      if (rc != HICGAT_OK) return rc;
+      if (a.db && (rc = add_col(J.slab + (int64_t)a.M * a.N, stride, sp, a.M, a.db, a.accumulate)) != HICGAT_OK)
+        return rc;
+    }
+  }
+  for (int i = 0; i < nc; ++i) {
+    if (c[i].rows < 0 || c[i].cols < 0 || (c[i].cols > 0 && !c[i].dst) || (c[i].rows > 0 && !c[i].src))
+      return HICGAT_EINVAL;
+    const int rc = add_col(c[i].src, c[i].ld, c[i].rows, c[i].cols, c[i].dst, c[i].accumulate);
+    if (rc != HICGAT_OK) return rc;
+  }
+  if (wg > 0) {
+    hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(wg), dim3(256), 0, s, wj);
+    HICGAT_CHECK_LAUNCH();
+  }
+  if (blk > 0) {
+    hipLaunchKernelGGL(colsum_grouped_kernel, dim3(blk), dim3(256), 0, s, cj);
+    HICGAT_CHECK_LAUNCH();
+  }
+  return HICGAT_OK;
+}
 
 extern "C" size_t hicgat_gemm_workspace_bytes(int M, int N, int splits) {
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;

@@ -16,6 +16,20 @@ c_int, c_i64, c_f, c_d, c_sz, c_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_floa
                                      ctypes.c_size_t, ctypes.c_void_p)
 c_u64 = ctypes.c_uint64
 
+
+class WgradJob(ctypes.Structure):
+    """include/hicgat.h hicgat_wgrad_job."""
+    _fields_ = [("dy", c_p), ("ldy", c_i64), ("x", c_p), ("ldx", c_i64), ("dw", c_p), ("lddw", c_i64), ("db", c_p),
+                ("M", c_int), ("N", c_int), ("K", c_int), ("accumulate", c_int)]
+
+
+class ColsumJob(ctypes.Structure):
+    """include/hicgat.h hicgat_colsum_job."""
+    _fields_ = [("src", c_p), ("ld", c_i64), ("rows", c_i64), ("cols", c_i64), ("dst", c_p), ("accumulate", c_int)]
+
+
+c_wjobs, c_cjobs = ctypes.POINTER(WgradJob), ctypes.POINTER(ColsumJob)
+
 # name -> (restype, argtypes); mirrors include/hicgat.h one to one
 SIGNATURES = {
     "hicgat_version": (c_int, []),
@@ -71,6 +85,9 @@ SIGNATURES = {
     "hicgat_xagg_rows_bwd": (c_int, [c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_xagg_edge": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_f, c_p, c_p]),
+    "hicgat_xagg_edge_acc": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p,
+                                     c_p, c_f, c_p, c_p]),
+    "hicgat_xagg_edge_acc_blocks": (c_int, []),
     "hicgat_xagg_slab_workspace_bytes": (c_sz, []),
     "hicgat_xagg_slab_sum": (c_int, [c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
@@ -85,6 +102,8 @@ SIGNATURES = {
     "hicgat_gemm_wgrad": (c_int, [c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_p,
                                   c_sz, c_p]),
     "hicgat_gemm_wgrad_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
+    "hicgat_param_grads_workspace_bytes": (c_sz, [c_wjobs, c_int, c_int]),
+    "hicgat_param_grads_grouped": (c_int, [c_wjobs, c_int, c_cjobs, c_int, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_ln_relu_res_fwd": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_p]),

@@ -299,12 +299,14 @@ class ShardedTrainer:
             self.trow0, self.tcol0 = b0, c0
             self.tband = truth.buf[b0:b1, c0:].contiguous() if b1 > b0 else torch.zeros((1, 4), **f32)
         # ---- graph and node buffers ---------------------------------------------------------------
+        self.slab_nnz = None
         if mode in ("slab", "xagg"):
             rp, cl = plan.own_csr(rank)
             self.rowptr, self.col = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
-            rp, cl = plan.slab_csr(rank)
-            self.rowptr_s, self.col_s = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
-            self.slab_nnz = int(cl.shape[0])
+            if mode == "slab":
+                rp, cl = plan.slab_csr(rank)
+                self.rowptr_s, self.col_s = torch.from_numpy(rp).to(dev), torch.from_numpy(cl).to(dev)
+                self.slab_nnz = int(cl.shape[0])
             self.x = x.to(dev).contiguous().float()          # the embeddings, gathered once (constant)
             rows = N                                          # node buffers in global row order
             self.a0, self.a1 = self.r0, self.r1               # own rows in buffer numbering
@@ -315,14 +317,12 @@ class ShardedTrainer:
             self.a0, self.a1 = self.q0, self.q1
         if mode == "xagg":
             Rl, F = self.local_rows, x.shape[1]
-            self.perm_s = torch.from_numpy(plan.slab_perm(rank)).to(dev)
-            self.x2 = torch.cat([self.x, self.x], 1).contiguous()          # [x | x]: one column sum per head
             self.X4 = torch.zeros((2, 2, Rl, F), **f32)                     # (xa, xa2) per head, own rows
             self.Y0 = torch.zeros((Rl, D), **f32)                           # out (pre-activation + bias)
             self.O = torch.zeros((Rl, D), **f32)                            # relu(out): the tail's input
             self.dout_l = torch.zeros((Rl, D), **f32)
             self.dxa = torch.zeros((Rl, 2 * F), **f32)
-            self.ds = torch.zeros((max(1, self.local_nnz), 2), **f32)
+            self.gpart = torch.zeros((kern.edge_acc_blocks(), 2 * F), **f32)   # g_src partial rows
             self.a_src = torch.zeros((N, self.H), **f32)
             self.a_dst = torch.zeros((N, self.H), **f32)
             self.g_src = torch.zeros(2 * F, **f32)
@@ -336,7 +336,7 @@ class ShardedTrainer:
         # packed rows [dout (D) | row stats (4H)] (the "allgather" form all-gathers them as one buffer)
         self.pack = torch.zeros((rows, D + 4 * self.H), **f32)
         self.dh = torch.zeros((rows, D), **f32)
-        self.da_src = torch.zeros((N if mode == "xagg" else rows, self.H), **f32)
+        self.da_src = torch.zeros((rows, self.H), **f32)
         # row stats; rows this rank does not own stay 0 forever (the slab source pass reads row r's
         # da_dst for every r: 0 there, so only the owner adds da_dst_r * att_dst into dh_r)
         self.rs = torch.zeros((N if mode == "xagg" else rows, 4 * self.H), **f32)
@@ -524,41 +524,29 @@ class ShardedTrainer:
             Y0.add_(bias)
             o, coords_loc, coords = self._tail(Y0)
         # ---- backward -----------------------------------------------------------------------
-        tail_done = None
-        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
+        # every parameter gradient of the step -- the tail's dW / db / LayerNorm sums (collected from
+        # its backward), dW_h += dout^h^T xa^h with dbias^h (the heads' column sums of dout), g_src
+        # (the edge pass's partial rows) and g_dst -- in ONE grouped GEMM launch + ONE grouped
+        # column-sum launch after the edge pass, on this stream: at a P = 8 shard the ~15 separate
+        # launches over side lanes were the critical path (profiles/r03w_simprof_xagg_P8_rank0_timeline.txt)
+        with ops.grouped_param_grads():
             coords_loc.backward(self.dcoords[r0:r1])
-            rs_own = self.rs[r0:r1]
+        rs_own = self.rs[r0:r1]
+        with torch.no_grad():
             K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
             # dxa^hd = dout^hd W_hd
             self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
                                           self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx"))
-            fork = ops.side_mark()   # the tail's queued dW / db launches run beside the passes below
-            # dW_h += dout^h^T xa^h (K = own rows, split) and dbias on side lanes 2 / 3, forked after the
-            # dxa GEMMs so they run beside the edge pass and the slab sum (issued after the slab sum
-            # they were ~60 us of the critical path at P = 8, forked before the dxa GEMMs a captured
-            # step ran them first and delayed the dxa GEMMs by as much, profiles/r03g_* / r03h_simprof_xagg_*);
-            # joined before xagg_param_finish adds into dW
-            with torch.no_grad():
-                for hd in (0, 1):
-                    with ops._side(self.dout_l, self.X4, lane=2 + hd):
-                        K.gemm(1, 1, C, F, Rl, self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0],
-                               self.W.grad[hd * C:(hd + 1) * C], accumulate=True, splits=ops._splits(C, F, Rl),
-                               name="gemm_dw")
-                if self.bias is not None:
-                    with ops._side(self.dout_l, lane=2):
-                        K.colsum(self.dout_l, self.bias.grad, accumulate=True)
-            K.xagg_edge(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
-                        self.ds, xa2=self.X4[:, 1])
-            K.xagg_slab_sum(self.rowptr_s, self.perm_s, self.ds, self.x, self.da_src, self.g_src)
-            ops.side_flush(after=fork, lanes=SIDE_LANES)
-            tail_done = self._side_event()
-            with torch.no_grad():
-                K.param_grad(self.x2[r0:r1], None, None, rs_own, H, out=(None, self.g_dst, None))
-        # after the join: the side lanes' dW_h are in W.grad
-        with torch.no_grad():
+            K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
+                            self.gpart, xa2=self.X4[:, 1])
+            extra = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
+                      None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
+            extra += [("c", self.gpart, self.g_src, False),
+                      ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)]
+            ops.grouped_flush(K, extra)
             K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
                                 self.att_r.grad.view(-1))
-        return coords, tail_done
+        return coords, None
 
     def _step_allgather(self):
         K, D = self.K, self.D

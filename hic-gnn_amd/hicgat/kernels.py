@@ -258,6 +258,20 @@ class HipKernels:
                                                  P(row_stats), P(dxa), P(xa2), float(ns), P(ds), _lib.stream(x.device)),
                        "hicgat_xagg_edge")
 
+    def xagg_edge_acc(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, gpart, xa2=None):
+        """The edge pass with g_src's partial rows (``gpart`` [edge_acc_blocks, 1024]); with ``xa2``
+        also da_dst (row_stats[:, 6:8])."""
+        N, F = x.shape
+        assert dxa.shape == (r1 - r0, 2 * F) and dxa.is_contiguous()
+        assert gpart.shape == (self.edge_acc_blocks(), 2 * F) and gpart.is_contiguous()
+        with _timed("gat_agg_bwd_dst"):
+            _lib.check(self.lib.hicgat_xagg_edge_acc(P(rowptr), P(col), N, F, 2, F // 2, r0, r1, P(x), P(a_src),
+                                                     P(a_dst), P(row_stats), P(dxa), P(xa2), float(ns), P(gpart),
+                                                     _lib.stream(x.device)), "hicgat_xagg_edge_acc")
+
+    def edge_acc_blocks(self):
+        return int(self.lib.hicgat_xagg_edge_acc_blocks())
+
     def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
         """da_src (every row, through the slab) and g_src [2, 512] = sum_j da_src_j x_j."""
         N = da_src.shape[0]
@@ -386,6 +400,30 @@ class HipKernels:
                                                   0 if ws is None else ws.numel(), _lib.stream(dev)),
                        "hicgat_gemm_wgrad")
         return W_out, b_out
+
+    # workgroups of the grouped weight-gradient launch (hicgat_param_grads_grouped): ~2 per CU
+    GROUP_WGS = int(os.environ.get("HICGAT_GROUP_WGS", "512"))
+
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
+        """Every queued parameter gradient of a step in two launches (include/hicgat.h
+        hicgat_param_grads_grouped): ``wjobs`` = [(dy [K, M], x [K, N], dW [M, N], db [M] or None,
+        accumulate)], ``cjobs`` = [(src [rows, cols], dst [cols], accumulate)]."""
+        target = self.GROUP_WGS if target_wgs is None else target_wgs
+        W = (_lib.WgradJob * max(1, len(wjobs)))()
+        for k, (dy, x, dw, db, acc) in enumerate(wjobs):
+            assert dy.stride(1) == 1 and x.stride(1) == 1 and dw.stride(1) == 1 and dy.shape[0] == x.shape[0]
+            assert db is None or db.is_contiguous()
+            W[k] = _lib.WgradJob(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), dw.stride(0),
+                                 None if db is None else db.data_ptr(), dy.shape[1], x.shape[1], dy.shape[0], int(acc))
+        C = (_lib.ColsumJob * max(1, len(cjobs)))()
+        for k, (src, dst, acc) in enumerate(cjobs):
+            assert src.dim() == 2 and src.stride(1) == 1 and dst.is_contiguous() and dst.numel() == src.shape[1]
+            C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(), int(acc))
+        dev = (wjobs[0][0] if wjobs else cjobs[0][0]).device
+        ws = _lib.workspace(self.lib.hicgat_param_grads_workspace_bytes(W, len(wjobs), target), dev)
+        with _timed("param_grads_grouped"):
+            _lib.check(self.lib.hicgat_param_grads_grouped(W, len(wjobs), C, len(cjobs), int(target), P(ws), ws.numel(),
+                                                           _lib.stream(dev)), "hicgat_param_grads_grouped")
 
     def colsum(self, A, out, accumulate=False):
         K, N = A.shape

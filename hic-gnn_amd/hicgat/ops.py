@@ -32,7 +32,7 @@ def _sink(p):
 # L2-bound aggregation backward instead of in series with it; in a captured step the fork and join
 # are graph edges.  Only sink-bound gradients (``_sink``) go to the side stream -- a gradient that
 # is returned to autograd is consumed on the backward's stream and must be produced there.
-_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": []}
+_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": [], "grouped": 0, "jobs": []}
 _SIDE_LOCK = threading.Lock()
 OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
 # LayerNorm dgamma/dbeta reductions queued with the deferred side work (1, default: 1.959 / 1.945 vs
@@ -158,6 +158,39 @@ def side_record():
     return evs
 
 
+@contextlib.contextmanager
+def grouped_param_grads():
+    """Inside: the sink-bound parameter gradients that have a job descriptor (every dW / db / LayerNorm
+    sum of the Linear, dual-Linear and fused-tail backward) are collected instead of launched;
+    ``grouped_flush`` then issues ALL of them as two launches (hicgat_param_grads_grouped).  A rank's
+    share of the sharded step is too small for ~15 separate launches: queued over side lanes they
+    were the critical path after the edge pass (profiles/r03w_simprof_xagg_P8_rank0_timeline.txt)."""
+    with _SIDE_LOCK:
+        _SIDE["grouped"] += 1
+    try:
+        yield
+    finally:
+        with _SIDE_LOCK:
+            _SIDE["grouped"] -= 1
+
+
+def grouped_flush(K=None, extra=(), target_wgs=None):
+    """Issue the collected jobs (plus ``extra`` descriptors) on the current stream: one grouped
+    weight-gradient launch and one grouped column-sum launch.  Returns the tensors they read (the
+    caller keeps them alive until the launches are ordered before any reuse)."""
+    with _SIDE_LOCK:
+        jobs, _SIDE["jobs"] = _SIDE["jobs"], []
+    jobs = jobs + [(j, ()) for j in extra]
+    if not jobs:
+        return []
+    K = K if K is not None else kernels.default()
+    # descriptors: ("w", dy, x, dW, db[, accumulate]) / ("c", src, dst[, accumulate]); accumulate defaults on
+    w = [(j[1], j[2], j[3], j[4], j[5] if len(j) > 5 else True) for j, _ in jobs if j[0] == "w"]
+    c = [(j[1], j[2], j[3] if len(j) > 3 else True) for j, _ in jobs if j[0] == "c"]
+    K.param_grads_grouped(w, c, target_wgs)
+    return [t for _, keep in jobs for t in keep]
+
+
 def side_join():
     """Flush the queue, make every stream that forked work onto the side stream wait for it, and
     drop the held inputs.  Always runs the queued launches, even after an exception upstream, so
@@ -193,10 +226,16 @@ def overlapped_param_grads(enabled=None):
 BIG_MAIN = float(os.environ.get("HICGAT_BIG_MAIN", "0"))
 
 
-def _param_launch(fn, *keep, small=False, work=0):
+def _param_launch(fn, *keep, small=False, work=0, job=None):
     """Launch a sink-bound parameter-gradient kernel ``fn()``: now on the current stream when not
     overlapping; queued for ``side_flush`` when deferring (``work``: its size, the issue order);
-    else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join)."""
+    else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join).
+    ``job``: the same work as a descriptor for ``grouped_flush`` -- ("w", dy, x, dW, db) for
+    dW += dy^T x (and db += column sums of dy), ("c", src, dst) for dst += column sums of src."""
+    if _SIDE["grouped"] and job is not None:
+        with _SIDE_LOCK:
+            _SIDE["jobs"].append((job, keep))
+        return
     if not _SIDE["on"] or (BIG_MAIN > 0 and work >= BIG_MAIN):
         fn()
     elif DEFER_DEFAULT:
@@ -394,7 +433,7 @@ def _weight_grad_to(K, p, dy, x):
     g = _sink(p)
     if g is not None:
         _param_launch(lambda: weight_grad(K, dy, x, out=g, accumulate=True), dy, x,
-                      work=dy.shape[0] * dy.shape[1] * x.shape[1])
+                      work=dy.shape[0] * dy.shape[1] * x.shape[1], job=("w", dy, x, g, None))
         return None
     return weight_grad(K, dy, x)
 
@@ -416,7 +455,8 @@ def _wb_grad_to(K, pW, pb, dy, x, need_w=True, need_b=True):
     n = x.shape[1]
     sp = _splits(m, n, rows)
     if gW is not None and (gb is not None or not need_b):
-        _param_launch(lambda: K.wgrad(dy, x, gW, gb, accumulate=True, splits=sp), dy, x, work=rows * m * n)
+        _param_launch(lambda: K.wgrad(dy, x, gW, gb, accumulate=True, splits=sp), dy, x, work=rows * m * n,
+                      job=("w", dy, x, gW, gb))
         return None, None
     if gW is None and (not need_b or _sink(pb) is None):
         dW = torch.empty((m, n), dtype=torch.float32, device=dy.device)
@@ -430,7 +470,7 @@ def _bias_grad_to(K, p, dy):
     """db = column sums of dy into the parameter's sink (returns None) or a new tensor."""
     g = _sink(p)
     if g is not None:
-        _param_launch(lambda: K.colsum(dy, g, accumulate=True), dy, small=True)
+        _param_launch(lambda: K.colsum(dy, g, accumulate=True), dy, small=True, job=("c", dy, g))
         return None
     return K.colsum(dy, torch.empty(dy.shape[1], dtype=torch.float32, device=dy.device))
 
@@ -639,15 +679,18 @@ def _dual_param_grads(K, W1, b1, W2, b2, dY, x):
         # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
         gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
         _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x,
-                      work=M * 2 * w * x.shape[1])
+                      work=M * 2 * w * x.shape[1], job=("w", dY, x, gWj, gbj))
     else:
         if w_pair:
-            _param_launch(lambda: weight_grad(K, dY, x, out=_joined(sW1, sW2), accumulate=True), dY, x)
+            gWj = _joined(sW1, sW2)
+            _param_launch(lambda: weight_grad(K, dY, x, out=gWj, accumulate=True), dY, x,
+                          job=("w", dY, x, gWj, None))
         else:
             dW1 = _weight_grad_to(K, W1, dY[:, :w], x)
             dW2 = _weight_grad_to(K, W2, dY[:, w:], x)
         if b_pair:
-            _param_launch(lambda: K.colsum(dY, _joined(sb1, sb2), accumulate=True), dY, small=True)
+            gbj = _joined(sb1, sb2)
+            _param_launch(lambda: K.colsum(dY, gbj, accumulate=True), dY, small=True, job=("c", dY, gbj))
         else:
             db1 = _bias_grad_to(K, b1, dY[:, :w].contiguous())
             db2 = _bias_grad_to(K, b2, dY[:, w:].contiguous())
@@ -663,7 +706,8 @@ def _ln_param_grads(K, gamma, beta, ws, rows):
     part = ws.view(torch.float32)[:rows * 2 * W].view(rows, 2 * W)
     sg, sb = _sink(gamma), _sink(beta)
     if sg is not None and sb is not None and _adjacent(sg, sb):
-        _param_launch(lambda: K.colsum(part, _joined(sg, sb), accumulate=True), ws, work=rows * 2 * W)
+        gj = _joined(sg, sb)
+        _param_launch(lambda: K.colsum(part, gj, accumulate=True), ws, work=rows * 2 * W, job=("c", part, gj))
         return None, None
     out = K.colsum(part, torch.empty(2 * W, dtype=torch.float32, device=part.device))
     return out[:W], out[W:]

@@ -175,6 +175,16 @@ int hicgat_xagg_rows_bwd(int rows, int D, int act, const float *g, const float *
 int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
                      int row_end, const float *x, const float *a_src, const float *a_dst, float *row_stats,
                      const float *dxa, const float *xa2, float neg_slope, float *ds, hicgat_stream_t stream);
+/* The edge pass with the source side folded in (replaces hicgat_xagg_edge + hicgat_xagg_slab_sum in
+ * the sharded step): g_src^h = sum_j da_src_j^h x_j = sum over the own rows' edges (i, j) of
+ * ds_ij^h x_j, formed in the pass that computes ds_ij; written as hicgat_xagg_edge_acc_blocks()
+ * partial rows gpart [blocks][1024] (head 0 | head 1) whose column sums are g_src (e.g. a
+ * hicgat_param_grads_grouped column-sum job); with xa2, da_dst into row_stats[6:8] as hicgat_xagg_edge.
+ * Deterministic (fixed row-to-block map and summation order). */
+int hicgat_xagg_edge_acc(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
+                         int row_end, const float *x, const float *a_src, const float *a_dst, float *row_stats,
+                         const float *dxa, const float *xa2, float neg_slope, float *gpart, hicgat_stream_t stream);
+int hicgat_xagg_edge_acc_blocks(void);
 size_t hicgat_xagg_slab_workspace_bytes(void);
 int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, const float *x,
                          float *da_src, float *g_src, void *workspace, size_t workspace_bytes,
@@ -340,6 +350,38 @@ int hicgat_gemm_wgrad(int M, int N, int K, const float *dY, int64_t ldy, const f
                       int64_t lddw, float *db, int accumulate, int splits, void *workspace, size_t workspace_bytes,
                       hicgat_stream_t stream);
 size_t hicgat_gemm_wgrad_workspace_bytes(int M, int N, int splits);
+/* ---- grouped parameter gradients (one training step's dW / db / LayerNorm sums in two launches) ----
+ * Replaces the per-Linear autograd weight-gradient calls (the ATen mm of dY^T X and the bias sum
+ * behind every torch.nn.Linear.backward in models.py:637-659, and GATConv lin_l's) when a
+ * step issues all of them at one point (the sharded step, hicgat.dist): the W weight-gradient
+ * jobs dW (+)= dY^T X, db (+)= column sums of dY (db may be NULL; dY [K, M] ld ldy, X [K, N] ld
+ * ldx, dW [M, N] ld lddw) run as ONE launch of 128 x 128 fp32-MFMA tiles over the union of their
+ * tiles, K split into chunks of one common depth (about target_wgs workgroups in all), partials in
+ * fp32 slabs; then ONE launch adds, in fixed order, every job's slabs into dW / db AND the C extra
+ * column-sum jobs dst[c] (+)= sum_{r < rows} src[r * ld + c] (LayerNorm dgamma/dbeta partial rows,
+ * bias sums).  Deterministic (no atomics); at most 16 weight-gradient and 32 column-sum jobs
+ * (HICGAT_EUNSUPPORTED beyond).  Workspace: hicgat_param_grads_workspace_bytes(same jobs). */
+typedef struct hicgat_wgrad_job {
+  const float *dy;
+  int64_t ldy;
+  const float *x;
+  int64_t ldx;
+  float *dw;
+  int64_t lddw;
+  float *db;
+  int M, N, K, accumulate;
+} hicgat_wgrad_job;
+typedef struct hicgat_colsum_job {
+  const float *src;
+  int64_t ld;
+  int64_t rows;
+  int64_t cols;
+  float *dst;
+  int accumulate;
+} hicgat_colsum_job;
+size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *wjobs, int nw, int target_wgs);
+int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
+                               int target_wgs, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 /* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
 int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                   size_t workspace_bytes, hicgat_stream_t stream);

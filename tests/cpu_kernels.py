@@ -249,6 +249,37 @@ class CpuKernels:
             s3 = row_stats[r0:r1, 3 * H:4 * H].double()
             row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
 
+    def edge_acc_blocks(self):
+        return 4
+
+    def xagg_edge_acc(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, gpart, xa2=None):
+        """hicgat_xagg_edge_acc: g_src = sum over the own rows' edges of ds_ij x_j, as partial rows
+        (here all of it in row 0), and da_dst with xa2."""
+        H = 2
+        Fd = x.shape[1]
+        row, ei = _rows(rowptr, r0, r1)
+        j = col.long()[ei]
+        al, lp = self._alpha(a_src, a_dst, row_stats, row, j, ns, H)
+        g = (dxa[row - r0].double().view(-1, H, Fd) * x[j].double().unsqueeze(1)).sum(-1)
+        ds = al * lp * (g - row_stats[row, 2 * H:3 * H].double())
+        gpart.zero_()
+        gpart[0] = (ds.t() @ x[j].double()).reshape(-1).float()
+        if xa2 is not None:
+            dx = dxa.double().view(r1 - r0, H, Fd)
+            q = torch.stack([(dx[:, hd] * xa2[hd].double()).sum(-1) for hd in range(H)], 1)
+            s3 = row_stats[r0:r1, 3 * H:4 * H].double()
+            row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
+
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
+        for dy, x, dw, db, acc in wjobs:
+            r = dy.double().t() @ x.double()
+            dw.copy_((r + dw.double()).float() if acc else r.float())
+            if db is not None:
+                b = dy.double().sum(0)
+                db.copy_((b + db.double()).float() if acc else b.float())
+        for src, dst, acc in cjobs:
+            self.colsum(src, dst, accumulate=acc)
+
     def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
         N = da_src.shape[0]
         j, k = _rows(rowptr_s, 0, N)

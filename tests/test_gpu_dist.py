@@ -66,25 +66,40 @@ def _single_gpu_steps(n, steps=2):
         losses.append(float(loss))
         if k == 0:
             g1, p1 = opt.grad.clone(), opt.flat.clone()
-    return dict(loss=losses, grad1=g1, flat1=p1, model=model, opt=opt, masks=masks, kinks=counts)
+    return dict(loss=losses, grad1=g1, flat1=p1, model=model, opt=opt, masks=masks, kinks=counts,
+                inputs=(x, adj, truth))
+
+
+def _loss_at(ref, flat):
+    """The single-GPU loss (forward + fused loss, no update) at the flat parameters ``flat``."""
+    x, adj, truth = ref["inputs"]
+    with torch.no_grad():
+        ref["opt"].flat.copy_(flat.to(ref["opt"].flat.device))
+        loss, _, _ = ref["model"].loss(x, adj, truth, "mse")
+    return float(loss)
 
 
 def _assert_step_matches(ref, res, loss_tol=1e-5, grad_tol=1e-4, label=""):
     """The kink-aware comparison (tests/kinks.py) of a sharded / other-form run ``res`` (rank 0's
-    saved losses, step-1 gradient and parameters) against the single-GPU ``ref``: loss to
-    ``loss_tol`` relative at both steps, every gradient to ``grad_tol`` of its max outside the
-    kink-decided entries, dense3.bias (exactly 0 in exact arithmetic: translation invariance) to
-    1e-3 of the largest gradient, and the step-1 Adam update wherever it is not sensitive to the
-    gradient's rounding (|g| above 1e-3 of its tensor's max and above 1e-6, unmasked: the update
-    is then lr sign(g) to fp32 rounding)."""
+    saved losses, step-1 gradient and parameters) against the single-GPU ``ref``: step-1 loss to
+    ``loss_tol`` relative, every gradient to ``grad_tol`` of its max outside the kink-decided
+    entries, dense3.bias (exactly 0 in exact arithmetic: translation invariance) to 1e-3 of the
+    largest gradient, and the step-1 Adam update wherever it is not sensitive to the gradient's
+    rounding (|g| above 1e-3 of its tensor's max and above 1e-6, unmasked: the update is then
+    lr sign(g) to fp32 rounding).  Step 2: Adam's first update is lr sign(g), so every entry whose
+    gradient is at rounding level (and every kink-decided one) takes a +-lr step of either sign in
+    the two runs -- measured 1.1-1.3e-5 relative on the step-2 loss at synth-20000 P = 2 and n = 3000
+    (gpurun_out/r04a_pytest_gpu.log).  So step 2 is checked teacher-forced: the single-GPU forward
+    at the run's OWN step-1 parameters must give its step-2 loss to ``loss_tol``, and the free
+    step-2 losses must agree to 1e-4."""
     from kinks import compare_flat
     model, opt, masks = ref["model"], ref["opt"], ref["masks"]
     g_ref, g = ref["grad1"], res["grad1"].to(ref["grad1"].device)
     per = compare_flat(model, zip(opt.params, opt.offsets), g_ref, g, masks)
     print(label, f"loss {ref['loss']} vs {res['loss']}; kinks {ref['kinks']};",
           {k: f"{d:.1e}/{m:.1e} ({c} masked)" for k, (d, m, c) in per.items()})
-    for k in range(min(len(ref["loss"]), len(res["loss"]))):
-        assert abs(res["loss"][k] - ref["loss"][k]) <= loss_tol * abs(ref["loss"][k]), (k, res["loss"], ref["loss"])
+    assert abs(res["loss"][0] - ref["loss"][0]) <= loss_tol * abs(ref["loss"][0]), (res["loss"], ref["loss"])
+    assert abs(res["loss"][1] - ref["loss"][1]) <= 1e-4 * abs(ref["loss"][1]), (res["loss"], ref["loss"])
     for name, (d, m, _) in per.items():
         assert d <= grad_tol * m, (label, name, d, m)
     names = {id(p): n for n, p in model.named_parameters()}
@@ -100,6 +115,9 @@ def _assert_step_matches(ref, res, loss_tol=1e-5, grad_tol=1e-4, label=""):
         if sig.any():
             dp = (ref["flat1"][sl].view(p.shape) - res["flat1"][sl].view(p.shape).to(gr.device)).abs()
             assert float(dp[sig].max()) < 1e-6, (label, name, float(dp[sig].max()))
+    l2 = _loss_at(ref, res["flat1"])          # teacher-forced step 2 (the ref model's state is spent)
+    print(label, f"step-2 loss at the run's own step-1 parameters: single GPU {l2:.9g} vs run {res['loss'][1]:.9g}")
+    assert abs(res["loss"][1] - l2) <= loss_tol * abs(l2), (res["loss"][1], l2)
 
 
 def _graph_worker(rank, world, port, n, out, mode):
@@ -254,7 +272,7 @@ def test_simulated_ranks_run_their_shares(mode, n, world):
         torch.cuda.synchronize()
         assert torch.isfinite(loss).item()
         tot["nnz"] += tr.local_nnz
-        tot["slab"] += tr.slab_nnz
+        tot["slab"] += tr.slab_nnz if mode == "slab" else tr.local_nnz    # the xagg form has no slab pass
         tot["tiles"] += tr.t1 - tr.t0
         tot["srows"] += tr.s1 - tr.s0
     assert tot["nnz"] == tot["slab"] == adj.device_nnz

@@ -80,7 +80,13 @@ def test_xagg_kernels_match_float64_reference(case):
         out[name].update(dout=dout.clone(), rs_rows=rs[r0:r1].clone())
         dxa = torch.randn((rows, 1024), generator=gen).to(loc)
         ds = torch.zeros((d["nnz"], 2), device=loc)
+        rs_pre = rs.clone()
         kern.xagg_edge(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs, dxa, 0.2, ds, xa2=X4[:, 1])
+        # the edge pass with g_src folded in (the sharded step's form): g_src = column sums of its
+        # partial rows, da_dst as above
+        gpart = torch.zeros((kern.edge_acc_blocks(), 1024), device=loc)
+        kern.xagg_edge_acc(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs_pre, dxa, 0.2, gpart, xa2=X4[:, 1])
+        out[name].update(g_src_acc=gpart.double().sum(0), rs_edge_acc=rs_pre[r0:r1].clone())
         da_src = torch.zeros((n, 2), device=loc)
         g_src = torch.zeros(1024, device=loc)
         kern.xagg_slab_sum(t["srp"], t["perm"], ds, t["x"], da_src, g_src)
@@ -98,7 +104,8 @@ def test_xagg_kernels_match_float64_reference(case):
         out[name].update(y0=y0, o=o)
     g, r = out["gpu"], out["ref"]
     errs = {k: _rel(g[k], r[k]) for k in ("a_src", "a_dst", "X4", "dout", "rs_rows", "ds", "da_src", "g_src",
-                                           "rs_edge", "dW", "dl", "dr", "y0", "o")}
+                                           "rs_edge", "dW", "dl", "dr", "y0", "o", "g_src_acc", "rs_edge_acc")}
+    errs["g_src_acc_vs_slab"] = _rel(g["g_src_acc"], r["g_src"])
     errs["rs_stats"] = _rel(g["rs"][d["r0"]:d["r1"], :4], r["rs"][d["r0"]:d["r1"], :4])
     errs["rs_s3"] = _rel(g["rs"][d["r0"]:d["r1"], 4:6], r["rs"][d["r0"]:d["r1"], 4:6])
     print({k: f"{v:.1e}" for k, v in errs.items()})
@@ -145,3 +152,56 @@ def test_xagg_gemm_calls_match_float64(shape):
     err = _rel(got, ref)
     print(shape, f"{err:.2e}")
     assert err < 1e-5
+
+
+@pytest.mark.parametrize("target", [64, 512])
+def test_param_grads_grouped_matches_float64(target):
+    """hicgat_param_grads_grouped (the sharded step's one-launch parameter gradients) against
+    float64 torch: weight-gradient jobs of the step's shapes -- a 512 x 512 dual-Linear pair with
+    its bias, the two per-head 256 x 512 blocks of lin_l (row views of one [512, 512] gradient) with
+    their bias halves, dense3's 3 x 64 (scalar-staged tile), g_dst's 2 x 512 from a strided [R, 8]
+    row-stats view (overwrite) -- and column-sum jobs (LayerNorm partial rows into an adjacent
+    [dgamma | dbeta], a [blocks, 1024] partial-row sum that overwrites); ``target`` = the workgroup
+    budget (64: few K chunks, 512: many).  Then the same call again must give the same bits."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hicgat
+    K = hicgat.kernels.default()
+    g = torch.Generator().manual_seed(9)
+    R = 2517
+
+    def rnd(*shape):
+        return torch.randn(shape, generator=g).cuda()
+
+    x, dY, dout, z3, dc, rs = rnd(R, 512), rnd(R, 512), rnd(R, 512), rnd(R, 64), rnd(R, 3), rnd(R, 8)
+    Wg, bg, W3g, b3g = rnd(512, 512), rnd(512), rnd(3, 64), rnd(3)
+    Wl, bl = rnd(512, 512), rnd(512)
+    gdst = rnd(2, 512)
+    lnp, lng = rnd(633, 512), rnd(512)
+    gp, gs = rnd(512, 1024), rnd(1024)
+    ref = {"Wg": Wg.double() + dY.double().t() @ x.double(), "bg": bg.double() + dY.double().sum(0),
+           "W3g": W3g.double() + dc.double().t() @ z3.double(), "b3g": b3g.double() + dc.double().sum(0),
+           "gdst": rs[:, 6:8].double().t() @ x.double(), "lng": lng.double() + lnp.double().sum(0),
+           "gs": gp.double().sum(0)}
+    Wl_ref, bl_ref = Wl.double().clone(), bl.double().clone()
+    for hd in range(2):
+        sl = slice(hd * 256, (hd + 1) * 256)
+        Wl_ref[sl] += dout[:, sl].double().t() @ x.double()
+        bl_ref[sl] += dout[:, sl].double().sum(0)
+    ref.update(Wl=Wl_ref, bl=bl_ref)
+    outs = {"Wg": Wg, "bg": bg, "W3g": W3g, "b3g": b3g, "gdst": gdst, "lng": lng, "gs": gs, "Wl": Wl, "bl": bl}
+    init = {k: v.clone() for k, v in outs.items()}
+    res = []
+    for rep in range(2):
+        for k in outs:
+            outs[k].copy_(init[k])
+        w = [(dY, x, Wg, bg, True), (dc, z3, W3g, b3g, True), (rs[:, 6:8], x, gdst, None, False)]
+        w += [(dout[:, hd * 256:(hd + 1) * 256], x, Wl[hd * 256:(hd + 1) * 256], bl[hd * 256:(hd + 1) * 256], True)
+              for hd in range(2)]
+        K.param_grads_grouped(w, [(lnp, lng, True), (gp, gs, False)], target_wgs=target)
+        torch.cuda.synchronize()
+        res.append({k: v.clone() for k, v in outs.items()})
+    errs = {k: _rel(res[0][k], ref[k]) for k in ref}
+    print(target, {k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < 1e-5 for v in errs.values()), errs
+    assert all(torch.equal(res[0][k], res[1][k]) for k in outs)
