@@ -596,6 +596,9 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
+#ifndef HICGAT_GROUP_DB
+#define HICGAT_GROUP_DB 0   // 1: double-buffered LDS in the grouped weight-gradient tiles (A/B builds)
+#endif
 struct WJob {
   const float *dy;
   const float *x;
@@ -618,7 +621,7 @@ __global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(
   const int64_t stride = (int64_t)J.M * J.N + J.M;
   float *cs = J.db ? (J.slab ? J.slab + (int64_t)J.M * J.N : J.db) : nullptr;
   if (J.vec)
-    gemm_tile<kGroupTile, kGroupTile, true, true, true, false, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
+    gemm_tile<kGroupTile, kGroupTile, true, true, true, HICGAT_GROUP_DB, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
                                                                      J.K, J.kchunk, nullptr, J.slab, stride,
                                                                      J.accumulate, cs, bx, by, bz);
   else
@@ -634,8 +637,9 @@ __global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(
 struct CJob {
   const float *src;
   float *dst;
-  int64_t ld, rows, cols;
-  int blk0, accumulate, vec;
+  const float *wt;    // optional row weights (stride ldw)
+  int64_t ld, rows, cols, ldw;
+  int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (6: 4 groups ... 2: 64 groups)
 };
 struct CJobs {
   CJob j[kMaxCJobs];
@@ -646,36 +650,56 @@ __device__ __forceinline__ float4 ld4(const float *p, bool vec, int64_t c, int64
   return make_float4(p[0], c + 1 < cols ? p[1] : 0.f, c + 2 < cols ? p[2] : 0.f, c + 3 < cols ? p[3] : 0.f);
 }
 __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
-  __shared__ float4 red[4][64];
+  __shared__ float4 red[256];
   int q = 0;
   while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].blk0) ++q;
   const CJob &J = jobs.j[q];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t c = ((int64_t)(blockIdx.x - J.blk0) * 64 + lane) * 4;   // first of this lane's 4 columns
-  const int64_t r0 = J.rows * g / 4, r1 = J.rows * (g + 1) / 4;
+  // a job of many rows (LayerNorm partial rows, g_src's partial rows) takes 16 or 64 row groups of
+  // 16 / 4 lanes per block, a short one (split-K slabs) 4 groups of 64 lanes: the in-order chain of
+  // one lane stays short either way
+  const int L = 1 << J.lg, ng = 256 >> J.lg;
+  const int lane = threadIdx.x & (L - 1), g = threadIdx.x >> J.lg;
+  const int64_t c = ((int64_t)(blockIdx.x - J.blk0) * L + lane) * 4;   // first of this lane's 4 columns
+  const int64_t r0 = J.rows * g / ng, r1 = J.rows * (g + 1) / ng;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < J.cols) {
     const bool vec = J.vec;
     const float *p = J.src + c;
+    const float *w = J.wt;
     int64_t r = r0;
     for (; r + 8 <= r1; r += 8) {
       float4 v[8];
+      float wv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld4(p + (r + u) * J.ld, vec, c, J.cols);
+      for (int u = 0; u < 8; ++u) {
+        v[u] = ld4(p + (r + u) * J.ld, vec, c, J.cols);
+        wv[u] = w ? w[(r + u) * J.ldw] : 1.f;
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+      for (int u = 0; u < 8; ++u) {
+        if (w) {
+          s.x = fmaf(wv[u], v[u].x, s.x); s.y = fmaf(wv[u], v[u].y, s.y);
+          s.z = fmaf(wv[u], v[u].z, s.z); s.w = fmaf(wv[u], v[u].w, s.w);
+        } else {
+          s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+        }
+      }
     }
     for (; r < r1; ++r) {
       const float4 v = ld4(p + r * J.ld, vec, c, J.cols);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      if (w) {
+        const float wr = w[r * J.ldw];
+        s.x = fmaf(wr, v.x, s.x); s.y = fmaf(wr, v.y, s.y); s.z = fmaf(wr, v.z, s.z); s.w = fmaf(wr, v.w, s.w);
+      } else {
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
     }
   }
-  red[g][lane] = s;
+  red[threadIdx.x] = s;
   __syncthreads();
   if (g != 0 || c >= J.cols) return;
-#pragma unroll
-  for (int w = 1; w < 4; ++w) {
-    const float4 v = red[w][lane];
+  for (int k = 1; k < ng; ++k) {     // the row groups in order
+    const float4 v = red[(k << J.lg) + lane];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
   float *d = J.dst + c;
@@ -731,19 +755,24 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
   int wg = 0, blk = 0;
   float *slab = static_cast<float *>(workspace);
   size_t used = 0;
-  auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc) {
+  auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc,
+                     const float *wt = nullptr, int64_t ldw = 0) {
     if (cols <= 0) return HICGAT_OK;
     if (cj.n == kMaxCJobs) return HICGAT_EUNSUPPORTED;
     CJob &J = cj.j[cj.n++];
     J.src = src;
     J.dst = dst;
+    J.wt = wt;
     J.ld = ld;
+    J.ldw = ldw;
     J.rows = rows;
     J.cols = cols;
     J.accumulate = acc;
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : 2;
     J.blk0 = blk;
-    blk += (int)((cols + 255) / 256);
+    const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
+    blk += (int)((cols + per - 1) / per);
     return HICGAT_OK;
   };
   for (int i = 0; i < nw; ++i) {
@@ -789,7 +818,7 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
   for (int i = 0; i < nc; ++i) {
     if (c[i].rows < 0 || c[i].cols < 0 || (c[i].cols > 0 && !c[i].dst) || (c[i].rows > 0 && !c[i].src))
       return HICGAT_EINVAL;
-    const int rc = add_col(c[i].src, c[i].ld, c[i].rows, c[i].cols, c[i].dst, c[i].accumulate);
+    const int rc = add_col(c[i].src, c[i].ld, c[i].rows, c[i].cols, c[i].dst, c[i].accumulate, c[i].wt, c[i].ldw);
     if (rc != HICGAT_OK) return rc;
   }
   if (wg > 0) {

@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
                                                             int64_t ldt, int64_t row0, int64_t col0,
                                                             int nb, int64_t t0,
                                                             float4 *__restrict__ part,
-                                                            double *__restrict__ mom, float bg) {
+                                                            double *__restrict__ mom, float bg,
+                                                            const int *__restrict__ cmap = nullptr) {
   static_assert(!BG || (MODE == MODE_SYM && !VEC), "the background form is the training loss without a T image");
   // one dynamic LDS array: [T tile 128x128 fp32 (VEC only)] -- 64 KiB, 16-B aligned
   extern __shared__ __attribute__((aligned(16))) float tile[];
@@ -284,9 +285,10 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
     const int g = (which ? J : I) * BT + li;
     float x = 0.f, y = 0.f, z = 0.f;
     if (g < N) {
-      x = coords[3 * (size_t)g];
-      y = coords[3 * (size_t)g + 1];
-      z = coords[3 * (size_t)g + 2];
+      const size_t gc = cmap ? (size_t)cmap[g] : (size_t)g;   // cmap: global row -> coords row (sharded step)
+      x = coords[3 * gc];
+      y = coords[3 * gc + 1];
+      z = coords[3 * gc + 2];
     }
     sc[which][li][0] = x;
     sc[which][li][1] = y;
@@ -396,6 +398,8 @@ constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-th
 
 __device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
                                       double *__restrict__ part);
+__device__ void moments_last_block(const double *__restrict__ part, unsigned *__restrict__ ticket, int N,
+                                   int loss_kind, double *__restrict__ stats, float *__restrict__ loss);
 
 // mom != NULL: the last kMomBlocks blocks sum runs of the moment records [m0, m1) (tiles, then the
 // support pass's blocks) into mpart instead (moments_partial_block); blocks [0, row_blocks) reduce
@@ -407,9 +411,13 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
                                                                const double *__restrict__ mom, int64_t m0, int64_t m1,
                                                                int row_blocks, double *__restrict__ mpart,
                                                                const float4 *__restrict__ corr, int corr_r0,
-                                                               int corr_r1, double *__restrict__ dc64) {
+                                                               int corr_r1, double *__restrict__ dc64,
+                                                               unsigned *__restrict__ ticket = nullptr,
+                                                               double *__restrict__ stats = nullptr,
+                                                               float *__restrict__ loss = nullptr, int loss_kind = 0) {
   if (mom && (int)blockIdx.x >= row_blocks) {
     moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
+    if (ticket) moments_last_block(mpart, ticket, N, loss_kind, stats, loss);
     return;
   }
   __shared__ float4 red[kRedGroups][64];
@@ -525,6 +533,32 @@ __device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0
   if (tid < 7) part[blk * 8 + tid] = mred[tid][0];
 }
 
+// The moments' second stage inside the reduce launch (no extra launch): every moment block, after
+// writing its partial, takes a ticket (device-scope atomic after a release fence); the block that
+// draws the last one adds the kMomBlocks partials in block order -- the same order and bits as
+// moments_finalize_kernel -- finalizes, and puts the ticket back to 0 for the next launch.
+__device__ void moments_last_block(const double *__restrict__ part, unsigned *__restrict__ ticket, int N,
+                                   int loss_kind, double *__restrict__ stats, float *__restrict__ loss) {
+  __shared__ int last;
+  __threadfence();                 // this block's partial (threads < 7) before the ticket
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == (unsigned)(kMomBlocks - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();                 // acquire: every other block's partial is visible
+  if (threadIdx.x < 7) {
+    double s = 0.0;
+    for (int b = 0; b < kMomBlocks; ++b)
+      s += __hip_atomic_load(part + b * 8 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stats[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    finalize_stats(N, loss_kind, stats, loss);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__restrict__ part, int N, int loss_kind,
                                                               double *__restrict__ stats, float *__restrict__ loss) {
   if (threadIdx.x < 7) {
@@ -551,20 +585,22 @@ __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__re
                                                                const int32_t *__restrict__ col,
                                                                const float *__restrict__ val,
                                                                const float *__restrict__ diag,
-                                                               float4 *__restrict__ corr, double *__restrict__ mom) {
+                                                               float4 *__restrict__ corr, double *__restrict__ mom,
+                                                               const int *__restrict__ cmap) {
   __shared__ double mred[4][7];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = row_begin + blockIdx.x * 4 + wv;
   float gx = 0.f, gy = 0.f, gz = 0.f;
   double L = 0.0, sdt = 0.0, st = 0.0, stt = 0.0, dg = 0.0;   // the support's moment changes in fp64
   if (i < row_end) {   // wave-uniform
-    const float xi = coords[3 * (size_t)i], yi = coords[3 * (size_t)i + 1], zi = coords[3 * (size_t)i + 2];
+    const size_t ic = cmap ? (size_t)cmap[i] : (size_t)i;
+    const float xi = coords[3 * ic], yi = coords[3 * ic + 1], zi = coords[3 * ic + 2];
     const int e1 = rowptr[i + 1];
     for (int e = rowptr[i] + lane; e < e1; e += 64) {
       const int j = col[e];
+      const size_t jc = cmap ? (size_t)cmap[j] : (size_t)j;
       const float t = val[e];
-      const float dx = xi - coords[3 * (size_t)j], dy = yi - coords[3 * (size_t)j + 1],
-                  dz = zi - coords[3 * (size_t)j + 2];
+      const float dx = xi - coords[3 * jc], dy = yi - coords[3 * jc + 1], dz = zi - coords[3 * jc + 2];
       const float d2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, 0x1.0p-100f)));
       const float inv = __builtin_amdgcn_rsqf(d2);
       const float d = d2 * inv;
@@ -816,13 +852,13 @@ extern "C" size_t hicgat_pairdist_support_workspace_bytes(int N) {
          kMomBlocks * 8 * sizeof(double) + (size_t)N * sizeof(float4) + 256;
 }
 
-extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background,
-                                                       const int32_t *rowptr, const int32_t *col, const float *val,
-                                                       const float *diag, int64_t tile_begin, int64_t tile_end,
-                                                       int support_row_begin, int support_row_end, int loss_kind,
-                                                       double *stats, float *loss, float *dcoords, double *dcoords64,
-                                                       void *workspace, size_t workspace_bytes,
-                                                       hicgat_stream_t stream) {
+extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, const int32_t *cmap, int N,
+                                                          float background, const int32_t *rowptr, const int32_t *col,
+                                                          const float *val, const float *diag, int64_t tile_begin,
+                                                          int64_t tile_end, int support_row_begin, int support_row_end,
+                                                          int loss_kind, double *stats, float *loss, float *dcoords,
+                                                          double *dcoords64, unsigned *ticket, void *workspace,
+                                                          size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !rowptr || !col || !val || !diag || !stats || !workspace) return HICGAT_EINVAL;
@@ -851,32 +887,48 @@ extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int 
   if (nt > 0) {
     if (loss_kind == 1)
       hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(nt), dim3(256), 0, s, coords,
-                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background);
+                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
     else
       hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true>), dim3(nt), dim3(256), 0, s, coords,
-                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background);
+                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
     HICGAT_CHECK_LAUNCH();
   }
   if (sblocks > 0) {
     if (loss_kind == 1)
       hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
                          support_row_begin, support_row_end, rowptr, col, val, diag, corr,
-                         mom + (size_t)tile_end * 8);
+                         mom + (size_t)tile_end * 8, cmap);
     else
       hipLaunchKernelGGL(pairdist_support_kernel<false>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
                          support_row_begin, support_row_end, rowptr, col, val, diag, corr,
-                         mom + (size_t)tile_end * 8);
+                         mom + (size_t)tile_end * 8, cmap);
     HICGAT_CHECK_LAUNCH();
   }
   const float scale = (float)(4.0 / ((double)N * (double)N));
   const int row_blocks = (dcoords || dcoords64) ? (N + 63) / 64 : 0;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
                      (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
-                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64);
+                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64, ticket, stats, loss,
+                     loss_kind);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
-  HICGAT_CHECK_LAUNCH();
+  if (!ticket) {
+    hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
+    HICGAT_CHECK_LAUNCH();
+  }
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background,
+                                                       const int32_t *rowptr, const int32_t *col, const float *val,
+                                                       const float *diag, int64_t tile_begin, int64_t tile_end,
+                                                       int support_row_begin, int support_row_end, int loss_kind,
+                                                       double *stats, float *loss, float *dcoords, double *dcoords64,
+                                                       void *workspace, size_t workspace_bytes,
+                                                       hicgat_stream_t stream) {
+  return hicgat_pairdist_mse_fused_support_range_ex(coords, nullptr, N, background, rowptr, col, val, diag, tile_begin,
+                                                    tile_end, support_row_begin, support_row_end, loss_kind, stats,
+                                                    loss, dcoords, dcoords64, nullptr, workspace, workspace_bytes,
+                                                    stream);
 }
 
 extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background,

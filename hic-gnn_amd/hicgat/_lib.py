@@ -25,7 +25,8 @@ class WgradJob(ctypes.Structure):
 
 class ColsumJob(ctypes.Structure):
     """include/hicgat.h hicgat_colsum_job."""
-    _fields_ = [("src", c_p), ("ld", c_i64), ("rows", c_i64), ("cols", c_i64), ("dst", c_p), ("accumulate", c_int)]
+    _fields_ = [("src", c_p), ("ld", c_i64), ("rows", c_i64), ("cols", c_i64), ("dst", c_p), ("accumulate", c_int),
+                ("wt", c_p), ("ldw", c_i64)]
 
 
 c_wjobs, c_cjobs = ctypes.POINTER(WgradJob), ctypes.POINTER(ColsumJob)
@@ -93,6 +94,9 @@ SIGNATURES = {
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_pairdist_mse_fused_support_range": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64, c_int,
                                                         c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "hicgat_pairdist_mse_fused_support_range_ex": (c_int, [c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64,
+                                                           c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_sz,
+                                                           c_p]),
     "hicgat_truth_support": (c_int, [c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),

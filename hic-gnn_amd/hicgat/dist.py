@@ -282,6 +282,10 @@ class ShardedTrainer:
         self.q1 = self.q0 + self.local_rows
         self.local_nnz = int(plan.nnz[rank])
         self.gidx = torch.from_numpy(plan.gidx).to(dev)
+        self.gidx32 = self.gidx.to(torch.int32)
+        # the loss reads the coordinates straight from the padded all-gather buffer (cmap = gidx) and
+        # finishes its moments inside its reduce launch (a zeroed ticket): the HIP path only
+        self.direct_coords = self.cuda and sf is not None
         conv = model.conv
         self.W, self.att_l, self.att_r, self.bias = conv.lin_l.weight, conv.att_l, conv.att_r, conv.bias
         self.ns = conv.negative_slope
@@ -352,6 +356,7 @@ class ShardedTrainer:
         self.stats = self.red[:12]
         self.dc64 = self.red[12:].view(N, 3)
         self.loss = torch.zeros((), **f32)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.opt = FlatAdam(model.flat_parameters(), lr=lr, kern=kern)
         # gradient buckets: the GATConv's parameters lead the flat buffer (flat_parameters order)
         conv_ids = {id(p) for p in (self.W, self.att_l, self.att_r, self.bias) if p is not None}
@@ -380,7 +385,10 @@ class ShardedTrainer:
         """The loss share, one fp64 all-reduce of [moments | dcoords], the finalised loss; returns
         this rank's rows of dcoords (fp32) for the tail's backward."""
         K, N = self.K, self.N
-        if self.sf is not None:
+        if self.direct_coords:      # coords = the padded all-gather buffer, read through gidx
+            K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
+                                       self.loss, self.dc64, cmap=self.gidx32, ticket=self.ticket)
+        elif self.sf is not None:
             K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
                                        self.loss, self.dc64)
         else:
@@ -399,12 +407,22 @@ class ShardedTrainer:
         if o is None:
             o = self.out[self.a0:self.a1]
         o = o.detach().requires_grad_(True)
-        coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
-        self.coords_buf[self.q0:self.q1].copy_(coords_loc.detach())
+        own = self.coords_buf[self.q0:self.q1]
+        if self.act and self.cuda and ops.fused_tail_ok(self.model, o):
+            coords_loc = ops.fused_tail(self.model, o, coords_out=own)   # written into the all-gather rows
+        else:
+            coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
+            own.copy_(coords_loc.detach())
         self.comm.all_gather_inplace(self.coords_buf, self._own(self.coords_buf))
-        coords = self.coords_buf.index_select(0, self.gidx)
+        # direct: the loss reads the padded buffer through gidx (no reorder launch); the returned
+        # coordinates are then in that layout (``global_coords`` reorders them)
+        coords = self.coords_buf if self.direct_coords else self.coords_buf.index_select(0, self.gidx)
         self._loss(coords)
         return o, coords_loc, coords
+
+    def global_coords(self):
+        """The last step's coordinates [N, 3] in global row order."""
+        return self.coords_buf.index_select(0, self.gidx)
 
     def step(self):
         self.opt.zero_grad()

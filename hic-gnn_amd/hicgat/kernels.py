@@ -319,26 +319,41 @@ class HipKernels:
                 int(kind), P(stats), P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
                 "hicgat_pairdist_mse_fused_band")
 
+    _tickets = {}
+
+    def ticket(self, device):
+        """A zeroed unsigned counter for the fused loss's in-launch moment finalize (one per device
+        and current stream; every launch leaves it 0).  Allocated on first use, outside any capture
+        when the caller warms up eagerly."""
+        key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+        t = self._tickets.get(key)
+        if t is None:
+            t = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=device)
+        return t
+
     def fused_loss_support(self, coords, sf, n, kind, stats, loss, dcoords):
         """The fused loss over a truth in background + support form (``graph.SupportForm``)."""
         ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
         with _timed("pairdist_mse_fused"):
-            _lib.check(self.lib.hicgat_pairdist_mse_fused_support(
-                P(coords), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(kind), P(stats),
-                P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
-                "hicgat_pairdist_mse_fused_support")
+            _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range_ex(
+                P(coords), None, n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), 0, -1, 0,
+                n, int(kind), P(stats), P(loss), P(dcoords), None, P(self.ticket(coords.device)), P(ws), ws.numel(),
+                _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range_ex")
 
-    def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords):
+    def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords, cmap=None,
+                                 ticket=None):
         """A rank's share of the background-form loss: bulk tiles [t0, t1), support rows [s0, s1)
         (partial moments and dcoords; the caller all-reduces them and calls ``loss_finalize``).
-        A float64 ``dcoords`` receives the fp32 gradient values widened (one all-reduce buffer)."""
+        A float64 ``dcoords`` receives the fp32 gradient values widened (one all-reduce buffer);
+        ``cmap`` (int32 [n]): global row -> row of ``coords``; ``ticket``: the in-launch finalize."""
         ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
         d32, d64 = (None, dcoords) if dcoords.dtype == torch.float64 else (dcoords, None)
+        assert cmap is None or (cmap.dtype == torch.int32 and cmap.numel() == n)
         with _timed("pairdist_mse_fused"):
-            _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range(
-                P(coords), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(t0),
-                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ws), ws.numel(),
-                _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range")
+            _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range_ex(
+                P(coords), P(cmap), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(t0),
+                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ticket), P(ws), ws.numel(),
+                _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range_ex")
 
     def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None):
         """mse / r / alpha / total from the (all-reduced) moments; with ``dc64`` also dcoords[r0:r1] =
@@ -403,12 +418,25 @@ class HipKernels:
 
     # workgroups of the grouped weight-gradient launch (hicgat_param_grads_grouped): ~2 per CU
     GROUP_WGS = int(os.environ.get("HICGAT_GROUP_WGS", "512"))
+    SMALL_M = 16
 
     def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
         """Every queued parameter gradient of a step in two launches (include/hicgat.h
         hicgat_param_grads_grouped): ``wjobs`` = [(dy [K, M], x [K, N], dW [M, N], db [M] or None,
-        accumulate)], ``cjobs`` = [(src [rows, cols], dst [cols], accumulate)]."""
+        accumulate)], ``cjobs`` = [(src [rows, cols], dst [cols], accumulate[, wt [rows] view])].
+        A weight gradient of fewer than ``SMALL_M`` output rows (dense3: 3, g_dst: 2) becomes M
+        weighted column sums (and a plain one for db) instead of a 128 x 128 MFMA tile that would
+        be 97 % padding."""
         target = self.GROUP_WGS if target_wgs is None else target_wgs
+        big, cjobs = [], list(cjobs)
+        for dy, x, dw, db, acc in wjobs:
+            if dy.shape[1] < self.SMALL_M:
+                cjobs += [(x, dw[m], acc, dy[:, m]) for m in range(dy.shape[1])]
+                if db is not None:
+                    cjobs.append((dy, db, acc))
+            else:
+                big.append((dy, x, dw, db, acc))
+        wjobs = big
         W = (_lib.WgradJob * max(1, len(wjobs)))()
         for k, (dy, x, dw, db, acc) in enumerate(wjobs):
             assert dy.stride(1) == 1 and x.stride(1) == 1 and dw.stride(1) == 1 and dy.shape[0] == x.shape[0]
@@ -416,9 +444,13 @@ class HipKernels:
             W[k] = _lib.WgradJob(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), dw.stride(0),
                                  None if db is None else db.data_ptr(), dy.shape[1], x.shape[1], dy.shape[0], int(acc))
         C = (_lib.ColsumJob * max(1, len(cjobs)))()
-        for k, (src, dst, acc) in enumerate(cjobs):
+        for k, job in enumerate(cjobs):
+            src, dst, acc = job[:3]
+            wt = job[3] if len(job) > 3 else None
             assert src.dim() == 2 and src.stride(1) == 1 and dst.is_contiguous() and dst.numel() == src.shape[1]
-            C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(), int(acc))
+            assert wt is None or (wt.dim() == 1 and wt.shape[0] == src.shape[0])
+            C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(), int(acc),
+                                  None if wt is None else wt.data_ptr(), 0 if wt is None else wt.stride(0))
         dev = (wjobs[0][0] if wjobs else cjobs[0][0]).device
         ws = _lib.workspace(self.lib.hicgat_param_grads_workspace_bytes(W, len(wjobs), target), dev)
         with _timed("param_grads_grouped"):
@@ -451,9 +483,10 @@ class HipKernels:
                                                    P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
                                                    _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
 
-    def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps):
+    def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, coords=None):
         """The flagship's MLP tail forward in one launch (tail_fused.hip): returns (coords, saved)
-        with saved = (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)."""
+        with saved = (Y1, st1, z1, Y2, st2, z2, y3, st3, z3); ``coords`` (contiguous [M, 3]): write
+        the output there (e.g. the rank's rows of the sharded step's all-gather buffer)."""
         M = x.shape[0]
         dev = x.device
         f = dict(dtype=torch.float32, device=dev)
@@ -461,7 +494,9 @@ class HipKernels:
         Y2, z2 = torch.empty((M, 256), **f), torch.empty((M, 128), **f)
         y3, z3 = torch.empty((M, 64), **f), torch.empty((M, 64), **f)
         st1, st2, st3 = (torch.empty((M, 2), **f) for _ in range(3))
-        coords = torch.empty((M, 3), **f)
+        if coords is None:
+            coords = torch.empty((M, 3), **f)
+        assert coords.shape == (M, 3) and coords.is_contiguous()
         ws = [W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4]
         assert all(t.is_contiguous() for t in ws) and x.stride(1) == 1
         with _timed("tail_fwd_fused"):

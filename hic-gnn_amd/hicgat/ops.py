@@ -747,14 +747,17 @@ class _FusedTailFn(torch.autograd.Function):
     sums are the per-layer path's."""
 
     @staticmethod
-    def forward(ctx, x, Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3, eps):
+    def forward(ctx, x, Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3, eps,
+                coords_out=None):
         K = kernels.default()
         x = x.contiguous()
         W1c, b1c = _joined(Wa, Wal).contiguous(), _joined(ba, bal).contiguous()
         W2c, b2c = _joined(W1, W1al).contiguous(), _joined(b1, b1al).contiguous()
         coords, saved = K.tail_fwd_fused(x, W1c, b1c, ga.contiguous(), bea.contiguous(), W2c, b2c, g1.contiguous(),
                                          be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
-                                         be2.contiguous(), W3.contiguous(), b3.contiguous(), eps)
+                                         be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out)
+        if coords_out is not None:
+            ctx.mark_dirty(coords_out)      # written in place (a caller's buffer, e.g. the all-gather rows)
         ctx.save_for_backward(x, *saved)
         ctx.params = (Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3)
         return coords
@@ -783,7 +786,7 @@ class _FusedTailFn(torch.autograd.Function):
             dga, dbea = _ln_param_grads(K, ga, bea, ws1, rows)
             dWa, dba, dWal, dbal = _dual_param_grads(K, Wa, ba, Wal, bal, dY1, x)
             return (dx if ctx.needs_input_grad[0] else None, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al,
-                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None)
+                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None, None)
         T = (True,) * 8
 
         def c(**kw):
@@ -799,7 +802,7 @@ class _FusedTailFn(torch.autograd.Function):
                                      saved_tensors=(x, Y1, st1, ga, bea), params=(Wa, ba, Wal, bal, ga, bea))
         dx, dWa, dba, dWal, dbal, dga, dbea, _ = _DualLnReluResFn.backward(ctx1, dz1)
         return (dx, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al, dg1, dbe1, dW2, db2, dg2, dbe2,
-                dW3, db3, None)
+                dW3, db3, None, None)
 
 
 def fused_tail_ok(model, x):
@@ -809,13 +812,14 @@ def fused_tail_ok(model, x):
             and model.norm_a.eps == model.norm1.eps == model.norm2.eps)
 
 
-def fused_tail(model, x):
-    """GATNetSelectiveResidualsUpdated.post_act on the fused forward (``fused_tail_ok`` first)."""
+def fused_tail(model, x, coords_out=None):
+    """GATNetSelectiveResidualsUpdated.post_act on the fused forward (``fused_tail_ok`` first);
+    ``coords_out``: a contiguous [M, 3] buffer the coordinates are written into (and returned)."""
     m = model
     return _FusedTailFn.apply(x, m.densea.weight, m.densea.bias, m.align_densea.weight, m.align_densea.bias,
                               m.norm_a.weight, m.norm_a.bias, m.dense1.weight, m.dense1.bias, m.align_dense1.weight,
                               m.align_dense1.bias, m.norm1.weight, m.norm1.bias, m.dense2.weight, m.dense2.bias,
-                              m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps)
+                              m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps, coords_out)
 
 
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):

@@ -310,6 +310,18 @@ int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float ba
                                             int support_row_end, int loss_kind, double *stats, float *loss,
                                             float *dcoords, double *dcoords64, void *workspace,
                                             size_t workspace_bytes, hicgat_stream_t stream);
+/* The same with two options for the sharded step (NULL = as above): cmap [N] maps global row g to
+ * its row in ``coords`` (the padded [P*R, 3] all-gather buffer, so no reorder launch), and ticket
+ * (a caller-owned unsigned, 0 before the call and left 0 after it) lets the reduce launch finish the
+ * moments itself (its last moment block, by an atomic ticket; same order and bits) -- one launch
+ * fewer. */
+int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, const int32_t *cmap, int N, float background,
+                                               const int32_t *rowptr, const int32_t *col, const float *val,
+                                               const float *diag, int64_t tile_begin, int64_t tile_end,
+                                               int support_row_begin, int support_row_end, int loss_kind,
+                                               double *stats, float *loss, float *dcoords, double *dcoords64,
+                                               unsigned *ticket, void *workspace, size_t workspace_bytes,
+                                               hicgat_stream_t stream);
 /* The background form of a symmetric N x N fp32 truth T (leading dim ldt): the sorted CSR of the
  * off-diagonal entries != background, their values, and the diagonal.  Two calls, as
  * hicgat_csr_from_dense: col == NULL fills rowptr (the counts, scanned); then col / val / diag. */
@@ -358,8 +370,8 @@ size_t hicgat_gemm_wgrad_workspace_bytes(int M, int N, int splits);
  * ldx, dW [M, N] ld lddw) run as ONE launch of 128 x 128 fp32-MFMA tiles over the union of their
  * tiles, K split into chunks of one common depth (about target_wgs workgroups in all), partials in
  * fp32 slabs; then ONE launch adds, in fixed order, every job's slabs into dW / db AND the C extra
- * column-sum jobs dst[c] (+)= sum_{r < rows} src[r * ld + c] (LayerNorm dgamma/dbeta partial rows,
- * bias sums).  Deterministic (no atomics); at most 16 weight-gradient and 32 column-sum jobs
+ * column-sum jobs dst[c] (+)= sum_{r < rows} (wt ? wt[r * ldw] : 1) src[r * ld + c] (LayerNorm
+ * dgamma/dbeta partial rows, bias sums, the rows of a few-row weight gradient).  Deterministic (no atomics); at most 16 weight-gradient and 32 column-sum jobs
  * (HICGAT_EUNSUPPORTED beyond).  Workspace: hicgat_param_grads_workspace_bytes(same jobs). */
 typedef struct hicgat_wgrad_job {
   const float *dy;
@@ -378,6 +390,8 @@ typedef struct hicgat_colsum_job {
   int64_t cols;
   float *dst;
   int accumulate;
+  const float *wt;    /* NULL, or row weights: dst[c] (+)= sum_r wt[r * ldw] src[r * ld + c] (a dW row of a */
+  int64_t ldw;        /* weight gradient with a handful of output rows, e.g. dense3's 3 x 64) */
 } hicgat_colsum_job;
 size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *wjobs, int nw, int target_wgs);
 int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
