@@ -45,8 +45,15 @@ namespace hicgat {
 // [64q, 64q + 64) of column k, the four quarters added in order (32 blocks: the 8-block form with a
 // 256-long chain per thread took 14 us, one launch on every step's critical path) -------------------
 __global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__ W, const float *__restrict__ att_s,
-                                                       const float *__restrict__ att_d, float *__restrict__ v) {
+                                                       const float *__restrict__ att_d, float *__restrict__ v,
+                                                       float *__restrict__ zero_buf, int64_t zero_n) {
   __shared__ float red[4][64];
+  if (zero_buf) {   // the step's flat gradient buffer (zero_grad) rides along: float4 stores, then the tail
+    const int64_t n4 = zero_n / 4, stride = (int64_t)gridDim.x * 256;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) reinterpret_cast<float4 *>(zero_buf)[i] = z;
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < zero_n; i += stride) zero_buf[i] = 0.f;
+  }
   const int which = blockIdx.x >> 3;                 // 0, 1: att_src heads 0, 1; 2, 3: att_dst heads 0, 1
   const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int k = (blockIdx.x & 7) * 64 + kl;
@@ -603,20 +610,28 @@ using namespace hicgat;
 
 extern "C" size_t hicgat_xagg_vec_bytes(void) { return 4 * 512 * sizeof(float); }
 
-extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
-                                  int F, int H, int C, float *vec, float *a_src, float *a_dst,
-                                  hicgat_stream_t stream) {
-  if (N < 0) return HICGAT_EINVAL;
+extern "C" int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst,
+                                       int N, int F, int H, int C, float *vec, float *a_src, float *a_dst,
+                                       float *zero_buf, int64_t zero_n, hicgat_stream_t stream) {
+  if (N < 0 || zero_n < 0) return HICGAT_EINVAL;
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
-  if (!W || !att_src || !att_dst || !vec) return HICGAT_EINVAL;
+  if (!W || !att_src || !att_dst || !vec || (zero_n > 0 && !zero_buf)) return HICGAT_EINVAL;
+  if (zero_buf && (reinterpret_cast<uintptr_t>(zero_buf) & 15)) return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(xagg_vec_kernel, dim3(32), dim3(256), 0, s, W, att_src, att_dst, vec);
+  hipLaunchKernelGGL(xagg_vec_kernel, dim3(32), dim3(256), 0, s, W, att_src, att_dst, vec, zero_n > 0 ? zero_buf : nullptr,
+                     zero_n);
   HICGAT_CHECK_LAUNCH();
   if (N == 0) return HICGAT_OK;
   if (!x || !a_src || !a_dst) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_logits_kernel, dim3((N + 3) / 4), dim3(256), 0, s, x, vec, N, a_src, a_dst);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
+                                  int F, int H, int C, float *vec, float *a_src, float *a_dst,
+                                  hicgat_stream_t stream) {
+  return hicgat_xagg_logits_zero(x, W, att_src, att_dst, N, F, H, C, vec, a_src, a_dst, nullptr, 0, stream);
 }
 
 extern "C" int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,

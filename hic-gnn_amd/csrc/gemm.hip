@@ -726,9 +726,124 @@ static int group_kchunk(const hicgat_wgrad_job *w, int nw, int target, int *spli
   return (int)kc;
 }
 
+// ---- grouped node-row GEMMs (hicgat_gemm_rows_grouped): C_j = A_j op(B_j) for a few jobs of one
+// layout in ONE launch of 64 x 128 tiles, K split in `splits` chunks into fp32 slabs, then ONE launch
+// adds the slabs in split order + bias and (optionally) writes relu of the sum to a second output --
+// the two heads of the sharded step's aggregate-first GATConv (out_h = xa_h W_h^T + b_h, relu) and
+// its dxa_h = dout_h W_h, which were two K-split launches + two slab sums (+ a bias/relu pass) each.
+constexpr int kMaxRJobs = 8;
+struct RJob {
+  const float *a;
+  const float *b;
+  float *c;
+  float *cr;          // relu(C) too (or null)
+  const float *bias;
+  float *slab;        // [splits][M][N]
+  int64_t lda, ldb, ldc, ldr;
+  int M, N, K, kchunk, tm, tn, wg0, blk0;
+};
+struct RJobs {
+  RJob j[kMaxRJobs];
+  int n, splits;
+};
+template <bool B_KM>
+__global__ __launch_bounds__(256, HICGAT_GEMM_OCC64) void gemm_rows_grouped_kernel(const RJobs jobs) {
+  int q = 0;
+  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].wg0) ++q;
+  const RJob &J = jobs.j[q];
+  const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
+  const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
+  gemm_tile<64, 128, false, B_KM, true, !B_KM ? false : true, false>(
+      J.a, J.lda, J.b, J.ldb, J.c, J.ldc, J.M, J.N, J.K, J.kchunk, nullptr, J.slab, (int64_t)J.M * J.N, 0, nullptr,
+      bx, by, bz);
+}
+__global__ __launch_bounds__(256) void rows_reduce_kernel(const RJobs jobs) {
+  int q = 0;
+  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].blk0) ++q;
+  const RJob &J = jobs.j[q];
+  const int64_t e = ((int64_t)(blockIdx.x - J.blk0) * 256 + threadIdx.x) * 4;   // element (row-major M x N)
+  const int64_t MN = (int64_t)J.M * J.N;
+  if (e >= MN) return;
+  const float4 *sl = reinterpret_cast<const float4 *>(J.slab + e);
+  const int64_t st = MN / 4;
+  float4 s = sl[0];
+  for (int z = 1; z < jobs.splits; ++z) {
+    const float4 v = sl[z * st];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const int64_t m = e / J.N, n = e % J.N;     // N % 4 == 0: the 4 elements share a row
+  if (J.bias) {
+    const float4 b = *reinterpret_cast<const float4 *>(J.bias + n);
+    s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+  }
+  *reinterpret_cast<float4 *>(J.c + m * J.ldc + n) = s;
+  if (J.cr) *reinterpret_cast<float4 *>(J.cr + m * J.ldr + n) = f4_relu(s);
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
+
+extern "C" size_t hicgat_gemm_rows_grouped_workspace_bytes(const hicgat_gemm_job *jobs, int n, int splits) {
+  if (n <= 0 || !jobs || splits < 1) return 0;
+  size_t tot = 0;
+  for (int i = 0; i < n; ++i) tot += (size_t)splits * jobs[i].M * jobs[i].N * sizeof(float);
+  return tot;
+}
+
+extern "C" int hicgat_gemm_rows_grouped(const hicgat_gemm_job *jobs, int n, int b_kmajor, int splits, void *workspace,
+                                        size_t workspace_bytes, hicgat_stream_t stream) {
+  if (n < 0 || (n && !jobs) || splits < 1) return HICGAT_EINVAL;
+  if (n > kMaxRJobs) return HICGAT_EUNSUPPORTED;
+  if (n == 0) return HICGAT_OK;
+  if (workspace_bytes < hicgat_gemm_rows_grouped_workspace_bytes(jobs, n, splits) || !workspace) return HICGAT_EINVAL;
+  RJobs rj;
+  rj.n = 0;
+  rj.splits = splits;
+  int wg = 0, blk = 0;
+  float *slab = static_cast<float *>(workspace);
+  for (int i = 0; i < n; ++i) {
+    const hicgat_gemm_job &a = jobs[i];
+    if (a.M <= 0 || a.N <= 0 || a.K <= 0 || !a.a || !a.b || !a.c) return HICGAT_EINVAL;
+    // float4 staging and float4 epilogue: every row a multiple of 4 floats, 16-B aligned
+    const bool ok = a.K % 4 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.N % 4 == 0 && a.ldc % 4 == 0 &&
+                    (!a.c_relu || a.ldr % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) | reinterpret_cast<uintptr_t>(a.c) |
+                      reinterpret_cast<uintptr_t>(a.c_relu) | reinterpret_cast<uintptr_t>(a.bias)) & 15) == 0;
+    if (!ok) return HICGAT_EUNSUPPORTED;
+    RJob &J = rj.j[rj.n++];
+    J.a = a.a;
+    J.b = a.b;
+    J.c = a.c;
+    J.cr = a.c_relu;
+    J.bias = a.bias;
+    J.lda = a.lda;
+    J.ldb = a.ldb;
+    J.ldc = a.ldc;
+    J.ldr = a.ldr;
+    J.M = a.M;
+    J.N = a.N;
+    J.K = a.K;
+    J.kchunk = ((a.K + splits - 1) / splits + GK - 1) / GK * GK;
+    J.tm = (a.M + 63) / 64;
+    J.tn = (a.N + 127) / 128;
+    J.slab = slab;
+    slab += (size_t)splits * a.M * a.N;
+    J.wg0 = wg;
+    wg += J.tm * J.tn * splits;
+    J.blk0 = blk;
+    blk += (int)(((int64_t)a.M * a.N / 4 + 255) / 256);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (b_kmajor)
+    hipLaunchKernelGGL(gemm_rows_grouped_kernel<true>, dim3(wg), dim3(256), 0, s, rj);
+  else
+    hipLaunchKernelGGL(gemm_rows_grouped_kernel<false>, dim3(wg), dim3(256), 0, s, rj);
+  HICGAT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3(blk), dim3(256), 0, s, rj);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
 
 extern "C" size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *w, int nw, int target_wgs) {
   if (nw <= 0 || nw > kMaxWJobs || !w) return 0;

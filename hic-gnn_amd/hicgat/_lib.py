@@ -29,7 +29,13 @@ class ColsumJob(ctypes.Structure):
                 ("wt", c_p), ("ldw", c_i64)]
 
 
-c_wjobs, c_cjobs = ctypes.POINTER(WgradJob), ctypes.POINTER(ColsumJob)
+class GemmJob(ctypes.Structure):
+    """include/hicgat.h hicgat_gemm_job."""
+    _fields_ = [("a", c_p), ("lda", c_i64), ("b", c_p), ("ldb", c_i64), ("c", c_p), ("ldc", c_i64), ("c_relu", c_p),
+                ("ldr", c_i64), ("bias", c_p), ("M", c_int), ("N", c_int), ("K", c_int)]
+
+
+c_wjobs, c_cjobs, c_gjobs = ctypes.POINTER(WgradJob), ctypes.POINTER(ColsumJob), ctypes.POINTER(GemmJob)
 
 # name -> (restype, argtypes); mirrors include/hicgat.h one to one
 SIGNATURES = {
@@ -80,6 +86,8 @@ SIGNATURES = {
     "hicgat_pairdist_support_workspace_bytes": (c_sz, [c_int]),
     "hicgat_xagg_vec_bytes": (c_sz, []),
     "hicgat_xagg_logits": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
+    "hicgat_xagg_logits_zero": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_i64,
+                                        c_p]),
     "hicgat_xagg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_f, c_p, c_p,
                                 c_p]),
     "hicgat_xagg_bias_relu": (c_int, [c_p, c_p, c_p, c_int, c_int, c_p]),
@@ -106,6 +114,8 @@ SIGNATURES = {
     "hicgat_gemm_wgrad": (c_int, [c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_p,
                                   c_sz, c_p]),
     "hicgat_gemm_wgrad_workspace_bytes": (c_sz, [c_int, c_int, c_int]),
+    "hicgat_gemm_rows_grouped_workspace_bytes": (c_sz, [c_gjobs, c_int, c_int]),
+    "hicgat_gemm_rows_grouped": (c_int, [c_gjobs, c_int, c_int, c_int, c_p, c_sz, c_p]),
     "hicgat_param_grads_workspace_bytes": (c_sz, [c_wjobs, c_int, c_int]),
     "hicgat_param_grads_grouped": (c_int, [c_wjobs, c_int, c_cjobs, c_int, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
@@ -127,6 +137,7 @@ SIGNATURES = {
                                       c_int, c_u64, c_int, c_p, c_p, c_p]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
+    "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p, c_p]),
 }
 
 

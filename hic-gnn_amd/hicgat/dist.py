@@ -67,8 +67,6 @@ def resolve_mode(mode, P):
     if mode == "auto":
         return "xagg" if P >= AUTO_XAGG_MIN_P else "slab"
     return mode
-# "xagg": head 1's GEMMs on a second stream beside head 0's (1, default) or both on one stream (0)
-HEAD_STREAM = os.environ.get("HICGAT_HEAD_STREAM", "1") != "0"
 # side streams for the MLP tail's queued parameter-gradient launches in the sharded step
 # (ops.side_flush lanes; 1 = one chain as on a single GPU)
 SIDE_LANES = int(os.environ.get("HICGAT_DIST_SIDE_LANES", "3"))
@@ -365,7 +363,6 @@ class ShardedTrainer:
         cut = (max(ends) + 3) // 4 * 4
         self.grad_split = cut if (firsts and min(firsts) >= cut) else None
         self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
-        self.head_stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
@@ -425,7 +422,10 @@ class ShardedTrainer:
         return self.coords_buf.index_select(0, self.gidx)
 
     def step(self):
-        self.opt.zero_grad()
+        if self.mode == "xagg" and self.cuda:
+            self.opt._reattach()     # the gradient buffer is zeroed by the step's first launch (xagg_logits)
+        else:
+            self.opt.zero_grad()
         self.model.train()
         if self.mode == "slab":
             coords, tail_done = self._step_slab()
@@ -506,20 +506,6 @@ class ShardedTrainer:
                          out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
         return coords, tail_done
 
-    def _heads(self, fn):
-        """``fn(hd)`` for both heads: head 1 on a second stream (the per-head GEMMs on a rank's
-        shard are a quarter of the chip's workgroups each), joined before returning."""
-        if not self.cuda or not HEAD_STREAM:
-            fn(0)
-            fn(1)
-            return
-        main = torch.cuda.current_stream()
-        self.head_stream.wait_stream(main)
-        fn(0)
-        with torch.cuda.stream(self.head_stream):
-            fn(1)
-        main.wait_stream(self.head_stream)
-
     def _step_xagg(self):
         """Aggregate-first GATConv (gat_xagg.hip): x replicated, every GEMM on own rows only."""
         K, D, H = self.K, self.D, self.H
@@ -529,18 +515,16 @@ class ShardedTrainer:
         W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
         bias = self.bias.detach()
         # ---- forward ------------------------------------------------------------------------
-        K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst)
+        K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst, zero=self.opt.grad if self.cuda else None)
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
         Y0 = self.Y0
-        # out (head hd columns) = xa^hd W_hd^T; the forward needs no out2 (da_dst comes from dxa . xa2)
-        self._heads(lambda hd: K.gemm(0, 0, Rl, C, F, self.X4[hd, 0], W[hd * C:(hd + 1) * C],
-                                      Y0[:, hd * C:(hd + 1) * C], name="gemm_fwd"))
-        if self.act:
-            K.xagg_bias_relu(Y0, bias, self.O)
-            o, coords_loc, coords = self._tail(self.O)
-        else:
-            Y0.add_(bias)
-            o, coords_loc, coords = self._tail(Y0)
+        # out (head hd columns) = xa^hd W_hd^T + b^hd (and relu(out) for the tail): both heads in one
+        # grouped launch + one slab sum with the bias / relu epilogue; the forward needs no out2 (da_dst
+        # comes from dxa . xa2)
+        hc = [slice(hd * C, (hd + 1) * C) for hd in (0, 1)]
+        K.gemm_rows_grouped([(self.X4[hd, 0], W[hc[hd]], Y0[:, hc[hd]], bias[hc[hd]],
+                              self.O[:, hc[hd]] if self.act else None) for hd in (0, 1)], b_kmajor=0, name="gemm_fwd")
+        o, coords_loc, coords = self._tail(self.O if self.act else Y0)
         # ---- backward -----------------------------------------------------------------------
         # every parameter gradient of the step -- the tail's dW / db / LayerNorm sums (collected from
         # its backward), dW_h += dout^h^T xa^h with dbias^h (the heads' column sums of dout), g_src
@@ -552,9 +536,9 @@ class ShardedTrainer:
         rs_own = self.rs[r0:r1]
         with torch.no_grad():
             K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
-            # dxa^hd = dout^hd W_hd
-            self._heads(lambda hd: K.gemm(0, 1, Rl, F, C, self.dout_l[:, hd * C:(hd + 1) * C], W[hd * C:(hd + 1) * C],
-                                          self.dxa[:, hd * F:(hd + 1) * F], name="gemm_dx"))
+            # dxa^hd = dout^hd W_hd, both heads in one grouped launch
+            K.gemm_rows_grouped([(self.dout_l[:, hc[hd]], W[hc[hd]], self.dxa[:, hd * F:(hd + 1) * F], None, None)
+                                 for hd in (0, 1)], b_kmajor=1, name="gemm_dx")
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                             self.gpart, xa2=self.X4[:, 1])
             extra = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],

@@ -217,14 +217,17 @@ class HipKernels:
         return datt_l, datt_r, dbias
 
     # -- aggregate-first GATConv (gat_xagg.hip): the multi-GPU "xagg" step (hicgat.dist) ---------------
-    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst):
-        """a_src / a_dst [N, 2] = x . (W_h^T att^h) for every row of x."""
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None):
+        """a_src / a_dst [N, 2] = x . (W_h^T att^h) for every row of x; ``zero``: a contiguous buffer
+        zeroed in the same launch (the step's flat gradient buffer)."""
         N, F = x.shape
         H, C = att_l.shape[-2], att_l.shape[-1]
         vec = _lib.workspace(self.lib.hicgat_xagg_vec_bytes(), x.device)
+        assert zero is None or zero.is_contiguous()
         with _timed("xagg_logits"):
-            _lib.check(self.lib.hicgat_xagg_logits(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src),
-                                                   P(a_dst), _lib.stream(x.device)), "hicgat_xagg_logits")
+            _lib.check(self.lib.hicgat_xagg_logits_zero(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src),
+                                                        P(a_dst), P(zero), 0 if zero is None else zero.numel(),
+                                                        _lib.stream(x.device)), "hicgat_xagg_logits_zero")
 
     def xagg_fwd(self, rowptr, col, r0, r1, x, a_src, a_dst, ns, X4, row_stats):
         """Own rows [r0, r1): X4 [2, 2, r1 - r0, 512] = (xa, xa2) per head; row stats (global rows)."""
@@ -457,6 +460,30 @@ class HipKernels:
             _lib.check(self.lib.hicgat_param_grads_grouped(W, len(wjobs), C, len(cjobs), int(target), P(ws), ws.numel(),
                                                            _lib.stream(dev)), "hicgat_param_grads_grouped")
 
+    def gemm_rows_grouped(self, jobs, b_kmajor, splits=None, name="gemm_grouped"):
+        """include/hicgat.h hicgat_gemm_rows_grouped: ``jobs`` = [(A [M, K], B, C [M, N], bias or None,
+        C_relu or None)], B [N, K] (``b_kmajor`` 0) or [K, N] (1).  ``splits`` None: enough K chunks
+        for ~512 workgroups over all jobs (each chunk >= 128 deep)."""
+        G = (_lib.GemmJob * len(jobs))()
+        wgs = 0
+        for k, (A, B, C, bias, Cr) in enumerate(jobs):
+            M, Kd = A.shape
+            N = C.shape[1]
+            assert A.stride(1) == 1 and B.stride(1) == 1 and C.stride(1) == 1 and C.shape[0] == M
+            assert (B.shape == (N, Kd)) if not b_kmajor else (B.shape == (Kd, N))
+            assert Cr is None or (Cr.shape == C.shape and Cr.stride(1) == 1)
+            G[k] = _lib.GemmJob(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                                None if Cr is None else Cr.data_ptr(), 0 if Cr is None else Cr.stride(0),
+                                None if bias is None else bias.data_ptr(), M, N, Kd)
+            wgs += -(-M // 64) * -(-N // 128)
+        if splits is None:
+            splits = max(1, min(jobs[0][0].shape[1] // 128, -(-512 // max(1, wgs))))
+        dev = jobs[0][2].device
+        ws = _lib.workspace(self.lib.hicgat_gemm_rows_grouped_workspace_bytes(G, len(jobs), splits), dev)
+        with _timed(name):
+            _lib.check(self.lib.hicgat_gemm_rows_grouped(G, len(jobs), int(b_kmajor), int(splits), P(ws), ws.numel(),
+                                                         _lib.stream(dev)), "hicgat_gemm_rows_grouped")
+
     def colsum(self, A, out, accumulate=False):
         K, N = A.shape
         ws = _lib.workspace(self.lib.hicgat_colsum_workspace_bytes(K, N), A.device)
@@ -532,11 +559,13 @@ class HipKernels:
                                                           _lib.stream(ws.device)), "hicgat_ln_relu_res_bwd_params")
 
     # -- a10 --------------------------------------------------------------------------------------
-    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):
+    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr, ticket=None):
+        """``ticket``: a zeroed int32 [1]: the step counter advances inside the Adam launch."""
         with _timed("adam"):
-            _lib.check(self.lib.hicgat_adam_step_table(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
-                                                       float(eps), P(table), table.shape[0], P(step_ctr),
-                                                       _lib.stream(flat.device)), "hicgat_adam_step_table")
+            _lib.check(self.lib.hicgat_adam_step_table_ex(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
+                                                          float(eps), P(table), table.shape[0], P(step_ctr),
+                                                          P(ticket), _lib.stream(flat.device)),
+                       "hicgat_adam_step_table_ex")
 
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):

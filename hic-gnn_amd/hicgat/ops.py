@@ -757,7 +757,11 @@ class _FusedTailFn(torch.autograd.Function):
                                          be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
                                          be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out)
         if coords_out is not None:
-            ctx.mark_dirty(coords_out)      # written in place (a caller's buffer, e.g. the all-gather rows)
+            # the kernel wrote into the caller's buffer (e.g. the all-gather rows); the output is a
+            # fresh tensor object over the same memory, so autograd sees a new output (no view or
+            # in-place bookkeeping on the caller's buffer, which a collective then fills around it)
+            coords = torch.empty(0, dtype=coords_out.dtype, device=coords_out.device).set_(
+                coords_out.untyped_storage(), coords_out.storage_offset(), coords_out.shape, coords_out.stride())
         ctx.save_for_backward(x, *saved)
         ctx.params = (Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3)
         return coords

@@ -166,6 +166,11 @@ int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *col, int N, 
 size_t hicgat_xagg_vec_bytes(void);
 int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N, int F,
                        int H, int C, float *vec, float *a_src, float *a_dst, hicgat_stream_t stream);
+/* hicgat_xagg_logits that also zeroes zero_buf[0, zero_n) (a step's flat gradient buffer: the
+ * optimizer's zero_grad, HiC-GNN_main.py:124) in its first launch -- one launch fewer per step. */
+int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
+                            int F, int H, int C, float *vec, float *a_src, float *a_dst, float *zero_buf,
+                            int64_t zero_n, hicgat_stream_t stream);
 int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
                     int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope, float *X4,
                     float *row_stats, hicgat_stream_t stream);
@@ -396,6 +401,29 @@ typedef struct hicgat_colsum_job {
 size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *wjobs, int nw, int target_wgs);
 int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
                                int target_wgs, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
+/* Grouped node-row GEMMs of one layout: C_j = A_j op(B_j) (+ bias_j), A_j [M, K] row-major (ld lda),
+ * op(B) = B^T (B [N, K], b_kmajor = 0: a Linear / head forward) or B (B [K, N], b_kmajor = 1: an
+ * input gradient), c_relu (NULL or ld ldr): relu of the result too.  ONE launch of 64 x 128 fp32-MFMA
+ * tiles over every job's tiles, K split in `splits` chunks into fp32 slabs; ONE launch adds the slabs
+ * in split order (+ bias, relu copy).  Replaces the per-head GEMM calls (ATen mm of GATConv lin_l,
+ * by linearity per head: hicgat.dist's aggregate-first form).  K, N, every ld a multiple of 4, every
+ * pointer 16-B aligned (else HICGAT_EUNSUPPORTED); at most 8 jobs.
+ * Workspace: hicgat_gemm_rows_grouped_workspace_bytes(same jobs, splits). */
+typedef struct hicgat_gemm_job {
+  const float *a;
+  int64_t lda;
+  const float *b;
+  int64_t ldb;
+  float *c;
+  int64_t ldc;
+  float *c_relu;
+  int64_t ldr;
+  const float *bias;
+  int M, N, K;
+} hicgat_gemm_job;
+size_t hicgat_gemm_rows_grouped_workspace_bytes(const hicgat_gemm_job *jobs, int n, int splits);
+int hicgat_gemm_rows_grouped(const hicgat_gemm_job *jobs, int n, int b_kmajor, int splits, void *workspace,
+                             size_t workspace_bytes, hicgat_stream_t stream);
 /* out[n] = sum_k A[k][n] over K rows (a Linear bias gradient), deterministic two-stage. */
 int hicgat_colsum(const float *A, int64_t lda, int K, int N, float *out, int accumulate, void *workspace,
                   size_t workspace_bytes, hicgat_stream_t stream);
@@ -508,6 +536,11 @@ int hicgat_adam_step(float *param, const float *grad, float *exp_avg, float *exp
 int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                            int64_t n, double beta1, double beta2, double eps, const float *table,
                            int64_t table_len, int64_t *step_counter, hicgat_stream_t stream);
+/* The same with ticket (a caller-owned unsigned, 0 before and after): the step counter is advanced
+ * inside the Adam launch by its last workgroup (an atomic ticket) instead of by a second launch. */
+int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                              int64_t n, double beta1, double beta2, double eps, const float *table,
+                              int64_t table_len, int64_t *step_counter, unsigned *ticket, hicgat_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -179,13 +179,24 @@ class CpuKernels:
         C.copy_(r.float())
         return C
 
+    def gemm_rows_grouped(self, jobs, b_kmajor, splits=None, name="gemm_grouped"):
+        for A, B, C, bias, Cr in jobs:
+            r = A.double() @ (B.double() if b_kmajor else B.double().t())
+            if bias is not None:
+                r = r + bias.double()
+            C.copy_(r.float())
+            if Cr is not None:
+                Cr.copy_(torch.relu(C))
+
     def colsum(self, A, out, accumulate=False):
         r = A.double().sum(0)
         out.copy_((r + out.double()).float() if accumulate else r.float())
         return out
 
     # -- aggregate-first GATConv (gat_xagg.hip) -------------------------------------------------------
-    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst):
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None):
+        if zero is not None:
+            zero.zero_()
         H, C = att_l.shape[-2], att_l.shape[-1]
         Wd = W.double().view(H, C, -1)
         vs = torch.einsum("hc,hck->hk", att_l.double().view(H, C), Wd)
