@@ -26,26 +26,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ p, const 
                                                    float *__restrict__ m, float *__restrict__ v,
                                                    int64_t n, AdamConsts k,
                                                    const float2 *__restrict__ table,
-                                                   int64_t *__restrict__ step_ctr, int64_t table_len,
-                                                   unsigned *__restrict__ ticket) {
+                                                   const int64_t *__restrict__ step_ctr, int64_t table_len) {
   if (table) {  // graph-replayable form: per-step constants from the host-computed table
     int64_t s = *step_ctr;
     if (s >= table_len) s = table_len - 1;
     k.neg_step = table[s].x;
     k.bc2s = table[s].y;
-  }
-  if (ticket) {
-    // the step count advances once every workgroup has read it: the last one to draw a ticket
-    // (each draws after its read) stores step + 1 and puts the ticket back to 0
-    __shared__ int last;
-    __syncthreads();
-    __threadfence();   // the step-count read above is done before this workgroup's ticket
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (last && threadIdx.x == 0) {
-      __hip_atomic_store(step_ctr, *step_ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -98,7 +84,7 @@ extern "C" int hicgat_adam_step(float *param, const float *grad, float *exp_avg,
   const int64_t work = (n + 3) / 4;
   const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                     exp_avg, exp_avg_sq, n, k, nullptr, nullptr, (int64_t)0, nullptr);
+                     exp_avg, exp_avg_sq, n, k, nullptr, nullptr, (int64_t)0);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
@@ -106,14 +92,7 @@ extern "C" int hicgat_adam_step(float *param, const float *grad, float *exp_avg,
 extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                                       int64_t n, double beta1, double beta2, double eps, const float *table,
                                       int64_t table_len, int64_t *step_counter, hicgat_stream_t stream) {
-  return hicgat_adam_step_table_ex(param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, table, table_len,
-                                   step_counter, nullptr, stream);
-}
 
-extern "C" int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
-                                         int64_t n, double beta1, double beta2, double eps, const float *table,
-                                         int64_t table_len, int64_t *step_counter, unsigned *ticket,
-                                         hicgat_stream_t stream) {
   if (n < 0 || table_len < 1) return HICGAT_EINVAL;
   if (!param || !grad || !exp_avg || !exp_avg_sq || !table || !step_counter) return HICGAT_EINVAL;
   const uintptr_t mis = reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
@@ -130,9 +109,8 @@ extern "C" int hicgat_adam_step_table_ex(float *param, const float *grad, float 
     const int64_t work = (n + 3) / 4;
     const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                       exp_avg_sq, n, k, reinterpret_cast<const float2 *>(table), step_counter, table_len, ticket);
+                       exp_avg_sq, n, k, reinterpret_cast<const float2 *>(table), step_counter, table_len);
     HICGAT_CHECK_LAUNCH();
-    if (ticket) return HICGAT_OK;
   }
   hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step_counter);
   HICGAT_CHECK_LAUNCH();

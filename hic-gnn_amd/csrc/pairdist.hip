@@ -63,6 +63,15 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return *reinterpret_cast<double *>(&q);
 }
 
+// Row partials of the background form: each thread's 8-column partial of every row it touches goes
+// to LDS (stride kRowPad float4: 16 lanes of a row-sum read hit distinct banks) and threads 128..255
+// add the 16 per row in tx order at the end, while 0..127 add the column partials -- instead of
+// three 16-lane DPP sums per row inside the pair loop (~20 % of its VALU issue).
+constexpr int kRowPad = 17;
+#ifndef HICGAT_PD_ROWLDS
+#define HICGAT_PD_ROWLDS 1   // 0: the per-row DPP sums (A/B builds)
+#endif
+
 // Per-thread accumulators of one tile: the moments and the column partials of its 8 columns.
 struct TileAcc {
   float L = 0.f, sd = 0.f, sdd = 0.f, sdt = 0.f, st = 0.f, stt = 0.f, dg = 0.f;
@@ -73,12 +82,12 @@ struct TileAcc {
 // bounds, i < j on the diagonal, the diagonal moment); interior tiles take MASK = false and do
 // no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
 // w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
-template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1, bool BG = false>
+template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1, bool BG = false, bool RLDS = false>
 __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int64_t row0, int64_t col0,
                                           int N, int I, int J, float bg,
                                           const float *tile, const float (*sc)[BT][3], int tx, int ty,
                                           const float *cx, const float *cy, const float *cz, const int *gj,
-                                          float4 *__restrict__ prow, TileAcc &A) {
+                                          float4 *__restrict__ prow, TileAcc &A, float4 *rowpart) {
 #pragma unroll 1
   for (int k = K0; k < K1; ++k) {
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
@@ -151,10 +160,14 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
       A.ay[q] = fmaf(-w, dy, A.ay[q]);
       A.az[q] = fmaf(-w, dz, A.az[q]);
     }
-    px = sum16(px);
-    py = sum16(py);
-    pz = sum16(pz);
-    if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
+    if constexpr (RLDS) {   // the thread's 8-column partial of row lr; the 16 of a row are added at the end
+      rowpart[lr * kRowPad + tx] = make_float4(px, py, pz, 0.f);
+    } else {
+      px = sum16(px);
+      py = sum16(py);
+      pz = sum16(pz);
+      if (tx == 0) prow[lr] = make_float4(px, py, pz, 0.f);
+    }
   }
 }
 
@@ -163,10 +176,10 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
 // v_pk_{add,mul,fma}_f32 (two pairs per instruction); v_rsq stays scalar.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-template <bool PEARSON, int K0, int K1, bool BG = false>
+template <bool PEARSON, int K0, int K1, bool BG = false, bool RLDS = false>
 __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const float (*sc)[BT][3], int tx, int ty,
                                              const float *cx, const float *cy, const float *cz,
-                                             float4 *__restrict__ prow, TileAcc &A) {
+                                             float4 *__restrict__ prow, TileAcc &A, float4 *rowpart) {
   f2 cx2[4], cy2[4], cz2[4], ax2[4], ay2[4], az2[4];
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
@@ -223,8 +236,12 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       ay2[h] = __builtin_elementwise_fma(-w, dy, ay2[h]);
       az2[h] = __builtin_elementwise_fma(-w, dz, az2[h]);
     }
-    const float sx = sum16(px.x + px.y), sy = sum16(py.x + py.y), sz = sum16(pz.x + pz.y);
-    if (tx == 0) prow[lr] = make_float4(sx, sy, sz, 0.f);
+    if constexpr (RLDS) {
+      rowpart[lr * kRowPad + tx] = make_float4(px.x + px.y, py.x + py.y, pz.x + pz.y, 0.f);
+    } else {
+      const float sx = sum16(px.x + px.y), sy = sum16(py.x + py.y), sz = sum16(pz.x + pz.y);
+      if (tx == 0) prow[lr] = make_float4(sx, sy, sz, 0.f);
+    }
   }
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
@@ -271,6 +288,9 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   __shared__ float sc[2][BT][3];
   __shared__ float4 colred[4][BT];
   __shared__ double mred[4][7];
+  constexpr bool RL = BG && HICGAT_PD_ROWLDS;
+  __shared__ float4 rowpart_s[RL ? BT * kRowPad : 1];
+  float4 *rowpart = RL ? rowpart_s : nullptr;
   const int64_t t = t0 + blockIdx.x;
   int I, J;
   if (MODE == MODE_SYM) {
@@ -332,18 +352,18 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   constexpr bool PK = (VEC || BG) && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4, BG>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
+    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 0, 4, BG>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 0, 4, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8, BG>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A);
-    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
+    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 4, 8, BG>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A);
+    tile_rows<MODE, VEC, PEARSON, true, 4, 8, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   }
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
@@ -384,6 +404,17 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
       s.z += o.z;
     }
     prow[BT + tid] = s;
+  } else if (RL) {
+    const int lr = tid - BT;
+    float4 s = rowpart[lr * kRowPad];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      const float4 o = rowpart[lr * kRowPad + q];
+      s.x += o.x;
+      s.y += o.y;
+      s.z += o.z;
+    }
+    prow[lr] = make_float4(s.x, s.y, s.z, 0.f);
   }
   if (MODE == MODE_SYM && tid < 7) {
     mom[(size_t)t * 8 + tid] = ((mred[0][tid] + mred[1][tid]) + mred[2][tid]) + mred[3][tid];
@@ -398,8 +429,6 @@ constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-th
 
 __device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
                                       double *__restrict__ part);
-__device__ void moments_last_block(const double *__restrict__ part, unsigned *__restrict__ ticket, int N,
-                                   int loss_kind, double *__restrict__ stats, float *__restrict__ loss);
 
 // mom != NULL: the last kMomBlocks blocks sum runs of the moment records [m0, m1) (tiles, then the
 // support pass's blocks) into mpart instead (moments_partial_block); blocks [0, row_blocks) reduce
@@ -411,13 +440,9 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
                                                                const double *__restrict__ mom, int64_t m0, int64_t m1,
                                                                int row_blocks, double *__restrict__ mpart,
                                                                const float4 *__restrict__ corr, int corr_r0,
-                                                               int corr_r1, double *__restrict__ dc64,
-                                                               unsigned *__restrict__ ticket = nullptr,
-                                                               double *__restrict__ stats = nullptr,
-                                                               float *__restrict__ loss = nullptr, int loss_kind = 0) {
+                                                               int corr_r1, double *__restrict__ dc64) {
   if (mom && (int)blockIdx.x >= row_blocks) {
     moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
-    if (ticket) moments_last_block(mpart, ticket, N, loss_kind, stats, loss);
     return;
   }
   __shared__ float4 red[kRedGroups][64];
@@ -531,32 +556,6 @@ __device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0
     __syncthreads();
   }
   if (tid < 7) part[blk * 8 + tid] = mred[tid][0];
-}
-
-// The moments' second stage inside the reduce launch (no extra launch): every moment block, after
-// writing its partial, takes a ticket (device-scope atomic after a release fence); the block that
-// draws the last one adds the kMomBlocks partials in block order -- the same order and bits as
-// moments_finalize_kernel -- finalizes, and puts the ticket back to 0 for the next launch.
-__device__ void moments_last_block(const double *__restrict__ part, unsigned *__restrict__ ticket, int N,
-                                   int loss_kind, double *__restrict__ stats, float *__restrict__ loss) {
-  __shared__ int last;
-  __threadfence();                 // this block's partial (threads < 7) before the ticket
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == (unsigned)(kMomBlocks - 1);
-  __syncthreads();
-  if (!last) return;
-  __threadfence();                 // acquire: every other block's partial is visible
-  if (threadIdx.x < 7) {
-    double s = 0.0;
-    for (int b = 0; b < kMomBlocks; ++b)
-      s += __hip_atomic_load(part + b * 8 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    stats[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    finalize_stats(N, loss_kind, stats, loss);
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__restrict__ part, int N, int loss_kind,
@@ -857,7 +856,7 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
                                                           const float *val, const float *diag, int64_t tile_begin,
                                                           int64_t tile_end, int support_row_begin, int support_row_end,
                                                           int loss_kind, double *stats, float *loss, float *dcoords,
-                                                          double *dcoords64, unsigned *ticket, void *workspace,
+                                                          double *dcoords64, void *workspace,
                                                           size_t workspace_bytes, hicgat_stream_t stream) {
   if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
@@ -908,13 +907,10 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
   const int row_blocks = (dcoords || dcoords64) ? (N + 63) / 64 : 0;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
                      (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
-                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64, ticket, stats, loss,
-                     loss_kind);
+                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64);
   HICGAT_CHECK_LAUNCH();
-  if (!ticket) {
-    hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
-    HICGAT_CHECK_LAUNCH();
-  }
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
+  HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
@@ -927,8 +923,7 @@ extern "C" int hicgat_pairdist_mse_fused_support_range(const float *coords, int 
                                                        hicgat_stream_t stream) {
   return hicgat_pairdist_mse_fused_support_range_ex(coords, nullptr, N, background, rowptr, col, val, diag, tile_begin,
                                                     tile_end, support_row_begin, support_row_end, loss_kind, stats,
-                                                    loss, dcoords, dcoords64, nullptr, workspace, workspace_bytes,
-                                                    stream);
+                                                    loss, dcoords, dcoords64, workspace, workspace_bytes, stream);
 }
 
 extern "C" int hicgat_pairdist_mse_fused_support(const float *coords, int N, float background,

@@ -92,13 +92,13 @@ __device__ __forceinline__ void store_tiles(const f32x4 (&acc)[RB / 16][NT], int
 }
 
 // one wave per row: z = relu((y - mean) rstd gamma + beta) (+ y[W + c] when RES), y = the row in LDS
-template <int RB, int W, bool RES>
+template <int RB, int W, bool RES, int NW = 4>
 __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, const float *__restrict__ gamma,
                                         const float *__restrict__ beta, float eps, float *__restrict__ Zs, int ldz,
                                         float *__restrict__ z, float2 *__restrict__ stats, int m0, int M, int wv,
                                         int lane) {
   constexpr int V = W / 64;
-  for (int rr = wv; rr < RB; rr += 4) {
+  for (int rr = wv; rr < RB; rr += NW) {
     const float *y = Ys + rr * lds;
     float v[V];
 #pragma unroll
@@ -127,9 +127,16 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
   }
 }
 
-// RB rows per workgroup (the launch uses 16).
-template <int RB>
-__global__ __launch_bounds__(256) void tail_fwd_kernel(
+// RB rows per workgroup (the launch uses 16), NW waves: every GEMM stage splits its output columns
+// over the waves (a column's k order, hence its bits, do not depend on NW), the LayerNorm rows too.
+// NW = 8: two waves per SIMD, so one wave's weight loads and LDS reads hide under the other's MFMAs
+// (with 4, one wave per SIMD, every latency of the chain is exposed; a rank's shard at P = 8 has
+// 157 workgroups for 256 CUs, one each).
+#ifndef HICGAT_TAIL_WAVES
+#define HICGAT_TAIL_WAVES 8
+#endif
+template <int RB, int NW>
+__global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
     const float *__restrict__ b2c, const float *__restrict__ g2, const float *__restrict__ be2,
@@ -143,43 +150,43 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   float *Bs = lds_tail + RB * XS;    // Y1, then Y2 / y3 rows
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * RB;
-  constexpr int H = RB / 16;
+  constexpr int H = RB / 16, NT1 = 32 / NW, NT2 = 16 / NW;   // 16-column tiles per wave: block 1 / block 2
   // x rows -> LDS (rows past M: zeros)
-  for (int e = tid; e < RB * 128; e += 256) {
+  for (int e = tid; e < RB * 128; e += 64 * NW) {
     const int r = e >> 7, c4 = e & 127;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + (size_t)(m0 + r) * ldx)[c4];
     *reinterpret_cast<float4 *>(&As[r * XS + 4 * c4]) = v;
   }
   __syncthreads();
-  // ---- block 1: 512 -> 512, wave wv: columns 128 wv .. 128 wv + 127 ----
+  // ---- block 1: 512 -> 512, wave wv: columns 16 NT1 wv .. + 16 NT1 - 1 ----
   {
-    f32x4 acc[H][8];
+    f32x4 acc[H][NT1];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, 8, 512>(As, XS, W1c, 128 * wv, acc, lane);
-    store_tiles<RB, 8>(acc, 128 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
+      for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, NT1, 512>(As, XS, W1c, 16 * NT1 * wv, acc, lane);
+    store_tiles<RB, NT1>(acc, 16 * NT1 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<RB, 256, true>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
+  ln_rows<RB, 256, true, NW>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
   __syncthreads();
-  // ---- block 2: 256 -> 256, wave wv: columns 64 wv .. 64 wv + 63 ----
+  // ---- block 2: 256 -> 256, wave wv: columns 16 NT2 wv .. ----
   {
-    f32x4 acc[H][4];
+    f32x4 acc[H][NT2];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, 4, 256>(As, XS, W2c, 64 * wv, acc, lane);
-    store_tiles<RB, 4>(acc, 64 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
+      for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, NT2, 256>(As, XS, W2c, 16 * NT2 * wv, acc, lane);
+    store_tiles<RB, NT2>(acc, 16 * NT2 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<RB, 128, true>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
+  ln_rows<RB, 128, true, NW>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
   __syncthreads();
-  // ---- block 3: 128 -> 64, wave wv: columns 16 wv .. 16 wv + 15 ----
-  {
+  // ---- block 3: 128 -> 64, waves 0..3: columns 16 wv .. 16 wv + 15 ----
+  if (wv < 4) {
     f32x4 acc[H][1];
 #pragma unroll
     for (int h = 0; h < H; ++h) acc[h][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -187,7 +194,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
     store_tiles<RB, 1>(acc, 16 * wv, b3, Bs, XS, y3, 64, m0, M, lane);
   }
   __syncthreads();
-  ln_rows<RB, 64, false>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
+  ln_rows<RB, 64, false, NW>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
   __syncthreads();
   // ---- dense3: 64 -> 3, thread t < 3 RB: row t / 3, output t % 3 (fp32 fma chain over k) ----
   if (tid < RB * 3) {
@@ -271,7 +278,7 @@ __device__ __forceinline__ void put_tiles(const f32x4 (&acc)[RB / 16][NT], int n
 // arithmetic): dz from LDS (Dz, stride ldd), y / stats from global; dy (and dres = dz beside it when
 // RES) into LDS (Gs, stride lds: [dy | dres]) and the global dY rows ([M][W or 2W]); the wave's
 // dgamma / dbeta partials into its slot of part ([slots][2][W], hicgat_ln_relu_res_bwd_params).
-template <int RB, int W, bool RES>
+template <int RB, int W, bool RES, int NW = 4>
 __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ldd, const float *__restrict__ y,
                                             int64_t ldy, const float2 *__restrict__ stats,
                                             const float *__restrict__ gamma, const float *__restrict__ beta,
@@ -285,7 +292,7 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
     b_[q] = beta[q * 64 + lane];
     pg[q] = pb[q] = 0.f;
   }
-  for (int rr = wv; rr < RB; rr += 4) {
+  for (int rr = wv; rr < RB; rr += NW) {
     const int row = m0 + rr;
     const bool live = row < M;
     const float2 st = live ? stats[row] : make_float2(0.f, 0.f);
@@ -323,10 +330,9 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
   }
 }
 
-constexpr int kTailBwdSlots = 4096;   // = kLnWaves (layernorm.hip): the partial slots of each LN workspace
 
-template <int RB>
-__global__ __launch_bounds__(256) void tail_bwd_kernel(
+template <int RB, int NW>
+__global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
     const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
     const float2 *__restrict__ st3, const float *__restrict__ W4, const float *__restrict__ W3,
@@ -339,11 +345,11 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   float *As = lds_tail;              // dz3, dz2, dz1 rows
   float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int slot = blockIdx.x * 4 + wv;
+  const int slot = blockIdx.x * NW + wv;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16;
   // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
-  for (int e = tid; e < RB * 64; e += 256) {
+  for (int e = tid; e < RB * 64; e += 64 * NW) {
     const int r = e >> 6, c = e & 63;
     float s = 0.f;
     if (m0 + r < M) {
@@ -353,41 +359,44 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     As[r * XS + c] = s;
   }
   __syncthreads();
-  ln_bwd_rows<RB, 64, false>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, m0, M, wv, lane);
+  ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, m0, M, wv, lane);
   __syncthreads();
-  // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 32 wv ..
+  // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 16 ND wv ..
+  constexpr int ND = 8 / NW, NT2 = 16 / NW, NT1 = 32 / NW;
   {
-    f32x4 acc[H][2];
-#pragma unroll
-    for (int h = 0; h < H; ++h) acc[h][0] = acc[h][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, 2, 64>(Bs, XS, W3, 128, 32 * wv, acc, lane);
-    put_tiles<RB, 2>(acc, 32 * wv, As, XS, nullptr, 0, m0, M, lane);
-  }
-  __syncthreads();
-  ln_bwd_rows<RB, 128, true>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, m0, M, wv, lane);
-  __syncthreads();
-  // block 2 backward: dz1 = [dy2 | dres2] [W_1; W_1al] ([RB x 256] [256 x 256]), wave wv: columns 64 wv ..
-  {
-    f32x4 acc[H][4];
+    f32x4 acc[H][ND];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, 4, 256>(Bs, XS, W2c, 256, 64 * wv, acc, lane);
-    put_tiles<RB, 4>(acc, 64 * wv, As, XS, nullptr, 0, m0, M, lane);
+      for (int t = 0; t < ND; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, ND, 64>(Bs, XS, W3, 128, 16 * ND * wv, acc, lane);
+    put_tiles<RB, ND>(acc, 16 * ND * wv, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
-  ln_bwd_rows<RB, 256, true>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, m0, M, wv, lane);
+  ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, m0, M, wv, lane);
   __syncthreads();
-  // block 1 backward: dx = [dy1 | dres1] [W_a; W_al] ([RB x 512] [512 x 512]), wave wv: columns 128 wv ..
+  // block 2 backward: dz1 = [dy2 | dres2] [W_1; W_1al] ([RB x 256] [256 x 256]), wave wv: columns 16 NT2 wv ..
   {
-    f32x4 acc[H][8];
+    f32x4 acc[H][NT2];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, 8, 512>(Bs, XS, W1c, 512, 128 * wv, acc, lane);
-    put_tiles<RB, 8>(acc, 128 * wv, nullptr, 0, dx, 512, m0, M, lane);
+      for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, NT2, 256>(Bs, XS, W2c, 256, 16 * NT2 * wv, acc, lane);
+    put_tiles<RB, NT2>(acc, 16 * NT2 * wv, As, XS, nullptr, 0, m0, M, lane);
+  }
+  __syncthreads();
+  ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, m0, M, wv, lane);
+  __syncthreads();
+  // block 1 backward: dx = [dy1 | dres1] [W_a; W_al] ([RB x 512] [512 x 512]), wave wv: columns 16 NT1 wv ..
+  {
+    f32x4 acc[H][NT1];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, NT1, 512>(Bs, XS, W1c, 512, 16 * NT1 * wv, acc, lane);
+    put_tiles<RB, NT1>(acc, 16 * NT1 * wv, nullptr, 0, dx, 512, m0, M, lane);
   }
 }
 
@@ -413,17 +422,23 @@ extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const f
   // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
   // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
   // with one workgroup per CU every phase's latency is exposed.
-  constexpr int RB = 16;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB>),
+  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL(tail_fwd_kernel<RB>, dim3((M + RB - 1) / RB), dim3(256), (size_t)2 * RB * XS * sizeof(float),
+  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW>), dim3((M + RB - 1) / RB), dim3(64 * NW), (size_t)2 * RB * XS * sizeof(float),
                      (hipStream_t)stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps,
                      Y1, reinterpret_cast<float2 *>(st1), z1, Y2, reinterpret_cast<float2 *>(st2), z2, y3,
                      reinterpret_cast<float2 *>(st3), z3, coords);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_tail_bwd_waves(void) { return HICGAT_TAIL_WAVES; }
+
+extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
+  return M <= 0 ? 16 : (size_t)HICGAT_TAIL_WAVES * ((M + 15) / 16) * 2 * W * sizeof(float);
 }
 
 extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
@@ -433,23 +448,22 @@ extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y
                                      const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
                                      size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
                                      hicgat_stream_t stream) {
-  constexpr int RB = 16;
+  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
   if (M < 0) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
-  // every workgroup owns four partial slots of each LN workspace: rows up to 4 slots x 16 rows each
-  if ((M + RB - 1) / RB > kTailBwdSlots / 4) return HICGAT_EUNSUPPORTED;
   const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
                       dx, dY1, dY2, dy3, ws1, ws2, ws3};
   for (const void *p : ps)
     if (!p) return HICGAT_EINVAL;
-  if (ws1_bytes < hicgat_ln_relu_res_workspace_bytes(256) || ws2_bytes < hicgat_ln_relu_res_workspace_bytes(128) ||
-      ws3_bytes < hicgat_ln_relu_res_workspace_bytes(64))
+  // every workgroup owns NW partial rows of each LN workspace (one per wave)
+  if (ws1_bytes < hicgat_tail_bwd_workspace_bytes(M, 256) || ws2_bytes < hicgat_tail_bwd_workspace_bytes(M, 128) ||
+      ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
     return HICGAT_EINVAL;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL(tail_bwd_kernel<RB>, dim3((M + RB - 1) / RB), dim3(256), (size_t)2 * RB * XS * sizeof(float),
+  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW>), dim3((M + RB - 1) / RB), dim3(64 * NW), (size_t)2 * RB * XS * sizeof(float),
                      (hipStream_t)stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1), Y2,
                      reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c, W1c,
                      g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1), static_cast<float *>(ws2),

@@ -103,8 +103,7 @@ SIGNATURES = {
     "hicgat_pairdist_mse_fused_support_range": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64, c_int,
                                                         c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_mse_fused_support_range_ex": (c_int, [c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64,
-                                                           c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_sz,
-                                                           c_p]),
+                                                           c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_truth_support": (c_int, [c_p, c_int, c_i64, c_f, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_int,
                             c_int, c_p, c_sz, c_p]),
@@ -126,6 +125,8 @@ SIGNATURES = {
     "hicgat_ln_relu_res_workspace_bytes": (c_sz, [c_int]),
     "hicgat_ln_relu_res_bwd_params": (c_int, [c_int, c_p, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_tail_fwd_fused": (c_int, [c_p, c_i64, c_int] + [c_p] * 14 + [c_f] + [c_p] * 10 + [c_p]),
+    "hicgat_tail_bwd_waves": (c_int, []),
+    "hicgat_tail_bwd_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p]),
     "hicgat_sage_weights": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_agg": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_int, c_int, c_p, c_i64,
@@ -137,7 +138,6 @@ SIGNATURES = {
                                       c_int, c_u64, c_int, c_p, c_p, c_p]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
-    "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p, c_p]),
 }
 
 

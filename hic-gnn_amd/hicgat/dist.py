@@ -281,8 +281,8 @@ class ShardedTrainer:
         self.local_nnz = int(plan.nnz[rank])
         self.gidx = torch.from_numpy(plan.gidx).to(dev)
         self.gidx32 = self.gidx.to(torch.int32)
-        # the loss reads the coordinates straight from the padded all-gather buffer (cmap = gidx) and
-        # finishes its moments inside its reduce launch (a zeroed ticket): the HIP path only
+        # the loss reads the coordinates straight from the padded all-gather buffer (cmap = gidx): the
+        # HIP path only
         self.direct_coords = self.cuda and sf is not None
         conv = model.conv
         self.W, self.att_l, self.att_r, self.bias = conv.lin_l.weight, conv.att_l, conv.att_r, conv.bias
@@ -354,7 +354,6 @@ class ShardedTrainer:
         self.stats = self.red[:12]
         self.dc64 = self.red[12:].view(N, 3)
         self.loss = torch.zeros((), **f32)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.opt = FlatAdam(model.flat_parameters(), lr=lr, kern=kern)
         # gradient buckets: the GATConv's parameters lead the flat buffer (flat_parameters order)
         conv_ids = {id(p) for p in (self.W, self.att_l, self.att_r, self.bias) if p is not None}
@@ -384,7 +383,7 @@ class ShardedTrainer:
         K, N = self.K, self.N
         if self.direct_coords:      # coords = the padded all-gather buffer, read through gidx
             K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
-                                       self.loss, self.dc64, cmap=self.gidx32, ticket=self.ticket)
+                                       self.loss, self.dc64, cmap=self.gidx32)
         elif self.sf is not None:
             K.fused_loss_support_range(coords, self.sf, N, self.kind, self.t0, self.t1, self.s0, self.s1, self.stats,
                                        self.loss, self.dc64)

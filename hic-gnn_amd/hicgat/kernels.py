@@ -322,40 +322,27 @@ class HipKernels:
                 int(kind), P(stats), P(loss), P(dcoords), P(ws), ws.numel(), _lib.stream(coords.device)),
                 "hicgat_pairdist_mse_fused_band")
 
-    _tickets = {}
-
-    def ticket(self, device):
-        """A zeroed unsigned counter for the fused loss's in-launch moment finalize (one per device
-        and current stream; every launch leaves it 0).  Allocated on first use, outside any capture
-        when the caller warms up eagerly."""
-        key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-        t = self._tickets.get(key)
-        if t is None:
-            t = self._tickets[key] = torch.zeros(1, dtype=torch.int32, device=device)
-        return t
-
     def fused_loss_support(self, coords, sf, n, kind, stats, loss, dcoords):
         """The fused loss over a truth in background + support form (``graph.SupportForm``)."""
         ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
         with _timed("pairdist_mse_fused"):
             _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range_ex(
                 P(coords), None, n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), 0, -1, 0,
-                n, int(kind), P(stats), P(loss), P(dcoords), None, P(self.ticket(coords.device)), P(ws), ws.numel(),
+                n, int(kind), P(stats), P(loss), P(dcoords), None, P(ws), ws.numel(),
                 _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range_ex")
 
-    def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords, cmap=None,
-                                 ticket=None):
+    def fused_loss_support_range(self, coords, sf, n, kind, t0, t1, s0, s1, stats, loss, dcoords, cmap=None):
         """A rank's share of the background-form loss: bulk tiles [t0, t1), support rows [s0, s1)
         (partial moments and dcoords; the caller all-reduces them and calls ``loss_finalize``).
         A float64 ``dcoords`` receives the fp32 gradient values widened (one all-reduce buffer);
-        ``cmap`` (int32 [n]): global row -> row of ``coords``; ``ticket``: the in-launch finalize."""
+        ``cmap`` (int32 [n]): global row -> row of ``coords``."""
         ws = _lib.workspace(self.lib.hicgat_pairdist_support_workspace_bytes(n), coords.device)
         d32, d64 = (None, dcoords) if dcoords.dtype == torch.float64 else (dcoords, None)
         assert cmap is None or (cmap.dtype == torch.int32 and cmap.numel() == n)
         with _timed("pairdist_mse_fused"):
             _lib.check(self.lib.hicgat_pairdist_mse_fused_support_range_ex(
                 P(coords), P(cmap), n, sf.background, P(sf.rowptr), P(sf.col_buf), P(sf.val_buf), P(sf.diag), int(t0),
-                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ticket), P(ws), ws.numel(),
+                int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ws), ws.numel(),
                 _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range_ex")
 
     def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None):
@@ -541,7 +528,7 @@ class HipKernels:
         dev = dcoords.device
         f = dict(dtype=torch.float32, device=dev)
         dx, dY1, dY2, dy3 = (torch.empty((M, w), **f) for w in (512, 512, 256, 64))
-        ws = [self.ln_workspace(w, dev) for w in (256, 128, 64)]
+        ws = [_lib.workspace(self.lib.hicgat_tail_bwd_workspace_bytes(M, w), dev) for w in (256, 128, 64)]
         ts = [W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3]
         assert all(t.is_contiguous() for t in ts) and dcoords.is_contiguous()
         with _timed("tail_bwd_fused"):
@@ -551,6 +538,10 @@ class HipKernels:
                 "hicgat_tail_bwd_fused")
         return dx, dY1, dY2, dy3, ws
 
+    def tail_partial_rows(self, M):
+        """Rows of LayerNorm partials hicgat_tail_bwd_fused leaves per workspace: one per wave."""
+        return int(self.lib.hicgat_tail_bwd_waves()) * (-(-M // 16))
+
     def ln_workspace(self, W, device):
         return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)
 
@@ -559,13 +550,11 @@ class HipKernels:
                                                           _lib.stream(ws.device)), "hicgat_ln_relu_res_bwd_params")
 
     # -- a10 --------------------------------------------------------------------------------------
-    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr, ticket=None):
-        """``ticket``: a zeroed int32 [1]: the step counter advances inside the Adam launch."""
+    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):
         with _timed("adam"):
-            _lib.check(self.lib.hicgat_adam_step_table_ex(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
-                                                          float(eps), P(table), table.shape[0], P(step_ctr),
-                                                          P(ticket), _lib.stream(flat.device)),
-                       "hicgat_adam_step_table_ex")
+            _lib.check(self.lib.hicgat_adam_step_table(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
+                                                       float(eps), P(table), table.shape[0], P(step_ctr),
+                                                       _lib.stream(flat.device)), "hicgat_adam_step_table")
 
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):

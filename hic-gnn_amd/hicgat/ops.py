@@ -728,7 +728,7 @@ def dual_ln_relu_res(x, lin1, lin2, norm):
 # N = 20000 step 1.977 vs 1.913 ms with the fused forward -- 16-row workgroups stream the 1.3 MB of
 # tail weights from L2 once per 16 rows (1.6 GB at N = 20000) where the tiled GEMMs reuse each weight
 # tile over 160 rows, and a 32-row form (one workgroup per CU) exposed every phase's latency -- and
-# the fused backward's LN partial slots end at 16 384 rows.
+# the fused backward's LN partials are one row per wave (workspaces sized by M).
 # Graphs below MIN_M (chr19: 58 / 114 loci) keep the per-layer kernels.
 FUSED_TAIL = os.environ.get("HICGAT_FUSED_TAIL", "1") != "0"
 FUSED_TAIL_MIN_M = int(os.environ.get("HICGAT_FUSED_TAIL_MIN_M", "1024"))
@@ -771,7 +771,7 @@ class _FusedTailFn(torch.autograd.Function):
         import types
         x, Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = ctx.saved_tensors
         Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3 = ctx.params
-        if FUSED_TAIL_BWD and dcoords.shape[0] <= 16384:   # hicgat_tail_bwd_fused's row limit
+        if FUSED_TAIL_BWD:
             # the input-gradient chain in one launch; the parameter gradients from its dY tensors
             # and LN partials, issued in the per-layer path's order (dense3, norm2, dense2, block 2,
             # block 1)
@@ -781,7 +781,7 @@ class _FusedTailFn(torch.autograd.Function):
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
                 g2.contiguous(), be2.contiguous())
-            rows = 4 * (-(-dc.shape[0] // 16))      # the kernel's partial rows: 4 waves per 16 node rows
+            rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per wave
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)
             dW2, db2 = _wb_grad_to(K, W2, b2, dy3, z2)

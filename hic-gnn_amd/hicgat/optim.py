@@ -50,8 +50,6 @@ class FlatAdam:
         tab[:, 1] = np.power(1.0 - np.power(b2, t), 0.5)
         self.table = torch.from_numpy(tab).to(self.flat.device)
         self.step_ctr = torch.full((1,), self.step_count, dtype=torch.int64, device=self.flat.device)
-        # the Adam launch advances step_ctr itself (its last workgroup, by this zeroed ticket)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=self.flat.device)
         return self
 
     def zero_grad(self, set_to_none=False):
@@ -79,7 +77,7 @@ class FlatAdam:
         kern = self.kern if self.kern is not None else kernels.default()
         if getattr(self, "step_ctr", None) is not None:
             kern.adam_table(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.betas[0],
-                            self.betas[1], self.eps, self.table, self.step_ctr, ticket=getattr(self, "ticket", None))
+                            self.betas[1], self.eps, self.table, self.step_ctr)
             return
         kern.adam(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.lr, self.betas[0],
                   self.betas[1], self.eps, self.step_count)

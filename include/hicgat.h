@@ -315,18 +315,14 @@ int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float ba
                                             int support_row_end, int loss_kind, double *stats, float *loss,
                                             float *dcoords, double *dcoords64, void *workspace,
                                             size_t workspace_bytes, hicgat_stream_t stream);
-/* The same with two options for the sharded step (NULL = as above): cmap [N] maps global row g to
- * its row in ``coords`` (the padded [P*R, 3] all-gather buffer, so no reorder launch), and ticket
- * (a caller-owned unsigned, 0 before the call and left 0 after it) lets the reduce launch finish the
- * moments itself (its last moment block, by an atomic ticket; same order and bits) -- one launch
- * fewer. */
+/* The same with cmap (NULL = as above): cmap [N] maps global row g to its row in ``coords`` (the
+ * sharded step's padded [P*R, 3] all-gather buffer, so no reorder launch before the loss). */
 int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, const int32_t *cmap, int N, float background,
                                                const int32_t *rowptr, const int32_t *col, const float *val,
                                                const float *diag, int64_t tile_begin, int64_t tile_end,
                                                int support_row_begin, int support_row_end, int loss_kind,
                                                double *stats, float *loss, float *dcoords, double *dcoords64,
-                                               unsigned *ticket, void *workspace, size_t workspace_bytes,
-                                               hicgat_stream_t stream);
+                                               void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 /* The background form of a symmetric N x N fp32 truth T (leading dim ldt): the sorted CSR of the
  * off-diagonal entries != background, their values, and the diagonal.  Two calls, as
  * hicgat_csr_from_dense: col == NULL fills rowptr (the counts, scanned); then col / val / diag. */
@@ -469,9 +465,12 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
  * g1/be1 = norm_a, g2/be2 = norm1, g3/be3 = norm2: writes dx [M][512] (the gradient of the tail's
  * input), dY1 [M][512] = [dy | dres] of block 1, dY2 [M][256] of block 2, dy3 [M][64] (dense2's output
  * gradient) -- the inputs of the weight-gradient GEMMs -- and each LayerNorm's dgamma/dbeta partials
- * into ws1 / ws2 / ws3 (workspaces of hicgat_ln_relu_res_workspace_bytes(256 / 128 / 64)): rows
- * [0, 4 ceil(M/16)) of a [.][2W] = [dgamma | dbeta] matrix, one per wave (their column sums, e.g.
- * hicgat_colsum, are dgamma / dbeta).  M <= 16384. */
+ * into ws1 / ws2 / ws3: rows
+ * [0, hicgat_tail_bwd_waves() ceil(M/16)) of a [.][2W] = [dgamma | dbeta] matrix, one per wave
+ * (their column sums, e.g. hicgat_colsum, are dgamma / dbeta); each workspace at least
+ * hicgat_tail_bwd_workspace_bytes(M, W) for W = 256 / 128 / 64. */
+int hicgat_tail_bwd_waves(void);
+size_t hicgat_tail_bwd_workspace_bytes(int M, int W);
 int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
                           const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
                           const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
@@ -536,12 +535,6 @@ int hicgat_adam_step(float *param, const float *grad, float *exp_avg, float *exp
 int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                            int64_t n, double beta1, double beta2, double eps, const float *table,
                            int64_t table_len, int64_t *step_counter, hicgat_stream_t stream);
-/* The same with ticket (a caller-owned unsigned, 0 before and after): the step counter is advanced
- * inside the Adam launch by its last workgroup (an atomic ticket) instead of by a second launch. */
-int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
-                              int64_t n, double beta1, double beta2, double eps, const float *table,
-                              int64_t table_len, int64_t *step_counter, unsigned *ticket, hicgat_stream_t stream);
-
 #ifdef __cplusplus
 }
 #endif

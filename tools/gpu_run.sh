@@ -16,6 +16,7 @@
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
 #   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world; _ag: allgather
 #                form, _xa: aggregate-first form, _au: bench.py's default "auto")
+#   kb:<jobs>:<libs> tools/kbench.py A/B of the named kernel jobs over the listed library builds
 #   simab:<env>  rank 0 of the simulated 8-rank xagg step (100 steps) under the environment assignment <env>
 #   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
@@ -90,6 +91,11 @@ for S in "$@"; do
       env ${S#simab:} timeout -k 10 240 python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 100 \
         --warmup 5 > gpurun_out/${T}_simab.json 2> gpurun_out/${T}_simab.err || exit $?
       echo "simab: ${S#simab:} $(python -c "import json;d=json.loads(open('gpurun_out/${T}_simab.json').read().strip().splitlines()[-1]);print([round(v,4) for v in d['simulated']['rank_ms']], [round(v,4) for v in d['simulated']['rank_median_ms']])")" ;;
+    kb:*)
+      # per-kernel A/B (tools/kbench.py): kb:<job substrings, comma-separated>:<library builds, comma-separated>
+      R=${S#kb:}; J=${R%%:*}; L=${R#*:}
+      timeout -k 10 300 python tools/kbench.py --only "$J" --libs "$L" --reps 20 --rounds 3 > gpurun_out/${T}_kbench.txt 2>&1 || exit $?
+      cat gpurun_out/${T}_kbench.txt | grep " med " ;;
     simprof|simprof_ag|simprof_xa)
       M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \
