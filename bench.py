@@ -560,8 +560,7 @@ def main():
         dom = max(cands, key=lambda k: kern_t[k]["total_ms"])
 
         def per_launch(k, b):
-            """A pass split into row chunks (ops._src_chunks) is several launches per step: each
-            launch's algorithmic bytes are its share."""
+            """A pass issued as several launches per step: each launch's algorithmic bytes are its share."""
             return b / max(1.0, kern_t[k]["launches"] / args.steps)
 
         for k in cands:
@@ -625,8 +624,7 @@ def main():
                    "n_nodes": n, "nnz_with_self_loops": nnz, "d": D_FEAT, "heads": HEADS,
                    "loss": args.loss,
                    "parallelism": (f"dst-row shard x{world} (nnz-balanced, {runner.mode})" if sharded else "single"),
-                   "gemm": ({0: "auto (x3 split where supported)", 1: "fp32 MFMA", 2: "x3 split"}[kernels.default().gemm_impl]
-                            if not args.selftest_cpu else "cpu stand-in")},
+                   "gemm": "fp32 MFMA" if not args.selftest_cpu else "cpu stand-in"},
         "final_loss": loss_v,
         "reference_loop": ref_loop,
         "roofline": roof,

@@ -372,25 +372,11 @@ __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict
   }
 }
 
-// Grid of the source pass: one workgroup per 4 rows, or HICGAT_SRC_WGS workgroups per CU (persistent)
-// when set -- then the gather leaves CU slots to the side stream's GEMMs.
-static int src_grid(int rows) {
-  static const int per_cu = getenv("HICGAT_SRC_WGS") ? atoi(getenv("HICGAT_SRC_WGS")) : 0;
-  const int full = (rows + 3) / 4;
-  if (per_cu <= 0) return full;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  return std::max(1, std::min(full, per_cu * cus));
-}
+// Grid of the source pass: one workgroup per 4 rows.  (A persistent grid of 2-3 workgroups per CU,
+// leaving slots to the side stream's GEMMs, measured the same step or slower)
 #define HICGAT_SRC_LAUNCH(SPLIT_, rows_, ...)                                                              \
-  do {                                                                                                     \
-    const int g_ = src_grid(rows_);                                                                        \
-    if (g_ < ((rows_) + 3) / 4)                                                                            \
-      hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, true>), dim3(g_), dim3(256), 0, __VA_ARGS__);  \
-    else                                                                                                   \
-      hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, false>), dim3(g_), dim3(256), 0, __VA_ARGS__); \
-  } while (0)
+  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, false>), dim3(((rows_) + 3) / 4), dim3(256), 0,    \
+                     __VA_ARGS__)
 
 // The gather half of hicgat_gat_agg_bwd_src_tiled (gat_tiles.hip): the sparse remainder's shares.
 int agg_bwd_src_split_launch(const int *rowptr_s, const int *col_s, int row_begin, int row_end, const float *h,

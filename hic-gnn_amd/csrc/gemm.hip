@@ -233,241 +233,6 @@ __global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_O
                                              csum, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-// ---- "x3": the same GEMM on the bf16 matrix cores by an exact three-way operand split ------------
-// Every fp32 operand is split x = x0 + x1 + x2 with x0 = bf16(x), x1 = bf16(x - x0),
-// x2 = bf16(x - x0 - x1) (each difference is exact in fp32; the three bf16 significands carry the
-// 24-bit fp32 one), and a*b is formed from the six products a_i b_j with i + j <= 2, each exact in
-// the fp32 accumulator of v_mfma_f32_32x32x16_bf16; the dropped terms are O(2^-24 |a b|), the size
-// of one fp32 rounding.  So the result has fp32-GEMM accuracy (tests/test_gpu_fast_paths.py checks
-// it against fp64 and against the f32-MFMA kernel above), at 6 x 32 = 192 cycles per 32x32x16 block
-// instead of 8 x 64 = 512 for v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md cycle table): 2.7x the
-// fp32 matrix rate.  Tile BM x 128 x 16, 4 waves in 2 x 2.  The staging threads split the operands
-// on the way into LDS (row-major operands: 4 consecutive k per thread; K-major operands: Q k-rows of
-// 4 columns per thread, transposed in registers); LDS holds the three bf16 planes of both tiles,
-// double buffered (one barrier per K-step), and the next K-step's global loads are in flight under
-// the current step's MFMAs.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
-
-constexpr int XK = 16;   // K-step = the K of one v_mfma_f32_32x32x16_bf16
-
-__device__ __forceinline__ unsigned short bf16_rn(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
-__device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_float((uint32_t)b << 16); }
-__device__ __forceinline__ void split3(float x, unsigned short &b0, unsigned short &b1, unsigned short &b2) {
-  b0 = bf16_rn(x);
-  const float r1 = x - bf16_f(b0);
-  b1 = bf16_rn(r1);
-  b2 = bf16_rn(r1 - bf16_f(b1));
-}
-__device__ __forceinline__ float f4_at(const float4 &v, int c) {
-  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-}
-
-// LDS image of one operand tile: plane p, tile row r (an m or n index), k in [0, 16): 32-B rows whose
-// two 16-B halves swap on rows with bit 3 set, so the 16 lanes of one ds_read_b128 phase (rows
-// r .. r+15, the same half) cover the 64 banks exactly once.
-template <int ROWS> struct X3Tile { unsigned short v[3][ROWS][XK]; };
-__device__ __forceinline__ int x3_col(int r, int k) { return ((((k >> 3) ^ (r >> 3)) & 1) << 3) | (k & 7); }
-
-// global -> registers, ROWS x 16 fp32 = ROWS/64 float4 per thread.  [rows, K] operands: piece e is
-// 4 consecutive k of tile row (e*256 + tid) / 4; [K, rows] operands: Q consecutive k rows of the same
-// 4 tile rows.  Out-of-range pieces are 0 (R % 4 == 0 and ke % 4 == 0: a float4 is all in or out).
-template <int ROWS, bool KM>
-__device__ __forceinline__ void x3_load(const float *__restrict__ P, int64_t ld, int r0, int R, int k0, int ke,
-                                        float4 (&reg)[ROWS / 64], unsigned &okm, int tid) {
-  constexpr int Q = ROWS / 64;
-  // every lane loads (out-of-range pieces from the operand's first float4) and x3_store zeroes them:
-  // one unconditional global_load_dwordx4 per piece, and no use of the data before the MFMAs
-  okm = 0;
-#pragma unroll
-  for (int e = 0; e < Q; ++e) {
-    size_t off;
-    bool ok;
-    if (!KM) {
-      const int idx = e * 256 + tid, gr = r0 + (idx >> 2), gk = k0 + (idx & 3) * 4;
-      ok = gr < R && gk < ke;
-      off = (size_t)gr * ld + gk;
-    } else {
-      constexpr int KQ = XK / Q;
-      const int gk = k0 + (tid % KQ) * Q + e, gr = r0 + (tid / KQ) * 4;
-      ok = gr < R && gk < ke;
-      off = (size_t)gk * ld + gr;
-    }
-    reg[e] = *reinterpret_cast<const float4 *>(P + (ok ? off : 0));
-    okm |= (ok ? 1u : 0u) << e;
-  }
-}
-
-template <int ROWS, bool KM>
-__device__ __forceinline__ void x3_store(X3Tile<ROWS> &T, const float4 (&reg)[ROWS / 64], unsigned okm, int tid) {
-  constexpr int Q = ROWS / 64;
-  auto val = [&](int e, int c) { return ((okm >> e) & 1u) ? f4_at(reg[e], c) : 0.f; };
-  if (!KM) {
-#pragma unroll
-    for (int e = 0; e < Q; ++e) {
-      const int idx = e * 256 + tid, r = idx >> 2, k = (idx & 3) * 4;
-      u16x4 p0, p1, p2;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        unsigned short b0, b1, b2;
-        split3(val(e, c), b0, b1, b2);
-        p0[c] = b0;
-        p1[c] = b1;
-        p2[c] = b2;
-      }
-      const int o = x3_col(r, k);
-      *reinterpret_cast<u16x4 *>(&T.v[0][r][o]) = p0;
-      *reinterpret_cast<u16x4 *>(&T.v[1][r][o]) = p1;
-      *reinterpret_cast<u16x4 *>(&T.v[2][r][o]) = p2;
-    }
-  } else {
-    constexpr int KQ = XK / Q;
-    const int k = (tid % KQ) * Q, rb = (tid / KQ) * 4;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int r = rb + c, o = x3_col(r, k);
-      if constexpr (Q == 2) {
-        u16x2 p0, p1, p2;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          unsigned short b0, b1, b2;
-          split3(val(e, c), b0, b1, b2);
-          p0[e] = b0;
-          p1[e] = b1;
-          p2[e] = b2;
-        }
-        *reinterpret_cast<u16x2 *>(&T.v[0][r][o]) = p0;
-        *reinterpret_cast<u16x2 *>(&T.v[1][r][o]) = p1;
-        *reinterpret_cast<u16x2 *>(&T.v[2][r][o]) = p2;
-      } else {
-        unsigned short b0, b1, b2;
-        split3(val(0, c), b0, b1, b2);
-        T.v[0][r][o] = b0;
-        T.v[1][r][o] = b1;
-        T.v[2][r][o] = b2;
-      }
-    }
-  }
-}
-
-// One K-step of a wave's TM x 2 grid of 32x32 output tiles: 6 MFMAs per tile, smallest terms first.
-template <int TM, int BM>
-__device__ __forceinline__ void x3_mma(const X3Tile<BM> &At, const X3Tile<128> &Bt, int am, int bn, int li, int lk,
-                                       f32x16 (&acc)[TM][2]) {
-  bf16x8 a[3][TM], b[3][2];
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int r = am + i * 32 + li;
-      a[p][i] = *reinterpret_cast<const bf16x8 *>(&At.v[p][r][x3_col(r, 8 * lk)]);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = bn + j * 32 + li;
-      b[p][j] = *reinterpret_cast<const bf16x8 *>(&Bt.v[p][r][x3_col(r, 8 * lk)]);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      f32x16 c = acc[i][j];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
-    }
-  }
-}
-
-#ifndef HICGAT_X3_OCC
-#define HICGAT_X3_OCC 2   // __launch_bounds__ min blocks per CU of the x3 kernel: VGPRs <= 256, 2 waves per SIMD
-#endif
-template <int BM, bool A_KM, bool B_KM>
-__global__ __launch_bounds__(256, HICGAT_X3_OCC) void gemm_x3_kernel(const float *__restrict__ A, int64_t lda,
-                                                      const float *__restrict__ B, int64_t ldb,
-                                                      float *__restrict__ C, int64_t ldc, int M, int N, int K,
-                                                      int kchunk, const float *__restrict__ bias,
-                                                      float *__restrict__ slab, int accumulate) {
-  constexpr int BN = 128, WM = BM / 2, TM = WM / 32;
-  __shared__ __attribute__((aligned(16))) X3Tile<BM> As[2];
-  __shared__ __attribute__((aligned(16))) X3Tile<BN> Bs[2];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1, li = lane & 31, lk = lane >> 5;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
-  f32x16 acc[TM][2];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  // global loads run two K-steps ahead of the MFMAs (a 16-deep step is ~770 MFMA cycles per wave,
-  // less than an HBM round trip): register sets 0 / 1 alternate with LDS buffers 0 / 1
-  float4 ra0[BM / 64], rb0[BN / 64], ra1[BM / 64], rb1[BN / 64];
-  unsigned oka0 = 0, okb0 = 0, oka1 = 0, okb1 = 0;
-  if (kb < ke) {
-    x3_load<BM, A_KM>(A, lda, m0, M, kb, ke, ra0, oka0, tid);
-    x3_load<BN, B_KM>(B, ldb, n0, N, kb, ke, rb0, okb0, tid);
-    if (kb + XK < ke) {
-      x3_load<BM, A_KM>(A, lda, m0, M, kb + XK, ke, ra1, oka1, tid);
-      x3_load<BN, B_KM>(B, ldb, n0, N, kb + XK, ke, rb1, okb1, tid);
-    }
-    x3_store<BM, A_KM>(As[0], ra0, oka0, tid);
-    x3_store<BN, B_KM>(Bs[0], rb0, okb0, tid);
-  }
-  __syncthreads();
-  for (int k0 = kb; k0 < ke; k0 += 2 * XK) {
-    // step k0 from LDS buffer 0; registers 1 hold step k0 + XK
-    if (k0 + 2 * XK < ke) {
-      x3_load<BM, A_KM>(A, lda, m0, M, k0 + 2 * XK, ke, ra0, oka0, tid);
-      x3_load<BN, B_KM>(B, ldb, n0, N, k0 + 2 * XK, ke, rb0, okb0, tid);
-    }
-    x3_mma<TM, BM>(As[0], Bs[0], wm * WM, wn * 64, li, lk, acc);
-    if (k0 + XK < ke) {
-      x3_store<BM, A_KM>(As[1], ra1, oka1, tid);
-      x3_store<BN, B_KM>(Bs[1], rb1, okb1, tid);
-    }
-    __syncthreads();
-    if (k0 + XK >= ke) break;
-    // step k0 + XK from LDS buffer 1; registers 0 hold step k0 + 2 XK
-    if (k0 + 3 * XK < ke) {
-      x3_load<BM, A_KM>(A, lda, m0, M, k0 + 3 * XK, ke, ra1, oka1, tid);
-      x3_load<BN, B_KM>(B, ldb, n0, N, k0 + 3 * XK, ke, rb1, okb1, tid);
-    }
-    x3_mma<TM, BM>(As[1], Bs[1], wm * WM, wn * 64, li, lk, acc);
-    if (k0 + 2 * XK < ke) {
-      x3_store<BM, A_KM>(As[0], ra0, oka0, tid);
-      x3_store<BN, B_KM>(Bs[0], rb0, okb0, tid);
-    }
-    __syncthreads();
-  }
-  // C/D map of a 32x32 f32 tile: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float *out = slab ? slab + (size_t)blockIdx.z * M * N : C;
-  const int64_t ldo = slab ? N : ldc;
-#pragma unroll
-  for (int a = 0; a < TM; ++a) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int gn = n0 + wn * 64 + b * 32 + li;
-      const float bb = (bias && !slab && gn < N) ? bias[gn] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int gm = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (gm < M && gn < N) {
-          float *o = out + (size_t)gm * ldo + gn;
-          *o = acc[a][b][r] + bb + ((accumulate && !slab) ? *o : 0.f);
-        }
-      }
-    }
-  }
-}
-
 __global__ void colsum_zero_kernel(float *out, int N, int accumulate) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n < N && !accumulate) out[n] = 0.f;
@@ -512,65 +277,24 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
   return HICGAT_OK;
 }
 
-template <int BM, bool AK, bool BK_>
-static int launch_x3(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
-                     int K, int splits, const float *bias, float *slab, int acc, hipStream_t s) {
-  const int kchunk = ((K + splits - 1) / splits + XK - 1) / XK * XK;
-  const dim3 grid((M + BM - 1) / BM, (N + 127) / 128, splits);
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, AK, BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, kchunk,
-                     bias, splits > 1 ? slab : nullptr, acc);
-  HICGAT_CHECK_LAUNCH();
-  if (splits > 1) {
-    const ColOut o{C, ldc, N, nullptr, bias, acc, nullptr, 0};
-    return colsum_wide_launch(slab, (int64_t)M * N, splits, (int64_t)M * N, o, s);
-  }
-  return HICGAT_OK;
-}
-
-// x3 needs float4 operand rows (16-B aligned, K or the row dim a multiple of 4) and a 64-wide N
-template <bool AK, bool BK_>
-static bool x3_ok(const float *A, int64_t lda, const float *B, int64_t ldb, int M, int N, int K) {
-  const bool a_ok = AK ? (M % 4 == 0 && lda % 4 == 0) : (K % 4 == 0 && lda % 4 == 0);
-  const bool b_ok = BK_ ? (N % 4 == 0 && ldb % 4 == 0) : (K % 4 == 0 && ldb % 4 == 0);
-  const bool al = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0;
-  return a_ok && b_ok && al && N >= 64 && M >= 32;
-}
-
 int gemm_tall_launch(bool b_kmajor, const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc,
                      int M, int N, int K, const float *bias, int accumulate, hipStream_t s);   // gemm_tall.hip
-
-// HICGAT_GEMM_TALL=0 (A/B measurement only): the 64x128 kernel for the tall problems too
-static bool tall_enabled() {
-  static const bool on = !(getenv("HICGAT_GEMM_TALL") && atoi(getenv("HICGAT_GEMM_TALL")) == 0);
-  return on;
-}
 
 // Problems with fewer 160x128 tiles than this go to the 64x128 kernel (2.5x the workgroups): one
 // workgroup per tile with the whole K inside, the tall kernel needs ~one tile per CU -- a rank's
 // 2700-row shard of a multi-GPU step is 68 tiles, a quarter of the chip (57 vs 98 us for 7x fewer
 // FLOP than the 20000-row GEMM).  The single-GPU shapes (>= 250 tiles) keep the tall kernel.
-// HICGAT_TALL_MIN_TILES overrides (A/B).
-static int64_t tall_min_tiles() {
-  static const int64_t v = getenv("HICGAT_TALL_MIN_TILES") ? atoll(getenv("HICGAT_TALL_MIN_TILES")) : 192;
-  return v;
-}
+static int64_t tall_min_tiles() { return 192; }
 
 template <bool AK, bool BK_>
 static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, int64_t ldc, int M, int N,
                     int K, int splits, const float *bias, float *slab, int acc, int impl, hipStream_t s) {
   // tall node-row problems (Linear forward, input gradient): the 160x128 LDS-DMA kernel (gemm_tall.hip)
-  if (!AK && impl == HICGAT_GEMM_F32 && splits == 1 && M >= 1024 && tall_enabled() &&
+  if (!AK && splits == 1 && M >= 1024 &&
       (int64_t)((M + 159) / 160) * (N / 128) >= tall_min_tiles()) {
     const int rc = gemm_tall_launch(BK_, A, lda, B, ldb, C, ldc, M, N, K, bias, acc, s);
     if (rc != HICGAT_EUNSUPPORTED) return rc;
   }
-  if (impl != HICGAT_GEMM_F32 && x3_ok<AK, BK_>(A, lda, B, ldb, M, N, K)) {
-    // 128-row tiles when they alone give >= 2 blocks per CU, else 64-row tiles
-    const int64_t blocks128 = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
-    if (blocks128 >= 512) return launch_x3<128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
-    return launch_x3<64, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
-  }
-  if (impl == HICGAT_GEMM_X3) return HICGAT_EUNSUPPORTED;
   // tall row-major problems (M = node rows): 64 x 128 tiles keep >= 2 blocks per CU in flight;
   // square-ish weight gradients (M, N = features, K = rows split): 128 x 128
 #ifndef HICGAT_GEMM_TALL128
@@ -962,7 +686,8 @@ extern "C" int hicgat_gemm_ex(int a_kmajor, int b_kmajor, int M, int N, int K, c
                               const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc,
                               int accumulate, int splits, int impl, void *workspace, size_t workspace_bytes,
                               hicgat_stream_t stream) {
-  if (impl != HICGAT_GEMM_AUTO && impl != HICGAT_GEMM_F32 && impl != HICGAT_GEMM_X3) return HICGAT_EINVAL;
+  if (impl == HICGAT_GEMM_X3) return HICGAT_EUNSUPPORTED;   // the bf16 x3 split was measured slower and removed
+  if (impl != HICGAT_GEMM_AUTO && impl != HICGAT_GEMM_F32) return HICGAT_EINVAL;
   if (M < 0 || N < 0 || K < 0 || splits < 1) return HICGAT_EINVAL;
   if (M == 0 || N == 0) return HICGAT_OK;
   if (!A || !B || !C) return HICGAT_EINVAL;

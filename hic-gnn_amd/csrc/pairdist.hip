@@ -766,10 +766,7 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   float4 *part;
   double *mom;
   carve(workspace, tiles, 1, &part, &mom);
-  // HICGAT_PD_NOLDS=1 (A/B measurement only): read T straight into registers instead of the
-  // LDS-DMA tile image
-  static const bool nolds = getenv("HICGAT_PD_NOLDS") && atoi(getenv("HICGAT_PD_NOLDS")) != 0;
-  const bool vec = !nolds && (ldt % 4 == 0) && (t_col0 % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+  const bool vec = (ldt % 4 == 0) && (t_col0 % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                    ldt >= (int64_t)nb * BT - t_col0;
   if (nt > 0) {
     // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only

@@ -13,14 +13,7 @@ from . import _lib
 
 # name -> list of (start, end) torch.cuda.Event pairs recorded around launches (bench.py)
 TIMERS = None
-GEMM_IMPLS = {"auto": 0, "f32": 1, "x3": 2}
-# the product default is the plain fp32 MFMA GEMM; HICGAT_GEMM=auto opts into the fp32-accurate x3
-# split where it applies (10-25 % faster GEMMs, profiles/r01_kbench_x3_sliced.txt)
-GEMM_DEFAULT = "f32"
-# lin_l + logits (a2): the tall 160x128 GEMM (gemm_tall.hip) and a separate logits pass (default,
-# 2.075 vs 2.095 ms per step) or HICGAT_LINATT=fused: the 64x256-tile kernel with the logits in its
-# epilogue
-LINATT_GEMM = os.environ.get("HICGAT_LINATT", "gemm") == "gemm"
+GEMM_F32 = 1   # include/hicgat.h HICGAT_GEMM_F32: fp32 MFMA (the only GEMM arithmetic)
 
 
 class _timed:
@@ -70,9 +63,7 @@ class HipKernels:
 
     def __init__(self):
         self.lib = _lib.lib()
-        # matrix-core arithmetic of the GEMMs (include/hicgat.h HICGAT_GEMM_*): 0 auto (x3 where
-        # supported), 1 fp32 MFMA only, 2 x3 only
-        self.gemm_impl = GEMM_IMPLS[os.environ.get("HICGAT_GEMM", GEMM_DEFAULT)]
+        self.gemm_impl = GEMM_F32
 
     # -- a2 ---------------------------------------------------------------------------------------
     def linear_att(self, x, W, att_l, att_r, h=None):
@@ -84,8 +75,10 @@ class HipKernels:
         assert h.shape == (N, H * C) and h.is_contiguous()
         a_src = torch.empty((N, H), dtype=torch.float32, device=x.device)
         a_dst = torch.empty_like(a_src)
-        if (self.gemm_impl != 1 or LINATT_GEMM) and N >= 32 and F % 4 == 0 and x.stride(0) % 4 == 0:
-            # x3 (or, HICGAT_LINATT=gemm, the 160x128 fp32) GEMM into h, then the logits in one pass over h
+        if N >= 32 and F % 4 == 0 and x.stride(0) % 4 == 0:
+            # the tall 160x128 GEMM into h, then the logits in one pass over h (2.075 vs 2.095 ms per
+            # step for the 64x256-tile hicgat_gat_linear_att with the logits in its epilogue, which
+            # takes the small / unaligned cases)
             st = _lib.stream(x.device)
             with _timed("gat_linear_att"):
                 _lib.check(self.lib.hicgat_gemm_ex(0, 0, N, H * C, F, P(x), x.stride(0), P(W), W.stride(0), None, P(h),

@@ -34,40 +34,15 @@ def _sink(p):
 # is returned to autograd is consumed on the backward's stream and must be produced there.
 _SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": [], "grouped": 0, "jobs": []}
 _SIDE_LOCK = threading.Lock()
-OVERLAP_DEFAULT = os.environ.get("HICGAT_OVERLAP", "1") != "0"
-# LayerNorm dgamma/dbeta reductions queued with the deferred side work (1, default: 1.959 / 1.945 vs
-# 1.965 / 1.961 ms per step, two A/B pairs, profiles/r02d_ab_step.txt) or inside the row-pass call (0)
-LN_SIDE = os.environ.get("HICGAT_LN_SIDE", "1") != "0"
-# bias column sums / GAT param_grad on the side stream (else on the backward's stream)
-SMALL_SIDE = os.environ.get("HICGAT_SMALL_SIDE", "1") != "0"
-# Deferred side work (HICGAT_DEFER=1, the default): the tail's parameter-gradient launches are
-# queued and issued by ``side_flush`` beside the GAT source-side gather pass (forked after the
-# gather-free row pass).  Issued as they come instead (HICGAT_DEFER=0), a captured step's graph
-# places some of them in front of the aggregation backward on its queue: 2.036 vs 2.060 ms per
-# graph step.
-DEFER_DEFAULT = os.environ.get("HICGAT_DEFER", "1") != "0"
-SIDE_PRIO = int(os.environ.get("HICGAT_SIDE_PRIO", "0"))
-# lin_l's dW on the backward's own stream right after the source pass (1, default: 2.011 / 2.014 ms
-# per step) or queued onto the side stream behind the tail's dW work (0: 2.037 / 2.037 ms)
-LINL_MAIN = os.environ.get("HICGAT_LINL_MAIN", "1") != "0"
-# the GAT param_grad (datt_l, datt_r, dbias column sums) on a second side stream beside lin_l's dW
-# (1: measured 2.06 vs 1.98 ms per step) or on the backward's stream in front of it (0, default)
-PG_SIDE = os.environ.get("HICGAT_PG_SIDE", "0") != "0"
-# issue order of the deferred side work: "fifo" (backward order, default) or "size" (largest first:
-# with the full-grid source pass the big dW GEMMs then wait for it to drain, 2.007 vs 1.978 ms per
-# step; with HICGAT_SRC_WGS=2 they all finish beside it, but the thinner gather takes 611 vs 489 us
-# and the step is the same, 1.953 vs 1.953-1.959 ms median)
-SIDE_ORDER = os.environ.get("HICGAT_SIDE_ORDER", "fifo")
-# deferred side work of at least this many multiply-adds (rows * m * n of a dW GEMM) goes to a
-# second side stream of its own (0: one side stream for all of it)
-SIDE_BIG = float(os.environ.get("HICGAT_SIDE_BIG", "0"))
-# the GAT param_grad split (1): datt_dst / dbias on the second side stream beside the source pass,
-# only datt_src behind it -- measured slower (2.02-2.03 vs 1.95-1.96 ms per step: the 82 MB stream
-# beside the gather slows it more than the 30 us it takes off the tail); 0 (default): all three
-# behind the source pass
-PG_SPLIT = os.environ.get("HICGAT_PG_SPLIT", "0") != "0"
-# side streams for the single-GPU step's deferred side work (side_flush lanes; 1 = one chain)
-SIDE_LANES = int(os.environ.get("HICGAT_SIDE_LANES", "1"))
+OVERLAP_DEFAULT = True
+# The tail's parameter-gradient launches (split-K dW GEMMs with their bias sums, the LayerNorm
+# dgamma/dbeta sums, bias column sums) are DEFERRED: queued, and issued by ``side_flush`` on the side
+# stream beside the GAT source-side gather (forked after the gather-free row pass).  Issued as they
+# come, a captured step's graph placed some of them in front of the aggregation backward on its
+# queue (2.036 vs 2.060 ms per step).  Measured slower and removed: largest-first
+# or small-first issue order, the big dW GEMMs on a stream of their own or on the backward's stream,
+# lin_l's dW queued behind the side work, the GAT param_grad on a second side stream or split around
+# the gather, the source pass in row chunks, two side lanes on one GPU.
 
 
 def side_begin():
@@ -97,50 +72,31 @@ def side_flush(after=None, lanes=1):
 
     ``lanes`` > 1 spreads the launches over that many side streams (largest work first, each to the
     least-loaded lane; every launch writes its own parameters' gradients, so they are independent):
-    a rank's shard of the multi-GPU step has a gather window too short for the tail's ~13 queued
-    launches in one chain (170 us at P = 8, profiles/r03i_simprof_xagg_P8_rank0_timeline.txt).  The
-    single-GPU step keeps one lane (a second one measured slower there)."""
+    a rank's shard of the multi-GPU slab step has a gather window too short for the tail's queued
+    launches in one chain.  The single-GPU step keeps one lane (a second one measured slower there,
+    DESIGN section 7)."""
     with _SIDE_LOCK:
         queue, _SIDE["queue"] = _SIDE["queue"], []
     if not queue:
         return
-    if lanes > 1 and SIDE_BIG == 0:
-        n = min(lanes, len(_FLUSH_LANES))
-        load, parts = [0] * n, [[] for _ in range(n)]
+    n = max(1, min(lanes, len(_FLUSH_LANES)))
+    load, parts = [0] * n, [[] for _ in range(n)]
+    if n == 1:
+        parts[0] = queue                     # backward order
+    else:
         for item in sorted(queue, key=lambda q: -q[2]):
             k = min(range(n), key=lambda a: (load[a], len(parts[a])))
             parts[k].append(item)
             load[k] += item[2]
-        for lane, items in zip(_FLUSH_LANES, parts):
-            # reductions without a GEMM (the LayerNorm dgamma/dbeta column sums: inputs ready, a few
-            # us each) first in their lane, then the GEMMs (behind the GEMMs they were the last ~30 us
-            # of a P = 8 rank step in profiles/r03v_simprof_xagg_P8_rank0_timeline.txt; the rank step
-            # measured even, 0.581 / 0.564 vs 0.569 / 0.584 ms: streams beyond the box's 4 hardware
-            # queues share one, and a stream waiting on an event stalls the others behind it)
+    for lane, items in zip(_FLUSH_LANES, parts):
+        if n > 1:
+            # reductions without a GEMM (LayerNorm dgamma/dbeta sums: inputs ready, a few us each)
+            # first in their lane, then the GEMMs
             items = [q for q in items if q[2] < SMALL_WORK] + [q for q in items if q[2] >= SMALL_WORK]
-            if items:
-                with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
-                    for fn, _, _ in items:
-                        fn()
-        return
-    if SIDE_ORDER == "size":
-        queue.sort(key=lambda q: -q[2])
-    elif SIDE_ORDER == "small_first":
-        # the reductions without a GEMM (LayerNorm dgamma/dbeta, work 0) first: their inputs are
-        # ready before the gather starts, so they finish beside it instead of delaying the big dW
-        # GEMMs that run after it
-        queue.sort(key=lambda q: q[2] > 0)
-    lanes = [queue]
-    if SIDE_BIG > 0:
-        # the big dW GEMMs on their own side stream: they start as the gather drains instead of
-        # queueing behind the small launches that crawl beside it
-        lanes = [[q for q in queue if q[2] < SIDE_BIG], [q for q in queue if q[2] >= SIDE_BIG]]
-    for lane, items in zip((0, 2), lanes):
-        if not items:
-            continue
-        with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
-            for fn, _, _ in items:
-                fn()
+        if items:
+            with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
+                for fn, _, _ in items:
+                    fn()
 
 
 def side_record():
@@ -220,12 +176,6 @@ def overlapped_param_grads(enabled=None):
         side_join()
 
 
-# deferred side work of at least this many multiply-adds runs at once on the backward's own stream
-# instead (A/B knob, 0 = off): the first tail block's 512 x 512 dW ahead of the GAT backward, so that
-# after the source gather only lin_l's dW is left
-BIG_MAIN = float(os.environ.get("HICGAT_BIG_MAIN", "0"))
-
-
 def _param_launch(fn, *keep, small=False, work=0, job=None):
     """Launch a sink-bound parameter-gradient kernel ``fn()``: now on the current stream when not
     overlapping; queued for ``side_flush`` when deferring (``work``: its size, the issue order);
@@ -236,19 +186,11 @@ def _param_launch(fn, *keep, small=False, work=0, job=None):
         with _SIDE_LOCK:
             _SIDE["jobs"].append((job, keep))
         return
-    if not _SIDE["on"] or (BIG_MAIN > 0 and work >= BIG_MAIN):
+    if not _SIDE["on"]:
         fn()
-    elif DEFER_DEFAULT:
+    else:
         with _SIDE_LOCK:
             _SIDE["queue"].append((fn, keep, work))
-    else:
-        with (_side_small(*keep) if small else _side(*keep)):
-            fn()
-
-
-def _side_small(*keep):
-    """``_side`` for the small parameter reductions (column sums), unless SMALL_SIDE is off."""
-    return _side(*keep) if SMALL_SIDE else contextlib.nullcontext()
 
 
 def _side(*keep, after=None, lane=0):
@@ -256,8 +198,7 @@ def _side(*keep, after=None, lane=0):
     current stream, or from the event ``after``) while overlapping, else a no-op.  ``keep`` are
     the inputs the side kernels read; they stay referenced until the join so the caching
     allocator cannot hand their memory to a later backward kernel while the side stream still
-    reads it.  HICGAT_SIDE_PRIO sets the side streams' priority (-1 = high: measured no different
-    from the default 0 in graph replay)."""
+    reads it."""
     if not _SIDE["on"]:
         return contextlib.nullcontext()
     cur = torch.cuda.current_stream()
@@ -266,7 +207,7 @@ def _side(*keep, after=None, lane=0):
     with _SIDE_LOCK:
         side = _SIDE["streams"].get(key)
         if side is None:
-            side = _SIDE["streams"][key] = torch.cuda.Stream(device=dev, priority=SIDE_PRIO)
+            side = _SIDE["streams"][key] = torch.cuda.Stream(device=dev)
         _SIDE["mains"].setdefault(key, cur)
         _SIDE["hold"].extend(keep)
     if after is not None:
@@ -283,17 +224,6 @@ def _dev_check(*ts):
 
 
 _ACTS = {None: 0, "relu": 1}
-
-
-# row chunks of the GAT source pass (see _GATConvFn.backward); 1 = one launch over all rows
-SRC_CHUNKS = int(os.environ.get("HICGAT_SRC_CHUNKS", "1"))
-
-
-def _src_chunks(n, chunks=None):
-    """[(r0, r1)] -- ``chunks`` near-equal row ranges (fewer when a chunk would be under 1024 rows)."""
-    c = max(1, min(SRC_CHUNKS if chunks is None else chunks, n // 1024))
-    b = [n * i // c for i in range(c + 1)]
-    return [(b[i], b[i + 1]) for i in range(c) if b[i + 1] > b[i]] or [(0, n)]
 
 
 class _GATConvFn(torch.autograd.Function):
@@ -350,51 +280,27 @@ class _GATConvFn(torch.autograd.Function):
         pW, pl, pr, pb = ctx.params
         sinks = (_sink(pl), _sink(pr), _sink(pb) if ctx.has_bias else None)
         use_sinks = all(t is not None for t in sinks)
-        chunks = _src_chunks(N) if ctx.tiles is None else [(0, N)]
-        pg_split = use_sinks and PG_SPLIT and _SIDE["on"] and len(chunks) == 1
-        if pg_split:
-            # datt_dst and dbias need only the row pass's outputs: summed on the second side stream
-            # beside the source pass; datt_src (da_src) is left behind it
-            with _side(h, dout, row_stats, lane=1):
-                K.param_grad(h, dout, None, row_stats, H, out=(None, sinks[1].view(-1), sinks[2]), accumulate=True)
-        gW = _sink(pW) if ctx.needs_input_grad[1] else None
-        # The source pass runs in row chunks; each chunk's parameter-gradient share (param_grad
-        # partial column sums, dW += dh_c^T x_c) is issued right after it -- on the side stream
-        # when overlapping -- so only the last chunk's share is left after the gathers (the
-        # backward's tail).  The sink and autograd paths add the same partials in the same order.
-        datt_l = datt_r = dbias = dW = None
-        for c, (r0, r1) in enumerate(chunks):
-            if ctx.tiles is not None:
-                K.agg_bwd_src_tiled(ctx.tiles, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
-            else:
-                K.agg_bwd_src(rowptr, col, r0, r1, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
-            if c == 0:
-                side_flush(after=fork, lanes=SIDE_LANES)
-            rows = slice(r0, r1)
-            if use_sinks:
-                # on a second side stream (PG_SIDE), beside lin_l's dW GEMM on this one, or in front of it
-                with (_side(h, dout, da_src, row_stats, lane=1) if PG_SIDE else contextlib.nullcontext()):
-                    K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                                 out=((sinks[0].view(-1), None, None) if pg_split else
-                                      (sinks[0].view(-1), sinks[1].view(-1), sinks[2])), accumulate=True)
-            else:
-                datt_l, datt_r, dbias = K.param_grad(h[rows], dout[rows], da_src[rows], row_stats[rows], H,
-                                                     out=None if c == 0 else (datt_l, datt_r, dbias),
-                                                     accumulate=c > 0)
-            if ctx.needs_input_grad[1]:
-                if gW is not None:
-                    if LINL_MAIN:   # right behind the source pass on this stream
-                        weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True)
-                    else:           # queued: on the side stream after the tail's dW work
-                        _param_launch(lambda rows=rows: weight_grad(K, dh[rows], x[rows], out=gW, accumulate=True),
-                                      dh, x)
-                else:
-                    dW = weight_grad(K, dh[rows], x[rows], out=dW, accumulate=dW is not None)
-        if not use_sinks:
+        if ctx.tiles is not None:
+            K.agg_bwd_src_tiled(ctx.tiles, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+        else:
+            K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+        side_flush(after=fork)
+        # after the gathers: the GAT column sums, then lin_l's dW on this stream (beside the side
+        # stream's first-block dW)
+        if use_sinks:
+            K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
+                         accumulate=True)
+            datt_l = datt_r = dbias = None
+        else:
+            datt_l, datt_r, dbias = K.param_grad(h, dout, da_src, row_stats, H)
             datt_l, datt_r = datt_l.view(al.shape), datt_r.view(ar.shape)
             dbias = dbias if ctx.has_bias else None
-        else:
-            datt_l = datt_r = dbias = None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            gW = _sink(pW)
+            dW = weight_grad(K, dh, x, out=gW, accumulate=gW is not None)
+            if gW is not None:
+                dW = None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")
@@ -443,9 +349,9 @@ def _wb_grad_to(K, pW, pb, dy, x, need_w=True, need_b=True):
     (``hicgat_gemm_wgrad``, db from the staged dY tiles).  Into the parameters' sinks (returns
     (None, None); on the side stream when overlapping) or new tensors (returned).  Falls back to
     separate GEMM / column-sum launches when only one of the two is wanted, when the sinks are
-    mixed, or when the x3 GEMM arithmetic was selected (HICGAT_GEMM)."""
+    mixed."""
     need_b = need_b and pb is not None
-    if not need_w or K.gemm_impl != 1:
+    if not need_w:
         dW = _weight_grad_to(K, pW, dy, x) if need_w else None
         db = _bias_grad_to(K, pb, dy) if need_b else None
         return dW, db
@@ -575,7 +481,7 @@ class _LnReluResFn(torch.autograd.Function):
         dz = dz.contiguous()
         dy = torch.empty(y.shape, dtype=torch.float32, device=y.device)
         sg, sb = _sink(ctx.params[0]), _sink(ctx.params[1])
-        if sg is not None and sb is not None and not (LN_SIDE and _SIDE["on"]):
+        if sg is not None and sb is not None and not _SIDE["on"]:
             K.ln_relu_res_bwd(dz, y, stats, gamma, beta, dy, sg, sb, accumulate=True)
             dgamma = dbeta = None
         elif sg is not None and sb is not None:
@@ -650,7 +556,7 @@ class _DualLnReluResFn(torch.autograd.Function):
         dY = torch.empty((M, 2 * w), dtype=torch.float32, device=dz.device)
         sg, sb = _sink(pg), _sink(pb)
         dgamma = dbeta = None
-        if sg is not None and sb is not None and not (LN_SIDE and _SIDE["on"]):
+        if sg is not None and sb is not None and not _SIDE["on"]:
             K.ln_relu_res_bwd(dz, Y[:, :w], stats, gamma, beta, dY[:, :w], sg, sb, accumulate=True, dres=dY[:, w:])
         elif sg is not None and sb is not None:
             ws = K.ln_workspace(w, dz.device)
@@ -675,7 +581,7 @@ def _dual_param_grads(K, W1, b1, W2, b2, dY, x):
     dW1 = dW2 = db1 = db2 = None
     w_pair = sW1 is not None and sW2 is not None and _adjacent(sW1, sW2)
     b_pair = sb1 is not None and sb2 is not None and _adjacent(sb1, sb2)
-    if w_pair and b_pair and K.gemm_impl == 1:
+    if w_pair and b_pair:
         # [dW1; dW2] and [db1; db2] of the pair in ONE GEMM launch (hicgat_gemm_wgrad)
         gWj, gbj, sp = _joined(sW1, sW2), _joined(sb1, sb2), _splits(2 * w, x.shape[1], M)
         _param_launch(lambda: K.wgrad(dY, x, gWj, gbj, accumulate=True, splits=sp), dY, x,

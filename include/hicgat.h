@@ -339,14 +339,10 @@ int hicgat_gemm(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A,
                 const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,
                 int splits, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
 size_t hicgat_gemm_workspace_bytes(int M, int N, int splits);
-/* The same GEMM with the matrix-core arithmetic chosen explicitly (hicgat_gemm = HICGAT_GEMM_AUTO):
- *   HICGAT_GEMM_F32: v_mfma_f32_32x32x2_f32 (fp32 products, fp32 accumulate);
- *   HICGAT_GEMM_X3:  every fp32 operand split exactly into three bf16 terms, the six products of
- *     order <= 2 on v_mfma_f32_32x32x16_bf16 with fp32 accumulate -- fp32-GEMM accuracy (the dropped
- *     terms are O(2^-24 |a b|)) at 2.7x the fp32 matrix rate; needs 16-B aligned operands, float4
- *     rows (K, or the row dim of a K-major operand, a multiple of 4), N >= 64 and M >= 32, else
- *     HICGAT_EUNSUPPORTED;
- *   HICGAT_GEMM_AUTO: X3 where supported, else F32. */
+/* The same GEMM with the matrix-core arithmetic named explicitly: HICGAT_GEMM_F32 (= AUTO, the
+ * only one): v_mfma_f32_32x32x2_f32, fp32 products, fp32 accumulate.  HICGAT_GEMM_X3 (a three-way
+ * bf16 operand split on the bf16 matrix cores, round 1-3) measured slower per step and was removed:
+ * HICGAT_EUNSUPPORTED. */
 enum { HICGAT_GEMM_AUTO = 0, HICGAT_GEMM_F32 = 1, HICGAT_GEMM_X3 = 2 };
 int hicgat_gemm_ex(int a_kmajor, int b_kmajor, int M, int N, int K, const float *A, int64_t lda,
                    const float *B, int64_t ldb, const float *bias, float *C, int64_t ldc, int accumulate,

@@ -1,6 +1,6 @@
 """GPU: the alternative fast kernels against the reference-form kernels on the same inputs.
 
-* the x3 (three-way bf16 split) GEMM vs fp64 and the fp32-MFMA GEMM;
+* the fp32-MFMA GEMM family vs fp64 (every layout / tile path), the fused linear + logits kernel;
 * the split LayerNorm backward (parameter reduction on a second stream) vs the one-call form.
 Tolerances as in test_gpu_parity.py (max-abs error relative to the tensor's max magnitude).
 """
@@ -25,19 +25,18 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
 
 
-# ---------------------------------------------------------------- x3 GEMM (csrc/gemm.hip)
+# ---------------------------------------------------------------- fp32 GEMM family (csrc/gemm.hip)
 @pytest.mark.parametrize("a_km,b_km,m,n,k,splits", [
-    (0, 0, 20000, 512, 512, 1),    # lin_l / Linear forward
+    (0, 0, 20000, 512, 512, 1),    # lin_l / Linear forward (the tall 160 x 128 kernel)
     (0, 0, 3001, 256, 512, 1),     # ragged M
     (0, 1, 5003, 512, 256, 1),     # input gradient
     (1, 1, 512, 512, 20000, 64),   # weight gradient, split K
     (1, 1, 256, 512, 4999, 7),     # ragged K and splits
     (0, 0, 130, 64, 20, 1),        # K not a multiple of the 16-deep K-step
 ])
-def test_gemm_x3_is_as_accurate_as_fp32(a_km, b_km, m, n, k, splits):
-    """The three-way bf16 split GEMM against fp64: error at most ~1.5x that of the fp32-MFMA kernel
-    (which the reference's fp32 sgemm matches in class) and below the GEMM tolerance of
-    test_gpu_parity.py; bias / accumulate epilogues identical in form."""
+def test_gemm_fp32_matches_fp64(a_km, b_km, m, n, k, splits):
+    """Every layout / tile path of the fp32-MFMA GEMM against fp64, with the bias and accumulate
+    epilogues (the GEMM tolerance of test_gpu_parity.py)."""
     import hicgat
     K = hicgat.kernels.default()
     torch.manual_seed(m + n + k)
@@ -47,58 +46,56 @@ def test_gemm_x3_is_as_accurate_as_fp32(a_km, b_km, m, n, k, splits):
     ref = (A.double().t() if a_km else A.double()) @ (B.double() if b_km else B.double().t())
     if bias is not None:
         ref = ref + bias.double()
-    err = {}
-    for impl in (1, 2):
-        C = torch.full((m, n), float("nan"), device=DEV)
-        K.gemm(a_km, b_km, m, n, k, A, B, C, bias=bias, splits=splits, impl=impl)
-        err[impl] = _rel(C.cpu(), ref.cpu())
-    assert err[2] <= 1.5 * err[1] + 1e-7, err
-    assert err[2] < 5e-6 * max(1.0, (k / splits / 512) ** 0.5), err
+    tol = 5e-6 * max(1.0, (k / splits / 512) ** 0.5)
+    C = torch.full((m, n), float("nan"), device=DEV)
+    K.gemm(a_km, b_km, m, n, k, A, B, C, bias=bias, splits=splits)
+    assert _rel(C.cpu(), ref.cpu()) < tol
     acc = torch.ones(m, n, device=DEV)
-    K.gemm(a_km, b_km, m, n, k, A, B, acc, bias=bias, accumulate=True, splits=splits, impl=2)
-    assert _rel(acc.cpu(), (ref + 1).cpu()) < 5e-6 * max(1.0, (k / splits / 512) ** 0.5)
+    K.gemm(a_km, b_km, m, n, k, A, B, acc, bias=bias, accumulate=True, splits=splits)
+    assert _rel(acc.cpu(), (ref + 1).cpu()) < tol
 
 
-def test_gemm_x3_unsupported_shapes_fall_back():
-    """N < 64 (dense3) or unaligned rows: impl x3 refuses (HICGAT_EUNSUPPORTED), auto runs fp32."""
+def test_gemm_x3_arithmetic_is_refused():
+    """HICGAT_GEMM_X3 was removed (measured slower per step): the ABI refuses it loudly."""
     import hicgat
     from hicgat import _lib
     K = hicgat.kernels.default()
     A = torch.randn(777, 64, device=DEV)
-    W = torch.randn(3, 64, device=DEV)
-    C = torch.empty(777, 3, device=DEV)
+    W = torch.randn(64, 64, device=DEV)
+    C = torch.empty(777, 64, device=DEV)
     with pytest.raises(_lib.HicgatError):
-        K.gemm(0, 0, 777, 3, 64, A, W, C, impl=2)
-    K.gemm(0, 0, 777, 3, 64, A, W, C, impl=0)
-    assert _rel(C.cpu(), (A.double() @ W.double().t()).cpu()) < 5e-6
+        K.gemm(0, 0, 777, 64, 64, A, W, C, impl=2)
 
 
-def test_linear_att_x3_matches_fused_fp32_kernel():
-    """The GATConv lin_l + logits as x3 GEMM + logits pass vs the fused fp32-MFMA kernel."""
+def test_linear_att_fused_kernel_matches_gemm_path():
+    """hicgat_gat_linear_att (the 64x256-tile GEMM with the logits in its epilogue) vs the product
+    path (tall GEMM + logits pass) and fp64."""
     import hicgat
-    from hicgat import kernels
+    from hicgat import _lib
+    K = hicgat.kernels.default()
     torch.manual_seed(2)
     n = 4097
     x = torch.randn(n, 512, device=DEV) * 0.1
     W = torch.randn(512, 512, device=DEV) * 0.05
     al = torch.randn(1, 2, 256, device=DEV)
     ar = torch.randn(1, 2, 256, device=DEV)
-    f32, x3 = kernels.HipKernels(), kernels.HipKernels()
-    f32.gemm_impl, x3.gemm_impl = 1, 2
-    h1, s1, d1 = f32.linear_att(x, W, al, ar)
-    h2, s2, d2 = x3.linear_att(x, W, al, ar)
+    h1, s1, d1 = K.linear_att(x, W, al, ar)
+    h2, s2, d2 = torch.empty_like(h1), torch.empty_like(s1), torch.empty_like(d1)
+    P = _lib.ptr
+    _lib.check(K.lib.hicgat_gat_linear_att(P(x), P(W), P(al), P(ar), n, 512, 2, 256, P(h2), P(s2), P(d2),
+                                           _lib.stream(x.device)), "hicgat_gat_linear_att")
     href = x.double() @ W.double().t()
-    assert _rel(h2.cpu(), href.cpu()) <= 1.5 * _rel(h1.cpu(), href.cpu()) + 1e-7
     hv = href.view(n, 2, 256)
-    assert _rel(s2.cpu(), (hv * al.double()).sum(-1).cpu()) < 1e-5
-    assert _rel(d2.cpu(), (hv * ar.double()).sum(-1).cpu()) < 1e-5
-    assert hicgat  # silence
+    for h, s, d in ((h1, s1, d1), (h2, s2, d2)):
+        assert _rel(h.cpu(), href.cpu()) < 5e-6
+        assert _rel(s.cpu(), (hv * al.double()).sum(-1).cpu()) < 1e-5
+        assert _rel(d.cpu(), (hv * ar.double()).sum(-1).cpu()) < 1e-5
 
 
 @pytest.mark.parametrize("W", [64, 128, 256])
 def test_ln_bwd_split_params_same_bits(W):
     """hicgat_ln_relu_res_bwd with dgamma = dbeta = NULL + hicgat_ln_relu_res_bwd_params on a
-    second stream (the HICGAT_LN_SIDE form) == the one-call backward, bit for bit."""
+    second stream (the deferred side-work form) == the one-call backward, bit for bit."""
     from hicgat import kernels
     K = kernels.default()
     M = 3001

@@ -96,6 +96,9 @@ for S in "$@"; do
       R=${S#kb:}; J=${R%%:*}; L=${R#*:}
       timeout -k 10 300 python tools/kbench.py --only "$J" --libs "$L" --reps 20 --rounds 3 > gpurun_out/${T}_kbench.txt 2>&1 || exit $?
       cat gpurun_out/${T}_kbench.txt | grep " med " ;;
+    probe)
+      timeout -k 10 300 python tools/xagg_probe.py > gpurun_out/${T}_probe.txt 2>&1 || exit $?
+      cat gpurun_out/${T}_probe.txt | tail -12 ;;
     simprof|simprof_ag|simprof_xa)
       M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \

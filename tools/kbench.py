@@ -67,12 +67,6 @@ def main():
         if not _tiles:
             _tiles["t"] = hicgat.graph.build_tiles(adj.rowptr32, adj.col32, 0, n, n, hicgat.graph.TILE_MIN or 64)
         return _tiles["t"]
-    def _with_impl(K, impl, fn):
-        saved, K.gemm_impl = K.gemm_impl, impl
-        try:
-            return fn()
-        finally:
-            K.gemm_impl = saved
     kset = []
     for path in libs:
         lib = ctypes.CDLL(path)
@@ -81,11 +75,10 @@ def main():
             fn.restype, fn.argtypes = res, args
         K = kernels.HipKernels.__new__(kernels.HipKernels)
         K.lib = lib
-        K.gemm_impl = 0              # GEMMs: auto (x3 where supported); "#f32" / "#x3" jobs force one
+        K.gemm_impl = 1              # fp32 MFMA
         kset.append((os.path.basename(path), K))
     jobs = {
         "gat_linear_att": lambda K: K.linear_att(x, W, al, ar),
-        "gat_linear_att#f32": lambda K: _with_impl(K, 1, lambda: K.linear_att(x, W, al, ar)),
         "gat_agg_fwd": lambda K: K.agg_fwd(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, out, rs),
         "gat_agg_fwd_train": lambda K: K.agg_fwd_act(adj.rowptr32, adj.col32, 0, n, h, a_s, a_d, b, 0.2, 1, out,
                                                      out2, rs),
@@ -107,16 +100,6 @@ def main():
         "gemm_fwd_densea": lambda K: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba),
         "gemm_dx_densea": lambda K: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa),
         "gemm_dw_densea": lambda K: hicgat.ops.weight_grad(K, ya, out),
-        **{f"gemm_fwd_densea#{nm}": (lambda K, i=i: K.gemm(0, 0, n, 256, 512, out, Wa, ya, bias=ba, impl=i))
-           for nm, i in (("f32", 1), ("x3", 2))},
-        **{f"gemm_fwd_512#{nm}": (lambda K, i=i: K.gemm(0, 0, n, 512, 512, x, W, dh, impl=i))
-           for nm, i in (("f32", 1), ("x3", 2))},
-        **{f"gemm_dx_densea#{nm}": (lambda K, i=i: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa, impl=i))
-           for nm, i in (("f32", 1), ("x3", 2))},
-        **{f"gemm_dw_512x512#{nm}": (lambda K, i=i: hicgat.ops.weight_grad(K, dh, x, impl=i))
-           for nm, i in (("f32", 1), ("x3", 2))},
-        **{f"gemm_dw_densea#{nm}": (lambda K, i=i: hicgat.ops.weight_grad(K, ya, out, impl=i))
-           for nm, i in (("f32", 1), ("x3", 2))},
         "torch_dw_densea": lambda K: ya.t().mm(out),
         "torch_fwd_densea": lambda K: torch.nn.functional.linear(out, Wa, ba),
     }
