@@ -358,7 +358,8 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
 // da_src_j = sum over the rank's edges (i, j) of ds_ij, so g_src^h = sum_i sum_j ds_ij^h x_j: the
 // edge pass that forms ds_ij has x_j in registers and adds ds_ij^h x_j into the block's running sum
 // -- no per-edge ds array, no transposed (slab) structure, no second gather.
-// Persistent blocks: logical block b (XCD-aware map) takes own rows [b R / G, (b+1) R / G) in order;
+// Workgroup b (XCD-aware map) takes own rows [b R / G, (b+1) R / G) in order (G = rows / RPB: a
+// persistent grid of 512 workgroups -- 2 per CU, 2 waves per SIMD -- left the gathers latency-bound);
 // per row its dxa (4 KiB) goes to LDS; 16-lane groups take the row's edges g, g + 16, ... (lane t of a
 // group holds float4 t, t + 16, ..., t + 112 of x_j); the two head dots are summed over the group by
 // DPP (sum16), then y^h += ds^h x_j per lane (64 accumulators).  At the end the 16 group sums are
@@ -376,7 +377,10 @@ __device__ __forceinline__ float row_sum16(float v) {   // every lane of a 16-la
   v += dpp_row<0xB1>(v);    // quad_perm [1,0,3,2]
   return v;
 }
-constexpr int kEdgeAccBlocks = 512;   // persistent blocks (partial rows of g_src)
+#ifndef HICGAT_EDGE_RPB
+#define HICGAT_EDGE_RPB 2   // own rows per workgroup of the edge pass (= partial rows of g_src: rows / RPB)
+#endif
+__host__ __device__ inline int edge_acc_blocks(int rows) { return rows <= 0 ? 1 : (rows + HICGAT_EDGE_RPB - 1) / HICGAT_EDGE_RPB; }
 __global__ __launch_bounds__(256) void xagg_edge_acc_kernel(const int *__restrict__ rowptr,
                                                             const int *__restrict__ col, int row_begin,
                                                             int row_end, const float *__restrict__ x,
@@ -689,7 +693,7 @@ extern "C" int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N
   return HICGAT_OK;
 }
 
-extern "C" int hicgat_xagg_edge_acc_blocks(void) { return kEdgeAccBlocks; }
+extern "C" int hicgat_xagg_edge_acc_blocks(int rows) { return edge_acc_blocks(rows); }
 
 extern "C" int hicgat_xagg_edge_acc(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C,
                                     int row_begin, int row_end, const float *x, const float *a_src,
@@ -699,7 +703,8 @@ extern "C" int hicgat_xagg_edge_acc(const int32_t *rowptr, const int32_t *col, i
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (!rowptr || !col || !x || !a_src || !a_dst || !row_stats || !dxa || !gpart) return HICGAT_EINVAL;
   // rows == 0 still writes the (zero) partial rows: the column sum that follows reads all of them
-  hipLaunchKernelGGL(xagg_edge_acc_kernel, dim3(kEdgeAccBlocks), dim3(256), 0, (hipStream_t)stream, rowptr, col,
+  hipLaunchKernelGGL(xagg_edge_acc_kernel, dim3(edge_acc_blocks(row_end - row_begin)), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col,
                      row_begin, row_end, x, a_src, a_dst, row_stats, dxa, neg_slope, xa2, gpart);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;

@@ -96,7 +96,7 @@ SIGNATURES = {
                                  c_f, c_p, c_p]),
     "hicgat_xagg_edge_acc": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p,
                                      c_p, c_f, c_p, c_p]),
-    "hicgat_xagg_edge_acc_blocks": (c_int, []),
+    "hicgat_xagg_edge_acc_blocks": (c_int, [c_int]),
     "hicgat_xagg_slab_workspace_bytes": (c_sz, []),
     "hicgat_xagg_slab_sum": (c_int, [c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),

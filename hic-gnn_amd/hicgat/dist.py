@@ -324,7 +324,7 @@ class ShardedTrainer:
             self.O = torch.zeros((Rl, D), **f32)                            # relu(out): the tail's input
             self.dout_l = torch.zeros((Rl, D), **f32)
             self.dxa = torch.zeros((Rl, 2 * F), **f32)
-            self.gpart = torch.zeros((kern.edge_acc_blocks(), 2 * F), **f32)   # g_src partial rows
+            self.gpart = torch.zeros((kern.edge_acc_blocks(Rl), 2 * F), **f32)   # g_src partial rows
             self.a_src = torch.zeros((N, self.H), **f32)
             self.a_dst = torch.zeros((N, self.H), **f32)
             self.g_src = torch.zeros(2 * F, **f32)

@@ -259,14 +259,15 @@ class HipKernels:
         also da_dst (row_stats[:, 6:8])."""
         N, F = x.shape
         assert dxa.shape == (r1 - r0, 2 * F) and dxa.is_contiguous()
-        assert gpart.shape == (self.edge_acc_blocks(), 2 * F) and gpart.is_contiguous()
+        assert gpart.shape == (self.edge_acc_blocks(r1 - r0), 2 * F) and gpart.is_contiguous()
         with _timed("gat_agg_bwd_dst"):
             _lib.check(self.lib.hicgat_xagg_edge_acc(P(rowptr), P(col), N, F, 2, F // 2, r0, r1, P(x), P(a_src),
                                                      P(a_dst), P(row_stats), P(dxa), P(xa2), float(ns), P(gpart),
                                                      _lib.stream(x.device)), "hicgat_xagg_edge_acc")
 
-    def edge_acc_blocks(self):
-        return int(self.lib.hicgat_xagg_edge_acc_blocks())
+    def edge_acc_blocks(self, rows):
+        """Partial rows of g_src that hicgat_xagg_edge_acc writes for ``rows`` own rows."""
+        return int(self.lib.hicgat_xagg_edge_acc_blocks(int(rows)))
 
     def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
         """da_src (every row, through the slab) and g_src [2, 512] = sum_j da_src_j x_j."""

@@ -182,14 +182,14 @@ int hicgat_xagg_edge(const int32_t *rowptr, const int32_t *col, int N, int F, in
                      const float *dxa, const float *xa2, float neg_slope, float *ds, hicgat_stream_t stream);
 /* The edge pass with the source side folded in (replaces hicgat_xagg_edge + hicgat_xagg_slab_sum in
  * the sharded step): g_src^h = sum_j da_src_j^h x_j = sum over the own rows' edges (i, j) of
- * ds_ij^h x_j, formed in the pass that computes ds_ij; written as hicgat_xagg_edge_acc_blocks()
+ * ds_ij^h x_j, formed in the pass that computes ds_ij; written as hicgat_xagg_edge_acc_blocks(rows)
  * partial rows gpart [blocks][1024] (head 0 | head 1) whose column sums are g_src (e.g. a
  * hicgat_param_grads_grouped column-sum job); with xa2, da_dst into row_stats[6:8] as hicgat_xagg_edge.
  * Deterministic (fixed row-to-block map and summation order). */
 int hicgat_xagg_edge_acc(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
                          int row_end, const float *x, const float *a_src, const float *a_dst, float *row_stats,
                          const float *dxa, const float *xa2, float neg_slope, float *gpart, hicgat_stream_t stream);
-int hicgat_xagg_edge_acc_blocks(void);
+int hicgat_xagg_edge_acc_blocks(int rows);
 size_t hicgat_xagg_slab_workspace_bytes(void);
 int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, const float *ds, const float *x,
                          float *da_src, float *g_src, void *workspace, size_t workspace_bytes,

@@ -260,7 +260,7 @@ class CpuKernels:
             s3 = row_stats[r0:r1, 3 * H:4 * H].double()
             row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
 
-    def edge_acc_blocks(self):
+    def edge_acc_blocks(self, rows):
         return 4
 
     def xagg_edge_acc(self, rowptr, col, r0, r1, x, a_src, a_dst, row_stats, dxa, ns, gpart, xa2=None):

@@ -84,7 +84,7 @@ def test_xagg_kernels_match_float64_reference(case):
         kern.xagg_edge(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs, dxa, 0.2, ds, xa2=X4[:, 1])
         # the edge pass with g_src folded in (the sharded step's form): g_src = column sums of its
         # partial rows, da_dst as above
-        gpart = torch.zeros((kern.edge_acc_blocks(), 1024), device=loc)
+        gpart = torch.zeros((kern.edge_acc_blocks(rows), 1024), device=loc)
         kern.xagg_edge_acc(t["rp"], t["cl"], r0, r1, t["x"], a_src, a_dst, rs_pre, dxa, 0.2, gpart, xa2=X4[:, 1])
         out[name].update(g_src_acc=gpart.double().sum(0), rs_edge_acc=rs_pre[r0:r1].clone())
         da_src = torch.zeros((n, 2), device=loc)
