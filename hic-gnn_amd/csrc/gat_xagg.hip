@@ -377,6 +377,43 @@ __device__ __forceinline__ float row_sum16(float v) {   // every lane of a 16-la
   v += dpp_row<0xB1>(v);    // quad_perm [1,0,3,2]
   return v;
 }
+// v of lane k of this lane's 16-lane DPP row (DPP row_share, gfx90a+: one VALU op); k is uniform
+template <int K>
+__device__ __forceinline__ int row_share_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ float row_share_f(float v) {
+  return __int_as_float(row_share_i<K>(__float_as_int(v)));
+}
+// (j, q0, q1) of edges k .. k + U - 1 of the group's chunk (k a multiple of U, < 16; a slot past the
+// row's end has q = 0 and j = the row itself, so it adds nothing)
+#ifndef HICGAT_EDGE_U
+#define HICGAT_EDGE_U 2   // edges per group per step of the edge pass (neighbour rows in flight)
+#endif
+constexpr int EU = HICGAT_EDGE_U;
+template <int U>
+__device__ __forceinline__ void row_share_n(int k, int j, float q0, float q1, int (&jj)[U], float (&qq0)[U],
+                                            float (&qq1)[U]) {
+  switch (k) {
+#define HICGAT_RS1(K, u)                                                        \
+  jj[u] = row_share_i<((K) + (u)) & 15>(j);                                     \
+  qq0[u] = row_share_f<((K) + (u)) & 15>(q0);                                   \
+  qq1[u] = row_share_f<((K) + (u)) & 15>(q1);
+#define HICGAT_RSN(K)                                                           \
+  case K:                                                                       \
+    HICGAT_RS1(K, 0)                                                            \
+    if constexpr (U > 1) { HICGAT_RS1(K, 1) }                                   \
+    if constexpr (U > 2) { HICGAT_RS1(K, 2) HICGAT_RS1(K, 3) }                  \
+    break;
+    HICGAT_RSN(0) HICGAT_RSN(1) HICGAT_RSN(2) HICGAT_RSN(3) HICGAT_RSN(4) HICGAT_RSN(5) HICGAT_RSN(6)
+    HICGAT_RSN(7) HICGAT_RSN(8) HICGAT_RSN(9) HICGAT_RSN(10) HICGAT_RSN(11) HICGAT_RSN(12) HICGAT_RSN(13)
+    HICGAT_RSN(14)
+    default: HICGAT_RSN(15)
+#undef HICGAT_RSN
+#undef HICGAT_RS1
+  }
+}
 #ifndef HICGAT_EDGE_RPB
 #define HICGAT_EDGE_RPB 2   // own rows per workgroup of the edge pass (= partial rows of g_src: rows / RPB)
 #endif
@@ -413,31 +450,58 @@ __global__ __launch_bounds__(256) void xagg_edge_acc_kernel(const int *__restric
     const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
     const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
     const float den0 = ms.z + 1e-16f, den1 = ms.w + 1e-16f;
-    for (int e = beg + g; e < end; e += 16) {           // group-uniform trip count
-      asm volatile("" ::: "memory");   // dxa re-read from LDS every edge: no 128-VGPR copy, more waves
-      const int j = col[e];
-      const float4 *xr = x4 + (size_t)j * 128 + t;
-      float4 xv[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) xv[c] = xr[16 * c];
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        s0 += f4_dot(xv[c], dl4[t + 16 * c]);
-        s1 += f4_dot(xv[c], dl4[128 + t + 16 * c]);
+    // the row's edges in chunks of 256: group g takes edges beg + 256 c + g + 16 k (k < 16); lane t
+    // of the group first computes, for ITS edge k = t, the neighbour j and the two softmax-gradient
+    // weights q = alpha lrelu' (one col / a_src load per lane, all in flight together), then the group
+    // walks k with j, q broadcast from lane k of its DPP row (row_share: one VALU op), two edges per
+    // step so two neighbour rows are in flight; ds = q (<dxa, x_j> - delta).
+    for (int cb = beg; cb < end; cb += 256) {
+      const int et = cb + g + 16 * t;
+      const bool lv = et < end;
+      const int jt = lv ? col[et] : i;
+      float q0t = 0.f, q1t = 0.f;
+      if (lv) {
+        const float2 sv = as2[jt];
+        const float ea = sv.x + ad.x, eb = sv.y + ad.y;
+        q0t = expf(lrelu(ea, ns) - ms.x) / den0 * (ea > 0.f ? 1.f : ns);
+        q1t = expf(lrelu(eb, ns) - ms.y) / den1 * (eb > 0.f ? 1.f : ns);
       }
-      s0 = row_sum16(s0);
-      s1 = row_sum16(s1);
-      const float2 sv = as2[j];
-      const float ea = sv.x + ad.x, eb = sv.y + ad.y;
-      const float al0 = expf(lrelu(ea, ns) - ms.x) / den0;
-      const float al1 = expf(lrelu(eb, ns) - ms.y) / den1;
-      const float ds0 = al0 * (ea > 0.f ? 1.f : ns) * (s0 - dl.x);
-      const float ds1 = al1 * (eb > 0.f ? 1.f : ns) * (s1 - dl.y);
+      // edges of this chunk for the wave's first group (the most of its four): a wave-uniform bound
+      const int kmax = min(16, (end - cb - 4 * wv + 15) / 16);
+#pragma unroll 1
+      for (int k = 0; k < kmax; k += EU) {
+        asm volatile("" ::: "memory");   // dxa re-read from LDS every step: no 128-VGPR copy, more waves
+        int jj[EU];
+        float qq0[EU], qq1[EU];
+        row_share_n<EU>(k, jt, q0t, q1t, jj, qq0, qq1);
+        float4 v[EU][8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        y0[c] = f4_fma(ds0, xv[c], y0[c]);
-        y1[c] = f4_fma(ds1, xv[c], y1[c]);
+        for (int u = 0; u < EU; ++u) {
+          const float4 *xr = x4 + (size_t)jj[u] * 128 + t;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[u][c] = xr[16 * c];
+        }
+        float s0[EU], s1[EU];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) s0[u] = s1[u] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float4 d0 = dl4[t + 16 * c], d1 = dl4[128 + t + 16 * c];
+#pragma unroll
+          for (int u = 0; u < EU; ++u) {
+            s0[u] += f4_dot(v[u][c], d0);
+            s1[u] += f4_dot(v[u][c], d1);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          const float ds0 = qq0[u] * (row_sum16(s0[u]) - dl.x), ds1 = qq1[u] * (row_sum16(s1[u]) - dl.y);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            y0[c] = f4_fma(ds0, v[u][c], y0[c]);
+            y1[c] = f4_fma(ds1, v[u][c], y1[c]);
+          }
+        }
       }
     }
     if (xa2 && wv == 0) {

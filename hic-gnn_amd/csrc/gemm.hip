@@ -51,7 +51,8 @@ __device__ __forceinline__ void gemm_tile(const float *__restrict__ A, int64_t l
                                           float *__restrict__ C, int64_t ldc, int M, int N,
                                           int K, int kchunk, const float *__restrict__ bias,
                                           float *__restrict__ slab, int64_t slab_stride, int accumulate,
-                                          float *__restrict__ csum, int bx, int by, int bz) {
+                                          float *__restrict__ csum, int bx, int by, int bz,
+                                          float *__restrict__ crelu = nullptr, int64_t ldr = 0) {
   static_assert(!CS || A_KM, "column sums of A need the K-major (weight-gradient) layout");
   constexpr int WM = BM / 2, WN = BN / 2;        // wave tile (4 waves in 2 x 2)
   constexpr int TM = WM / 32, TN = WN / 32;      // 32x32 MFMA tiles per wave
@@ -214,7 +215,9 @@ __device__ __forceinline__ void gemm_tile(const float *__restrict__ A, int64_t l
         const int gm = m0 + wm * WM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
         if (gm < M && gn < N) {
           float *o = out + (size_t)gm * ldo + gn;
-          *o = acc[a][b][r] + bb + ((accumulate && !slab) ? *o : 0.f);
+          const float v = acc[a][b][r] + bb + ((accumulate && !slab) ? *o : 0.f);
+          *o = v;
+          if (crelu && !slab) crelu[(size_t)gm * ldr + gn] = fmaxf(v, 0.f);   // relu(C) beside C (no split)
         }
       }
     }
@@ -477,9 +480,11 @@ __global__ __launch_bounds__(256, HICGAT_GEMM_OCC64) void gemm_rows_grouped_kern
   const RJob &J = jobs.j[q];
   const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
   const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
+  // splits = 1: the tile writes C (+ bias, + relu copy) itself and no reduce launch follows
+  const bool direct = jobs.splits == 1;
   gemm_tile<64, 128, false, B_KM, true, !B_KM ? false : true, false>(
-      J.a, J.lda, J.b, J.ldb, J.c, J.ldc, J.M, J.N, J.K, J.kchunk, nullptr, J.slab, (int64_t)J.M * J.N, 0, nullptr,
-      bx, by, bz);
+      J.a, J.lda, J.b, J.ldb, J.c, J.ldc, J.M, J.N, J.K, J.kchunk, direct ? J.bias : nullptr,
+      direct ? nullptr : J.slab, (int64_t)J.M * J.N, 0, nullptr, bx, by, bz, direct ? J.cr : nullptr, J.ldr);
 }
 __global__ __launch_bounds__(256) void rows_reduce_kernel(const RJobs jobs) {
   int q = 0;
@@ -509,7 +514,7 @@ __global__ __launch_bounds__(256) void rows_reduce_kernel(const RJobs jobs) {
 using namespace hicgat;
 
 extern "C" size_t hicgat_gemm_rows_grouped_workspace_bytes(const hicgat_gemm_job *jobs, int n, int splits) {
-  if (n <= 0 || !jobs || splits < 1) return 0;
+  if (n <= 0 || !jobs || splits <= 1) return 0;   // one chunk: the tiles write C directly
   size_t tot = 0;
   for (int i = 0; i < n; ++i) tot += (size_t)splits * jobs[i].M * jobs[i].N * sizeof(float);
   return tot;
@@ -520,7 +525,8 @@ extern "C" int hicgat_gemm_rows_grouped(const hicgat_gemm_job *jobs, int n, int 
   if (n < 0 || (n && !jobs) || splits < 1) return HICGAT_EINVAL;
   if (n > kMaxRJobs) return HICGAT_EUNSUPPORTED;
   if (n == 0) return HICGAT_OK;
-  if (workspace_bytes < hicgat_gemm_rows_grouped_workspace_bytes(jobs, n, splits) || !workspace) return HICGAT_EINVAL;
+  if (workspace_bytes < hicgat_gemm_rows_grouped_workspace_bytes(jobs, n, splits) || (splits > 1 && !workspace))
+    return HICGAT_EINVAL;
   RJobs rj;
   rj.n = 0;
   rj.splits = splits;
@@ -564,8 +570,10 @@ extern "C" int hicgat_gemm_rows_grouped(const hicgat_gemm_job *jobs, int n, int 
   else
     hipLaunchKernelGGL(gemm_rows_grouped_kernel<false>, dim3(wg), dim3(256), 0, s, rj);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(rows_reduce_kernel, dim3(blk), dim3(256), 0, s, rj);
-  HICGAT_CHECK_LAUNCH();
+  if (splits > 1) {
+    hipLaunchKernelGGL(rows_reduce_kernel, dim3(blk), dim3(256), 0, s, rj);
+    HICGAT_CHECK_LAUNCH();
+  }
   return HICGAT_OK;
 }
 

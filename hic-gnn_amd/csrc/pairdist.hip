@@ -55,6 +55,13 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// v + the values of lanes l^16, l^32 and l^48 (ds_bpermute shuffles; a v_permlane16/32_swap form
+// measured slower: the loss chain 0.162 vs 0.157 ms, profiles/r04h_kbench_pairdist.txt)
+__device__ __forceinline__ float sum_rows4(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   const int2 p = *reinterpret_cast<int2 *>(&v);
   int2 q;
@@ -369,12 +376,9 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    A.ax[q] += __shfl_xor(A.ax[q], 16);
-    A.ax[q] += __shfl_xor(A.ax[q], 32);
-    A.ay[q] += __shfl_xor(A.ay[q], 16);
-    A.ay[q] += __shfl_xor(A.ay[q], 32);
-    A.az[q] += __shfl_xor(A.az[q], 16);
-    A.az[q] += __shfl_xor(A.az[q], 32);
+    A.ax[q] = sum_rows4(A.ax[q]);
+    A.ay[q] = sum_rows4(A.ay[q]);
+    A.az[q] = sum_rows4(A.az[q]);
   }
   if (lane < 16) {
 #pragma unroll
@@ -427,12 +431,13 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
 // sums are combined in group order (fixed order: bitwise reproducible).
 constexpr int kRedGroups = 16;   // J-groups per row in pairdist_reduce (1024-thread blocks)
 
-__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
+__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk, int nblk,
                                       double *__restrict__ part);
 
-// mom != NULL: the last kMomBlocks blocks sum runs of the moment records [m0, m1) (tiles, then the
-// support pass's blocks) into mpart instead (moments_partial_block); blocks [0, row_blocks) reduce
-// the coordinate partials, plus the support pass's per-row term corr (background form) last.
+// mom != NULL: the blocks from row_blocks on (gridDim.x - row_blocks of them) sum runs of the moment
+// records [m0, m1) (tiles, then the support pass's blocks) into mpart instead (moments_partial_block);
+// blocks [0, row_blocks) reduce the coordinate partials, plus the support pass's per-row term corr
+// (background form) last.
 __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__restrict__ part, int ncol,
                                                                int N, int nb, int mode, int64_t t0,
                                                                int64_t t1, float scale,
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
                                                                const float4 *__restrict__ corr, int corr_r0,
                                                                int corr_r1, double *__restrict__ dc64) {
   if (mom && (int)blockIdx.x >= row_blocks) {
-    moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, mpart);
+    moments_partial_block(mom, m0, m1, (int)blockIdx.x - row_blocks, (int)gridDim.x - row_blocks, mpart);
     return;
   }
   __shared__ float4 red[kRedGroups][64];
@@ -529,14 +534,17 @@ __global__ __launch_bounds__(64) void finalize_kernel(int N, int loss_kind, doub
 // Tile moments over [t0,t1) in two fixed-order stages (deterministic): kMomBlocks extra blocks of
 // pairdist_reduce_kernel each sum a contiguous tile run (256 threads, each a strided subset with
 // its loads in flight, then a fixed tree) into part[b][0..6]; moments_finalize_kernel adds the
-// kMomBlocks partials in block order into stats[0..6] and finalizes.
+// kMomBlocks partials in block order into stats[0..6] and finalizes.  A rank's share whose partial
+// moments are all-reduced before the finalize (the sharded step) with at most kOneBlockMoments
+// records: ONE such block writes stats[0..6] itself (no moments_finalize launch).
 constexpr int kMomBlocks = 64;
+constexpr int64_t kOneBlockMoments = 4096;
 
-__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk,
+__device__ void moments_partial_block(const double *__restrict__ mom, int64_t t0, int64_t t1, int blk, int nblk,
                                       double *__restrict__ part) {
   __shared__ double mred[7][256];
   const int tid = threadIdx.x;
-  const int64_t per = (t1 - t0 + kMomBlocks - 1) / kMomBlocks;
+  const int64_t per = (t1 - t0 + nblk - 1) / nblk;
   const int64_t b0 = t0 + (int64_t)blk * per, b1 = min(t1, b0 + per);
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
   if (tid < 256) {
@@ -902,12 +910,17 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
   }
   const float scale = (float)(4.0 / ((double)N * (double)N));
   const int row_blocks = (dcoords || dcoords64) ? (N + 63) / 64 : 0;
-  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, s, part, 1, N, nb,
-                     (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
-                     row_blocks, mpart, corr, support_row_begin, support_row_end, dcoords64);
+  // dcoords64: the caller all-reduces [stats | dcoords64] and finalizes (hicgat_pairdist_finalize_rows),
+  // so a small share's moments go straight into stats[0..6] (stats[7..11] and loss are left alone)
+  const bool one = dcoords64 && nt + sblocks <= kOneBlockMoments;
+  hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + (one ? 1 : kMomBlocks)), dim3(1024), 0, s, part, 1,
+                     N, nb, (int)MODE_SYM, tile_begin, tile_end, scale, dcoords, mom, tile_begin, tile_end + sblocks,
+                     row_blocks, one ? stats : mpart, corr, support_row_begin, support_row_end, dcoords64);
   HICGAT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
-  HICGAT_CHECK_LAUNCH();
+  if (!one) {
+    hipLaunchKernelGGL(moments_finalize_kernel, dim3(1), dim3(64), 0, s, mpart, N, loss_kind, stats, loss);
+    HICGAT_CHECK_LAUNCH();
+  }
   return HICGAT_OK;
 }
 

@@ -538,13 +538,16 @@ class ShardedTrainer:
             # dxa^hd = dout^hd W_hd, both heads in one grouped launch
             K.gemm_rows_grouped([(self.dout_l[:, hc[hd]], W[hc[hd]], self.dxa[:, hd * F:(hd + 1) * F], None, None)
                                  for hd in (0, 1)], b_kmajor=1, name="gemm_dx")
+            heads = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
+                      None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                             self.gpart, xa2=self.X4[:, 1])
-            extra = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
-                      None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
-            extra += [("c", self.gpart, self.g_src, False),
-                      ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)]
-            ops.grouped_flush(K, extra)
+            # g_src (the edge pass's partial rows) and g_dst (its da_dst) need the edge pass; the heads'
+            # dW in the same launch pair (on a side stream beside the edge pass: 0.468 vs 0.459 ms per
+            # rank step at P = 8, profiles/r04h_sim_ab.txt)
+            ops.grouped_flush(K, heads + [("c", self.gpart, self.g_src, False),
+                                          ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None,
+                                           False)])
             K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
                                 self.att_r.grad.view(-1))
         return coords, None

@@ -407,7 +407,9 @@ class Truth:
         self.asymmetric_source = not bool(torch.equal(view, view.t()))
         self.raw = None
         if self.asymmetric_source:
-            self.raw = view.clone()     # the target as given: dSCC scores its upper triangle (scoring())
+            # the target as given, kept on the HOST (scoring() is read once per run; a device copy would
+            # double the truth's HBM for the whole run): dSCC scores its upper triangle
+            self.raw = view.to("cpu", copy=True)
             self._symmetrise()
         self.symmetric = True
         self.support = None
@@ -440,4 +442,4 @@ class Truth:
     def scoring(self):
         """The matrix whose upper triangle the reference scores dSCC against (HiC-GNN_main.py:135-139
         takes truth[triu] as given): the target before symmetrisation when it was asymmetric."""
-        return self.raw if self.raw is not None else self.dense()
+        return self.raw.to(self.buf.device) if self.raw is not None else self.dense()

@@ -44,7 +44,7 @@ P = _lib.ptr
 # Shapes that fill the chip on their own -- every single-GPU shape at N = 20000 (the tall kernel,
 # or >= 256 tiles) -- keep splits = 1.  HICGAT_ROW_SPLIT=0: off (A/B).
 ROW_SPLIT = os.environ.get("HICGAT_ROW_SPLIT", "1") != "0"
-_TALL_MIN_TILES = int(os.environ.get("HICGAT_TALL_MIN_TILES", "192"))   # gemm.hip tall_min_tiles()
+_TALL_MIN_TILES = 192   # gemm.hip tall_min_tiles(): the tall kernel takes shapes with at least this many tiles
 
 
 def row_splits(M, N, K):
@@ -402,6 +402,9 @@ class HipKernels:
 
     # workgroups of the grouped weight-gradient launch (hicgat_param_grads_grouped): ~2 per CU
     GROUP_WGS = int(os.environ.get("HICGAT_GROUP_WGS", "512"))
+    # target workgroups of a grouped node-row GEMM launch (sets its K split; 0 = no split: the tiles
+    # write C, bias and relu copy themselves and the slab-sum launch goes away)
+    ROWS_WGS = int(os.environ.get("HICGAT_ROWS_WGS", "512"))
     SMALL_M = 16
 
     def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
@@ -458,7 +461,7 @@ class HipKernels:
                                 None if bias is None else bias.data_ptr(), M, N, Kd)
             wgs += -(-M // 64) * -(-N // 128)
         if splits is None:
-            splits = max(1, min(jobs[0][0].shape[1] // 128, -(-512 // max(1, wgs))))
+            splits = max(1, min(jobs[0][0].shape[1] // 128, -(-self.ROWS_WGS // max(1, wgs)))) if self.ROWS_WGS else 1
         dev = jobs[0][2].device
         ws = _lib.workspace(self.lib.hicgat_gemm_rows_grouped_workspace_bytes(G, len(jobs), splits), dev)
         with _timed(name):

@@ -45,6 +45,12 @@ OVERLAP_DEFAULT = True
 # the gather, the source pass in row chunks, two side lanes on one GPU.
 
 
+# single-GPU step: parameter-gradient jobs of at least this many multiply-adds (the first tail block's
+# 512 x 512 dW) are held and issued with lin_l's dW as ONE grouped launch after the source gather
+# (0: off -- they go to the side stream like the rest)
+BIG_GROUP = float(os.environ.get("HICGAT_BIG_GROUP", "0"))
+
+
 def side_begin():
     """Route sink-bound parameter gradients to the side stream until ``side_join``."""
     with _SIDE_LOCK:
@@ -153,6 +159,9 @@ def side_join():
     no gradient kernel is left behind for a later step."""
     try:
         side_flush()
+        if _SIDE["jobs"] and not _SIDE["grouped"]:
+            # held big jobs that no GATConv backward issued (BIG_GROUP with another model): now
+            _SIDE["hold"].extend(grouped_flush())
     finally:
         with _SIDE_LOCK:
             _SIDE["on"] = max(0, _SIDE["on"] - 1)
@@ -182,7 +191,7 @@ def _param_launch(fn, *keep, small=False, work=0, job=None):
     else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join).
     ``job``: the same work as a descriptor for ``grouped_flush`` -- ("w", dy, x, dW, db) for
     dW += dy^T x (and db += column sums of dy), ("c", src, dst) for dst += column sums of src."""
-    if _SIDE["grouped"] and job is not None:
+    if job is not None and (_SIDE["grouped"] or (BIG_GROUP > 0 and _SIDE["on"] and work >= BIG_GROUP)):
         with _SIDE_LOCK:
             _SIDE["jobs"].append((job, keep))
         return
@@ -298,9 +307,13 @@ class _GATConvFn(torch.autograd.Function):
         dW = None
         if ctx.needs_input_grad[1]:
             gW = _sink(pW)
-            dW = weight_grad(K, dh, x, out=gW, accumulate=gW is not None)
-            if gW is not None:
-                dW = None
+            if gW is not None and _SIDE["jobs"]:
+                # the held big dW jobs and lin_l's as one grouped launch (BIG_GROUP)
+                _SIDE["hold"].extend(grouped_flush(K, [("w", dh, x, gW, None)]))
+            else:
+                dW = weight_grad(K, dh, x, out=gW, accumulate=gW is not None)
+                if gW is not None:
+                    dW = None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(0, 1, N, x.shape[1], h.shape[1], dh, W, torch.empty_like(x), name="gemm_dx")

@@ -308,7 +308,9 @@ size_t hicgat_pairdist_support_workspace_bytes(int N);
  * whole loss: a caller all-reduces stats[0..6] + dcoords and calls hicgat_pairdist_finalize);
  * 0, -1, 0, N is hicgat_pairdist_mse_fused_support.  dcoords64 (instead of dcoords): the same
  * fp32 gradient values widened to fp64, e.g. right behind stats[12] in one fp64 buffer that the
- * caller all-reduces as a whole.  Same workspace. */
+ * caller all-reduces as a whole; with dcoords64 and at most 4096 tiles + support blocks in the share,
+ * stats[7..11] and loss are not written (the caller's finalize after the all-reduce sets them).
+ * Same workspace. */
 int hicgat_pairdist_mse_fused_support_range(const float *coords, int N, float background, const int32_t *rowptr,
                                             const int32_t *col, const float *val, const float *diag,
                                             int64_t tile_begin, int64_t tile_end, int support_row_begin,
@@ -397,7 +399,8 @@ int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicg
  * op(B) = B^T (B [N, K], b_kmajor = 0: a Linear / head forward) or B (B [K, N], b_kmajor = 1: an
  * input gradient), c_relu (NULL or ld ldr): relu of the result too.  ONE launch of 64 x 128 fp32-MFMA
  * tiles over every job's tiles, K split in `splits` chunks into fp32 slabs; ONE launch adds the slabs
- * in split order (+ bias, relu copy).  Replaces the per-head GEMM calls (ATen mm of GATConv lin_l,
+ * in split order (+ bias, relu copy).  splits = 1: the tiles write C (+ bias, relu copy) themselves,
+ * no second launch, no workspace (NULL allowed).  Replaces the per-head GEMM calls (ATen mm of GATConv lin_l,
  * by linearity per head: hicgat.dist's aggregate-first form).  K, N, every ld a multiple of 4, every
  * pointer 16-B aligned (else HICGAT_EUNSUPPORTED); at most 8 jobs.
  * Workspace: hicgat_gemm_rows_grouped_workspace_bytes(same jobs, splits). */

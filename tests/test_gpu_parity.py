@@ -1317,7 +1317,7 @@ def test_dscc_chr19_1mb_k3000_matches_oracle(feats):
     _, hist = hicgat.train.train(model, data, tr, steps=K)
     with torch.no_grad():
         coords = model.get_model(data.x.float(), data.edge_index)
-    rho = hicgat.metrics.dscc(coords, tr.dense())
+    rho = hicgat.metrics.dscc(coords, tr.scoring())
     if feats == "node2vec":
         # with these node2vec features the oracle itself collapses to (near-)constant coordinates
         # at 1/2/4/8 threads (final loss 8.5743e-2 at 1, 4 and 8 threads, dSCC undefined / 0.0035):
@@ -1353,7 +1353,7 @@ def _chr19_device_dscc(x_fix, seed, K):
     hicgat.train.train(model, data, tr, steps=K)
     with torch.no_grad():
         coords = model.get_model(data.x.float(), data.edge_index)
-    return hicgat.metrics.dscc(coords, tr.dense()), data.edge_index
+    return hicgat.metrics.dscc(coords, tr.scoring()), data.edge_index
 
 
 @pytest.mark.parametrize("form", ["gather", "tiles"])

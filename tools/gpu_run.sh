@@ -18,6 +18,7 @@
 #                form, _xa: aggregate-first form, _au: bench.py's default "auto")
 #   kb:<jobs>:<libs> tools/kbench.py A/B of the named kernel jobs over the listed library builds
 #   simab:<env>  rank 0 of the simulated 8-rank xagg step (100 steps) under the environment assignment <env>
+#   probe[:<env>] tools/xagg_probe.py: rank 0's xagg kernels one by one (optionally under <env>)
 #   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
 #   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
@@ -96,8 +97,9 @@ for S in "$@"; do
       R=${S#kb:}; J=${R%%:*}; L=${R#*:}
       timeout -k 10 300 python tools/kbench.py --only "$J" --libs "$L" --reps 20 --rounds 3 > gpurun_out/${T}_kbench.txt 2>&1 || exit $?
       cat gpurun_out/${T}_kbench.txt | grep " med " ;;
-    probe)
-      timeout -k 10 300 python tools/xagg_probe.py > gpurun_out/${T}_probe.txt 2>&1 || exit $?
+    probe|probe:*)
+      E=${S#probe}; E=${E#:}
+      env $E timeout -k 10 300 python tools/xagg_probe.py > gpurun_out/${T}_probe.txt 2>&1 || exit $?
       cat gpurun_out/${T}_probe.txt | tail -12 ;;
     simprof|simprof_ag|simprof_xa)
       M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg

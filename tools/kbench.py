@@ -101,6 +101,7 @@ def main():
         "gemm_dx_densea": lambda K: K.gemm(0, 1, n, 512, 256, ya, Wa, dxa),
         "gemm_dw_densea": lambda K: hicgat.ops.weight_grad(K, ya, out),
         "torch_dw_densea": lambda K: ya.t().mm(out),
+        "torch_dw_512x512": lambda K: dh.t().mm(x),   # the library GEMM (hipBLASLt) on the same shape
         "torch_fwd_densea": lambda K: torch.nn.functional.linear(out, Wa, ba),
     }
     if a.only:
