@@ -26,9 +26,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ p, const 
                                                    float *__restrict__ m, float *__restrict__ v,
                                                    int64_t n, AdamConsts k,
                                                    const float2 *__restrict__ table,
-                                                   const int64_t *__restrict__ step_ctr, int64_t table_len) {
+                                                   const int64_t *__restrict__ step_ctr, int64_t table_len,
+                                                   int counted) {
   if (table) {  // graph-replayable form: per-step constants from the host-computed table
-    int64_t s = *step_ctr;
+    int64_t s = *step_ctr - counted;   // counted: this step's increment already happened (step start)
+    if (s < 0) s = 0;
     if (s >= table_len) s = table_len - 1;
     k.neg_step = table[s].x;
     k.bc2s = table[s].y;
@@ -84,16 +86,16 @@ extern "C" int hicgat_adam_step(float *param, const float *grad, float *exp_avg,
   const int64_t work = (n + 3) / 4;
   const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                     exp_avg, exp_avg_sq, n, k, nullptr, nullptr, (int64_t)0);
+                     exp_avg, exp_avg_sq, n, k, nullptr, nullptr, (int64_t)0, 0);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
-extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
-                                      int64_t n, double beta1, double beta2, double eps, const float *table,
-                                      int64_t table_len, int64_t *step_counter, hicgat_stream_t stream) {
-
-  if (n < 0 || table_len < 1) return HICGAT_EINVAL;
+extern "C" int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                                         int64_t n, double beta1, double beta2, double eps, const float *table,
+                                         int64_t table_len, int64_t *step_counter, int counted,
+                                         hicgat_stream_t stream) {
+  if (n < 0 || table_len < 1 || (counted != 0 && counted != 1)) return HICGAT_EINVAL;
   if (!param || !grad || !exp_avg || !exp_avg_sq || !table || !step_counter) return HICGAT_EINVAL;
   const uintptr_t mis = reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
                         reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq);
@@ -109,10 +111,19 @@ extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *ex
     const int64_t work = (n + 3) / 4;
     const int blocks = (int)std::min<int64_t>((work + 255) / 256, 4096);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                       exp_avg_sq, n, k, reinterpret_cast<const float2 *>(table), step_counter, table_len);
+                       exp_avg_sq, n, k, reinterpret_cast<const float2 *>(table), step_counter, table_len, counted);
     HICGAT_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step_counter);
-  HICGAT_CHECK_LAUNCH();
+  if (!counted) {
+    hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step_counter);
+    HICGAT_CHECK_LAUNCH();
+  }
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                                      int64_t n, double beta1, double beta2, double eps, const float *table,
+                                      int64_t table_len, int64_t *step_counter, hicgat_stream_t stream) {
+  return hicgat_adam_step_table_ex(param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, table, table_len,
+                                   step_counter, 0, stream);
 }

@@ -46,8 +46,12 @@ namespace hicgat {
 // 256-long chain per thread took 14 us, one launch on every step's critical path) -------------------
 __global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__ W, const float *__restrict__ att_s,
                                                        const float *__restrict__ att_d, float *__restrict__ v,
-                                                       float *__restrict__ zero_buf, int64_t zero_n) {
+                                                       float *__restrict__ zero_buf, int64_t zero_n,
+                                                       int64_t *__restrict__ step_ctr) {
   __shared__ float red[4][64];
+  // the optimizer's device step count advances here, at the step's first launch (Adam reads it at
+  // the step's end: hicgat_adam_step_table_ex with counted = 1, no increment launch of its own)
+  if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] = step_ctr[0] + 1;
   if (zero_buf) {   // the step's flat gradient buffer (zero_grad) rides along: float4 stores, then the tail
     const int64_t n4 = zero_n / 4, stride = (int64_t)gridDim.x * 256;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -680,14 +684,15 @@ extern "C" size_t hicgat_xagg_vec_bytes(void) { return 4 * 512 * sizeof(float); 
 
 extern "C" int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst,
                                        int N, int F, int H, int C, float *vec, float *a_src, float *a_dst,
-                                       float *zero_buf, int64_t zero_n, hicgat_stream_t stream) {
+                                       float *zero_buf, int64_t zero_n, int64_t *step_counter,
+                                       hicgat_stream_t stream) {
   if (N < 0 || zero_n < 0) return HICGAT_EINVAL;
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (!W || !att_src || !att_dst || !vec || (zero_n > 0 && !zero_buf)) return HICGAT_EINVAL;
   if (zero_buf && (reinterpret_cast<uintptr_t>(zero_buf) & 15)) return HICGAT_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(xagg_vec_kernel, dim3(32), dim3(256), 0, s, W, att_src, att_dst, vec, zero_n > 0 ? zero_buf : nullptr,
-                     zero_n);
+                     zero_n, step_counter);
   HICGAT_CHECK_LAUNCH();
   if (N == 0) return HICGAT_OK;
   if (!x || !a_src || !a_dst) return HICGAT_EINVAL;
@@ -699,7 +704,7 @@ extern "C" int hicgat_xagg_logits_zero(const float *x, const float *W, const flo
 extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
                                   int F, int H, int C, float *vec, float *a_src, float *a_dst,
                                   hicgat_stream_t stream) {
-  return hicgat_xagg_logits_zero(x, W, att_src, att_dst, N, F, H, C, vec, a_src, a_dst, nullptr, 0, stream);
+  return hicgat_xagg_logits_zero(x, W, att_src, att_dst, N, F, H, C, vec, a_src, a_dst, nullptr, 0, nullptr, stream);
 }
 
 extern "C" int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,

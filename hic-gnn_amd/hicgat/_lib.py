@@ -87,7 +87,7 @@ SIGNATURES = {
     "hicgat_xagg_vec_bytes": (c_sz, []),
     "hicgat_xagg_logits": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_xagg_logits_zero": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_i64,
-                                        c_p]),
+                                        c_p, c_p]),
     "hicgat_xagg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_f, c_p, c_p,
                                 c_p]),
     "hicgat_xagg_bias_relu": (c_int, [c_p, c_p, c_p, c_int, c_int, c_p]),
@@ -138,6 +138,7 @@ SIGNATURES = {
                                       c_int, c_u64, c_int, c_p, c_p, c_p]),
     "hicgat_adam_step": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_i64, c_p]),
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
+    "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_int, c_p]),
 }
 
 

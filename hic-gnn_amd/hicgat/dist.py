@@ -433,8 +433,14 @@ class ShardedTrainer:
         else:
             coords, tail_done = self._step_allgather()
         self._grad_allreduce(tail_done)
-        self.opt.step()
+        self.opt.step(counted=self._ctr() is not None)
         return self.loss, self.stats, coords
+
+    def _ctr(self):
+        """The optimizer's device step count when the xagg step's first launch advances it (HIP path,
+        device step enabled), else None (Adam increments it itself)."""
+        return self.opt.step_ctr if (self.mode == "xagg" and self.cuda and
+                                     getattr(self.opt, "step_ctr", None) is not None) else None
 
     def _grad_allreduce(self, tail_done):
         """The flat gradient all-reduce in two buckets: the MLP tail's (on the comm stream, after
@@ -514,7 +520,8 @@ class ShardedTrainer:
         W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
         bias = self.bias.detach()
         # ---- forward ------------------------------------------------------------------------
-        K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst, zero=self.opt.grad if self.cuda else None)
+        K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst, zero=self.opt.grad if self.cuda else None,
+                      step_ctr=self._ctr())
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
         Y0 = self.Y0
         # out (head hd columns) = xa^hd W_hd^T + b^hd (and relu(out) for the tail): both heads in one

@@ -210,9 +210,10 @@ class HipKernels:
         return datt_l, datt_r, dbias
 
     # -- aggregate-first GATConv (gat_xagg.hip): the multi-GPU "xagg" step (hicgat.dist) ---------------
-    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None):
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None, step_ctr=None):
         """a_src / a_dst [N, 2] = x . (W_h^T att^h) for every row of x; ``zero``: a contiguous buffer
-        zeroed in the same launch (the step's flat gradient buffer)."""
+        zeroed in the same launch (the step's flat gradient buffer); ``step_ctr``: the optimizer's
+        device step count, advanced in the same launch (its Adam then runs with ``counted=True``)."""
         N, F = x.shape
         H, C = att_l.shape[-2], att_l.shape[-1]
         vec = _lib.workspace(self.lib.hicgat_xagg_vec_bytes(), x.device)
@@ -220,7 +221,7 @@ class HipKernels:
         with _timed("xagg_logits"):
             _lib.check(self.lib.hicgat_xagg_logits_zero(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src),
                                                         P(a_dst), P(zero), 0 if zero is None else zero.numel(),
-                                                        _lib.stream(x.device)), "hicgat_xagg_logits_zero")
+                                                        P(step_ctr), _lib.stream(x.device)), "hicgat_xagg_logits_zero")
 
     def xagg_fwd(self, rowptr, col, r0, r1, x, a_src, a_dst, ns, X4, row_stats):
         """Own rows [r0, r1): X4 [2, 2, r1 - r0, 512] = (xa, xa2) per head; row stats (global rows)."""
@@ -547,11 +548,12 @@ class HipKernels:
                                                           _lib.stream(ws.device)), "hicgat_ln_relu_res_bwd_params")
 
     # -- a10 --------------------------------------------------------------------------------------
-    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr):
+    def adam_table(self, flat, grad, m, v, n, b1, b2, eps, table, step_ctr, counted=False):
         with _timed("adam"):
-            _lib.check(self.lib.hicgat_adam_step_table(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
-                                                       float(eps), P(table), table.shape[0], P(step_ctr),
-                                                       _lib.stream(flat.device)), "hicgat_adam_step_table")
+            _lib.check(self.lib.hicgat_adam_step_table_ex(P(flat), P(grad), P(m), P(v), int(n), float(b1), float(b2),
+                                                          float(eps), P(table), table.shape[0], P(step_ctr),
+                                                          int(bool(counted)), _lib.stream(flat.device)),
+                       "hicgat_adam_step_table_ex")
 
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):

@@ -46,9 +46,10 @@ OVERLAP_DEFAULT = True
 
 
 # single-GPU step: parameter-gradient jobs of at least this many multiply-adds (the first tail block's
-# 512 x 512 dW) are held and issued with lin_l's dW as ONE grouped launch after the source gather
-# (0: off -- they go to the side stream like the rest)
-BIG_GROUP = float(os.environ.get("HICGAT_BIG_GROUP", "0"))
+# 512 x 512 dW, 5.2e9 at N = 20000) are held and issued with lin_l's dW as ONE grouped launch after
+# the source gather (0: off -- they go to the side stream like the rest): 1.876 / 1.879 vs 1.889 /
+# 1.888 ms per step (profiles/r04i_ab_big_group.txt)
+BIG_GROUP = float(os.environ.get("HICGAT_BIG_GROUP", "5e9"))
 
 
 def side_begin():

@@ -71,13 +71,15 @@ class FlatAdam:
                 p.grad = view.view_as(p)
 
     @torch.no_grad()
-    def step(self):
+    def step(self, counted=False):
+        """``counted``: the device step count was already advanced by an earlier launch of this step
+        (``kernels.xagg_logits(step_ctr=...)``), so Adam reads it without an increment launch."""
         self._reattach()
         self.step_count += 1
         kern = self.kern if self.kern is not None else kernels.default()
         if getattr(self, "step_ctr", None) is not None:
             kern.adam_table(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.betas[0],
-                            self.betas[1], self.eps, self.table, self.step_ctr)
+                            self.betas[1], self.eps, self.table, self.step_ctr, counted=counted)
             return
         kern.adam(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.lr, self.betas[0],
                   self.betas[1], self.eps, self.step_count)

@@ -167,10 +167,12 @@ size_t hicgat_xagg_vec_bytes(void);
 int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N, int F,
                        int H, int C, float *vec, float *a_src, float *a_dst, hicgat_stream_t stream);
 /* hicgat_xagg_logits that also zeroes zero_buf[0, zero_n) (a step's flat gradient buffer: the
- * optimizer's zero_grad, HiC-GNN_main.py:124) in its first launch -- one launch fewer per step. */
+ * optimizer's zero_grad, HiC-GNN_main.py:124) in its first launch -- one launch fewer per step --
+ * and, with step_counter (NULL: none), advances the optimizer's device step count there (the step's
+ * Adam then calls hicgat_adam_step_table_ex with counted = 1). */
 int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
                             int F, int H, int C, float *vec, float *a_src, float *a_dst, float *zero_buf,
-                            int64_t zero_n, hicgat_stream_t stream);
+                            int64_t zero_n, int64_t *step_counter, hicgat_stream_t stream);
 int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
                     int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope, float *X4,
                     float *row_stats, hicgat_stream_t stream);
@@ -534,6 +536,12 @@ int hicgat_adam_step(float *param, const float *grad, float *exp_avg, float *exp
 int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                            int64_t n, double beta1, double beta2, double eps, const float *table,
                            int64_t table_len, int64_t *step_counter, hicgat_stream_t stream);
+/* The same; counted = 1: this step's increment of *step_counter already happened in an earlier
+ * launch of the step (hicgat_xagg_logits_zero), so the table row is *step_counter - 1 and no
+ * increment follows (one launch fewer); counted = 0 is hicgat_adam_step_table. */
+int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                              int64_t n, double beta1, double beta2, double eps, const float *table,
+                              int64_t table_len, int64_t *step_counter, int counted, hicgat_stream_t stream);
 #ifdef __cplusplus
 }
 #endif

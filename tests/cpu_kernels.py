@@ -194,7 +194,7 @@ class CpuKernels:
         return out
 
     # -- aggregate-first GATConv (gat_xagg.hip) -------------------------------------------------------
-    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None):
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None, step_ctr=None):
         if zero is not None:
             zero.zero_()
         H, C = att_l.shape[-2], att_l.shape[-1]

@@ -119,3 +119,32 @@ def test_ln_bwd_split_params_same_bits(W):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     assert torch.equal(dy1, dy2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
+
+
+@pytest.mark.parametrize("b_km", [0, 1])
+@pytest.mark.parametrize("splits", [None, 1, 3])
+def test_gemm_rows_grouped_matches_fp64(b_km, splits):
+    """hicgat_gemm_rows_grouped (the xagg step's per-head GEMMs and dxa GEMMs): two jobs of a rank's
+    shard shape in one launch, K split into slabs (None: the auto split) or written directly
+    (splits = 1), bias and the relu copy, against fp64."""
+    import hicgat
+    K = hicgat.kernels.default()
+    torch.manual_seed(7 + b_km)
+    M, Kd, N = 2701, 256 if b_km else 512, 512 if b_km else 256
+    jobs, refs = [], []
+    for hd in range(2):
+        A = torch.randn(M, Kd, device=DEV)
+        B = torch.randn((Kd, N) if b_km else (N, Kd), device=DEV)
+        C = torch.full((M, N), float("nan"), device=DEV)
+        bias = None if b_km else torch.randn(N, device=DEV)
+        Cr = None if b_km else torch.full((M, N), float("nan"), device=DEV)
+        ref = A.double() @ (B.double() if b_km else B.double().t())
+        if bias is not None:
+            ref = ref + bias.double()
+        jobs.append((A, B, C, bias, Cr))
+        refs.append(ref)
+    K.gemm_rows_grouped(jobs, b_kmajor=b_km, splits=splits)
+    for (A, B, C, bias, Cr), ref in zip(jobs, refs):
+        assert _rel(C.cpu(), ref.cpu()) < 5e-6
+        if Cr is not None:
+            assert torch.equal(Cr, torch.relu(C))
