@@ -135,7 +135,12 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
 #ifndef HICGAT_TAIL_WAVES
 #define HICGAT_TAIL_WAVES 8
 #endif
-template <int RB, int NW>
+// HEADS (the sharded aggregate-first GATConv, gat_xagg.hip): the tail's input rows are formed here
+// from the two heads' aggregates, out^h = xa^h W_h^T + b^h (xa^h = x + h * xa_hs, row stride ldx; W_h
+// = rows 256h .. of lin_l's weight Wh [512][512]), written as Y0 (pre-activation) and O = relu(Y0)
+// (the tail's input, kept for the backward's weight gradients) -- the per-head GEMM launches and
+// their slab sum leave the step.  Waves 0-3 take head 0's 256 columns, 4-7 head 1's.
+template <int RB, int NW, bool HEADS = false>
 __global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
@@ -144,21 +149,52 @@ __global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
     const float *__restrict__ be3, const float *__restrict__ W4, const float *__restrict__ b4, float eps,
     float *__restrict__ Y1, float2 *__restrict__ st1, float *__restrict__ z1, float *__restrict__ Y2,
     float2 *__restrict__ st2, float *__restrict__ z2, float *__restrict__ y3, float2 *__restrict__ st3,
-    float *__restrict__ z3, float *__restrict__ coords) {
+    float *__restrict__ z3, float *__restrict__ coords, int64_t xa_hs = 0, const float *__restrict__ Wh = nullptr,
+    const float *__restrict__ bh = nullptr, float *__restrict__ Y0 = nullptr, float *__restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // x rows, then z1 / z2 / z3 rows
   float *Bs = lds_tail + RB * XS;    // Y1, then Y2 / y3 rows
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16, NT1 = 32 / NW, NT2 = 16 / NW;   // 16-column tiles per wave: block 1 / block 2
-  // x rows -> LDS (rows past M: zeros)
-  for (int e = tid; e < RB * 128; e += 64 * NW) {
-    const int r = e >> 7, c4 = e & 127;
+  // x rows (HEADS: xa^0 rows -> As, xa^1 rows -> Bs) -> LDS (rows past M: zeros)
+  for (int e = tid; e < (HEADS ? 2 : 1) * RB * 128; e += 64 * NW) {
+    const int hd = e / (RB * 128), r = (e >> 7) % RB, c4 = e & 127;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + (size_t)(m0 + r) * ldx)[c4];
-    *reinterpret_cast<float4 *>(&As[r * XS + 4 * c4]) = v;
+    if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + hd * xa_hs + (size_t)(m0 + r) * ldx)[c4];
+    *reinterpret_cast<float4 *>(&(hd ? Bs : As)[r * XS + 4 * c4]) = v;
   }
   __syncthreads();
+  if constexpr (HEADS) {
+    static_assert(NW == 8, "the head GEMMs take 4 waves per head");
+    const int hd = wv >> 2, n0 = 64 * (wv & 3);
+    f32x4 acc[H][4];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, 4, 512>(hd ? Bs : As, XS, Wh + (size_t)hd * 256 * 512, n0, acc, lane);
+    __syncthreads();   // every wave is done with xa^0 / xa^1 before As takes relu(out)
+    const int li = lane & 15, r0 = 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = 256 * hd + n0 + 16 * t + li;
+      const float bb = bh[c];
+#pragma unroll
+      for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * h + r0 + r;
+          const float v = acc[h][t][r] + bb, o = fmaxf(v, 0.f);
+          As[row * XS + c] = o;
+          if (m0 + row < M) {
+            Y0[(size_t)(m0 + row) * 512 + c] = v;
+            O[(size_t)(m0 + row) * 512 + c] = o;
+          }
+        }
+    }
+    __syncthreads();
+  }
   // ---- block 1: 512 -> 512, wave wv: columns 16 NT1 wv .. + 16 NT1 - 1 ----
   {
     f32x4 acc[H][NT1];
@@ -331,7 +367,12 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
 }
 
 
-template <int RB, int NW>
+// HEADS: the GATConv's rows backward and its dxa GEMM after the chain (xagg_rows_bwd + the dxa
+// grouped GEMM of gat_xagg.hip / gemm.hip): dx stays in LDS, dout = dx (Y0 > 0) (act) is written
+// with delta^h = <dout^h, Y0^h - b^h> into row_stats[8r + 4 + h] (S3 moved to [6:8], as
+// xagg_rows_bwd does), then dxa^h = dout^h W_h ([RB x 256] [256 x 512], waves 0-3 head 0, 4-7 head 1)
+// into dxa [M][1024].
+template <int RB, int NW, bool HEADS = false>
 __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
     const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
@@ -340,7 +381,9 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     const float *__restrict__ be1, const float *__restrict__ g2, const float *__restrict__ be2,
     const float *__restrict__ g3, const float *__restrict__ be3, float *__restrict__ dx, float *__restrict__ dY1,
     float *__restrict__ dY2, float *__restrict__ dy3, float *__restrict__ p1, float *__restrict__ p2,
-    float *__restrict__ p3) {
+    float *__restrict__ p3, int act = 0, const float *__restrict__ Y0 = nullptr, const float *__restrict__ Wh = nullptr,
+    const float *__restrict__ bh = nullptr, float *__restrict__ dout = nullptr, float *__restrict__ row_stats = nullptr,
+    float *__restrict__ dxa = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // dz3, dz2, dz1 rows
   float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
@@ -396,7 +439,55 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     mfma_rows_t<RB, NT1, 512>(Bs, XS, W1c, 512, 16 * NT1 * wv, acc, lane);
-    put_tiles<RB, NT1>(acc, 16 * NT1 * wv, nullptr, 0, dx, 512, m0, M, lane);
+    put_tiles<RB, NT1>(acc, 16 * NT1 * wv, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
+  }
+  if constexpr (HEADS) {
+    static_assert(NW == 8, "the dxa GEMMs take 4 waves per head");
+    __syncthreads();
+    // rows: lane l holds float4 l (head 0) and 64 + l (head 1) of the row, as xagg_rows_bwd_kernel
+    for (int rr = wv; rr < RB; rr += NW) {
+      const int row = m0 + rr;
+      if (row >= M) {   // wave-uniform: zero rows of the A image
+        *reinterpret_cast<float4 *>(&As[rr * XS + 4 * lane]) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4 *>(&As[rr * XS + 256 + 4 * lane]) = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      float4 d0 = *reinterpret_cast<const float4 *>(&As[rr * XS + 4 * lane]);
+      float4 d1 = *reinterpret_cast<const float4 *>(&As[rr * XS + 256 + 4 * lane]);
+      const float4 *y4 = reinterpret_cast<const float4 *>(Y0 + (size_t)row * 512);
+      const float4 y0v = y4[lane], y1v = y4[64 + lane];
+      const float4 b0 = reinterpret_cast<const float4 *>(bh)[lane], b1 = reinterpret_cast<const float4 *>(bh)[64 + lane];
+      if (act) {
+        d0 = make_float4(y0v.x <= 0.f ? 0.f : d0.x, y0v.y <= 0.f ? 0.f : d0.y, y0v.z <= 0.f ? 0.f : d0.z,
+                         y0v.w <= 0.f ? 0.f : d0.w);
+        d1 = make_float4(y1v.x <= 0.f ? 0.f : d1.x, y1v.y <= 0.f ? 0.f : d1.y, y1v.z <= 0.f ? 0.f : d1.z,
+                         y1v.w <= 0.f ? 0.f : d1.w);
+      }
+      float4 *d4 = reinterpret_cast<float4 *>(dout + (size_t)row * 512);
+      d4[lane] = d0;
+      d4[64 + lane] = d1;
+      *reinterpret_cast<float4 *>(&As[rr * XS + 4 * lane]) = d0;
+      *reinterpret_cast<float4 *>(&As[rr * XS + 256 + 4 * lane]) = d1;
+      const float4 e0 = make_float4(y0v.x - b0.x, y0v.y - b0.y, y0v.z - b0.z, y0v.w - b0.w);
+      const float4 e1 = make_float4(y1v.x - b1.x, y1v.y - b1.y, y1v.z - b1.z, y1v.w - b1.w);
+      float v[2] = {f4_dot(d0, e0), f4_dot(d1, e1)};
+      transpose_reduce<2>(v, lane);   // lane 0: head 0, lane 32: head 1
+      const float dl0 = readlane_f(v[0], 0), dl1 = readlane_f(v[0], 32);
+      if (lane == 0) {
+        float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+        const float4 t = rs4[2 * (size_t)row + 1];   // (S3_0, S3_1, -, -) from xagg_fwd
+        rs4[2 * (size_t)row + 1] = make_float4(dl0, dl1, t.x, t.y);
+      }
+    }
+    __syncthreads();
+    const int hd = wv >> 2, n0 = 128 * (wv & 3);
+    f32x4 acc[H][8];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, 8, 256>(As + 256 * hd, XS, Wh + (size_t)hd * 256 * 512, 512, n0, acc, lane);
+    put_tiles<RB, 8>(acc, n0, nullptr, 0, dxa + 512 * hd, 1024, m0, M, lane);
   }
 }
 
@@ -404,35 +495,78 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
 
 using namespace hicgat;
 
-extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c,
-                                     const float *g1, const float *be1, const float *W2c, const float *b2c,
-                                     const float *g2, const float *be2, const float *W3, const float *b3,
-                                     const float *g3, const float *be3, const float *W4, const float *b4, float eps,
-                                     float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2, float *y3,
-                                     float *st3, float *z3, float *coords, hicgat_stream_t stream) {
+namespace {
+struct TailHeads {   // the HEADS operands of the head-fused forms (all null: the plain tail)
+  const float *xa = nullptr;
+  int64_t xa_hs = 0;
+  const float *Wh = nullptr, *bh = nullptr;
+  float *Y0 = nullptr, *O = nullptr;
+};
+
+template <bool HEADS>
+int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c, const float *g1,
+                    const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2,
+                    const float *W3, const float *b3, const float *g3, const float *be3, const float *W4,
+                    const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2,
+                    float *y3, float *st3, float *z3, float *coords, const TailHeads &hh, hipStream_t stream) {
   if (M < 0 || ldx < 512 || (ldx & 3)) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
   const void *ps[] = {x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4,
                       Y1, st1, z1, Y2, st2, z2, y3, st3, z3, coords};
   for (const void *p : ps)
     if (!p) return HICGAT_EINVAL;
+  if (HEADS && (!hh.Wh || !hh.bh || !hh.Y0 || !hh.O || (hh.xa_hs & 3))) return HICGAT_EINVAL;
   // float4 rows: x, the weight rows and the LDS images need 16-B alignment
-  if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3) & 15) return HICGAT_EUNSUPPORTED;
+  if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3 | (uintptr_t)hh.Wh | (uintptr_t)hh.Y0 |
+       (uintptr_t)hh.O) & 15)
+    return HICGAT_EUNSUPPORTED;
   // 16 rows per workgroup (66 KiB of dynamic LDS: two workgroups per CU).  A 32-row form (132 KiB,
   // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
   // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
   // with one workgroup per CU every phase's latency is exposed.
   constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW>), dim3((M + RB - 1) / RB), dim3(64 * NW), (size_t)2 * RB * XS * sizeof(float),
-                     (hipStream_t)stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps,
-                     Y1, reinterpret_cast<float2 *>(st1), z1, Y2, reinterpret_cast<float2 *>(st2), z2, y3,
-                     reinterpret_cast<float2 *>(st3), z3, coords);
+  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, HEADS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+                     (size_t)2 * RB * XS * sizeof(float), stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3,
+                     b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1, Y2,
+                     reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords, hh.xa_hs,
+                     hh.Wh, hh.bh, hh.Y0, hh.O);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+}  // namespace
+
+extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c,
+                                     const float *g1, const float *be1, const float *W2c, const float *b2c,
+                                     const float *g2, const float *be2, const float *W3, const float *b3,
+                                     const float *g3, const float *be3, const float *W4, const float *b4, float eps,
+                                     float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2, float *y3,
+                                     float *st3, float *z3, float *coords, hicgat_stream_t stream) {
+  return tail_fwd_launch<false>(x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
+                                st1, z1, Y2, st2, z2, y3, st3, z3, coords, TailHeads{}, (hipStream_t)stream);
+}
+
+extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64_t xa_head_stride, const float *Wh,
+                                           const float *bh, float *Y0, float *O, int M, const float *W1c,
+                                           const float *b1c, const float *g1, const float *be1, const float *W2c,
+                                           const float *b2c, const float *g2, const float *be2, const float *W3,
+                                           const float *b3, const float *g3, const float *be3, const float *W4,
+                                           const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2,
+                                           float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
+                                           hicgat_stream_t stream) {
+  if (HICGAT_TAIL_WAVES != 8) return HICGAT_EUNSUPPORTED;
+  TailHeads hh;
+  hh.xa = xa;
+  hh.xa_hs = xa_head_stride;
+  hh.Wh = Wh;
+  hh.bh = bh;
+  hh.Y0 = Y0;
+  hh.O = O;
+  return tail_fwd_launch<true>(xa, ld_xa, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
+                               st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh, (hipStream_t)stream);
 }
 
 extern "C" int hicgat_tail_bwd_waves(void) { return HICGAT_TAIL_WAVES; }
@@ -441,6 +575,49 @@ extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
   return M <= 0 ? 16 : (size_t)HICGAT_TAIL_WAVES * ((M + 15) / 16) * 2 * W * sizeof(float);
 }
 
+namespace {
+struct TailHeadsBwd {   // the HEADS operands of the backward (all null: the plain tail)
+  int act = 0;
+  const float *Y0 = nullptr, *Wh = nullptr, *bh = nullptr;
+  float *dout = nullptr, *row_stats = nullptr, *dxa = nullptr;
+};
+
+template <bool HEADS>
+int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
+                    const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c,
+                    const float *W1c, const float *g1, const float *be1, const float *g2, const float *be2,
+                    const float *g3, const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
+                    size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
+                    const TailHeadsBwd &hh, hipStream_t stream) {
+  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
+  if (M < 0) return HICGAT_EINVAL;
+  if (M == 0) return HICGAT_OK;
+  const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                      HEADS ? hh.dout : dx, dY1, dY2, dy3, ws1, ws2, ws3};
+  for (const void *p : ps)
+    if (!p) return HICGAT_EINVAL;
+  if (HEADS && (!hh.Y0 || !hh.Wh || !hh.bh || !hh.row_stats || !hh.dxa)) return HICGAT_EINVAL;
+  if (HEADS && (((uintptr_t)hh.Y0 | (uintptr_t)hh.bh | (uintptr_t)hh.dout | (uintptr_t)hh.row_stats) & 15))
+    return HICGAT_EUNSUPPORTED;
+  // every workgroup owns NW partial rows of each LN workspace (one per wave)
+  if (ws1_bytes < hicgat_tail_bwd_workspace_bytes(M, 256) || ws2_bytes < hicgat_tail_bwd_workspace_bytes(M, 128) ||
+      ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
+    return HICGAT_EINVAL;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
+  if (!attr) return HICGAT_ELAUNCH;
+  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+                     (size_t)2 * RB * XS * sizeof(float), stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
+                     Y2, reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c,
+                     W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1),
+                     static_cast<float *>(ws2), static_cast<float *>(ws3), hh.act, hh.Y0, hh.Wh, hh.bh, hh.dout,
+                     hh.row_stats, hh.dxa);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+}  // namespace
+
 extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
                                      const float *st2, const float *y3, const float *st3, const float *W4,
                                      const float *W3, const float *W2c, const float *W1c, const float *g1,
@@ -448,26 +625,30 @@ extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y
                                      const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
                                      size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
                                      hicgat_stream_t stream) {
-  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
-  if (M < 0) return HICGAT_EINVAL;
-  if (M == 0) return HICGAT_OK;
-  const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
-                      dx, dY1, dY2, dy3, ws1, ws2, ws3};
-  for (const void *p : ps)
-    if (!p) return HICGAT_EINVAL;
-  // every workgroup owns NW partial rows of each LN workspace (one per wave)
-  if (ws1_bytes < hicgat_tail_bwd_workspace_bytes(M, 256) || ws2_bytes < hicgat_tail_bwd_workspace_bytes(M, 128) ||
-      ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
-    return HICGAT_EINVAL;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
-  if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW>), dim3((M + RB - 1) / RB), dim3(64 * NW), (size_t)2 * RB * XS * sizeof(float),
-                     (hipStream_t)stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1), Y2,
-                     reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c, W1c,
-                     g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1), static_cast<float *>(ws2),
-                     static_cast<float *>(ws3));
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  return tail_bwd_launch<false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                                dx, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, TailHeadsBwd{},
+                                (hipStream_t)stream);
+}
+
+extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const float *Y1, const float *st1,
+                                           const float *Y2, const float *st2, const float *y3, const float *st3,
+                                           const float *W4, const float *W3, const float *W2c, const float *W1c,
+                                           const float *g1, const float *be1, const float *g2, const float *be2,
+                                           const float *g3, const float *be3, float *dY1, float *dY2, float *dy3,
+                                           void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
+                                           size_t ws3_bytes, int act, const float *Y0, const float *Wh,
+                                           const float *bh, float *dout, float *row_stats, float *dxa,
+                                           hicgat_stream_t stream) {
+  if (HICGAT_TAIL_WAVES != 8) return HICGAT_EUNSUPPORTED;
+  TailHeadsBwd hh;
+  hh.act = act ? 1 : 0;
+  hh.Y0 = Y0;
+  hh.Wh = Wh;
+  hh.bh = bh;
+  hh.dout = dout;
+  hh.row_stats = row_stats;
+  hh.dxa = dxa;
+  return tail_bwd_launch<true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                               nullptr, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, hh,
+                               (hipStream_t)stream);
 }

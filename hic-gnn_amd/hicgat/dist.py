@@ -397,15 +397,17 @@ class ShardedTrainer:
                         dcoords=self.dcoords)
         return self.dcoords[self.r0:self.r1]
 
-    def _tail(self, o=None):
+    def _tail(self, o=None, heads=None):
         """Tail forward on own rows (input ``o``, default this rank's rows of ``out``), the coords
-        all-gather, the loss share and its all-reduce."""
+        all-gather, the loss share and its all-reduce.  ``heads`` (``ops.TailHeads``): o's rows are
+        formed by the tail kernel itself from the xagg aggregates."""
         if o is None:
             o = self.out[self.a0:self.a1]
         o = o.detach().requires_grad_(True)
         own = self.coords_buf[self.q0:self.q1]
         if self.act and self.cuda and ops.fused_tail_ok(self.model, o):
-            coords_loc = ops.fused_tail(self.model, o, coords_out=own)   # written into the all-gather rows
+            # written into the all-gather rows
+            coords_loc = ops.fused_tail(self.model, o, coords_out=own, heads=heads)
         else:
             coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
             own.copy_(coords_loc.detach())
@@ -524,13 +526,22 @@ class ShardedTrainer:
                       step_ctr=self._ctr())
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
         Y0 = self.Y0
-        # out (head hd columns) = xa^hd W_hd^T + b^hd (and relu(out) for the tail): both heads in one
-        # grouped launch + one slab sum with the bias / relu epilogue; the forward needs no out2 (da_dst
-        # comes from dxa . xa2)
+        rs_own = self.rs[r0:r1]
         hc = [slice(hd * C, (hd + 1) * C) for hd in (0, 1)]
-        K.gemm_rows_grouped([(self.X4[hd, 0], W[hc[hd]], Y0[:, hc[hd]], bias[hc[hd]],
-                              self.O[:, hc[hd]] if self.act else None) for hd in (0, 1)], b_kmajor=0, name="gemm_fwd")
-        o, coords_loc, coords = self._tail(self.O if self.act else Y0)
+        if self.act and self.cuda and ops.tail_heads_ok(self.model, self.O):
+            # the head GEMMs (+ bias, relu) at the head of the one-kernel tail forward, and the rows
+            # backward + dxa GEMMs at the end of its backward: four launches fewer per step
+            heads = ops.TailHeads(self.X4, W.contiguous(), bias, Y0, self.dout_l, rs_own, self.dxa, act=self.act)
+            o, coords_loc, coords = self._tail(self.O, heads=heads)
+        else:
+            heads = None
+            # out (head hd columns) = xa^hd W_hd^T + b^hd (and relu(out) for the tail): both heads in one
+            # grouped launch + one slab sum with the bias / relu epilogue; the forward needs no out2
+            # (da_dst comes from dxa . xa2)
+            K.gemm_rows_grouped([(self.X4[hd, 0], W[hc[hd]], Y0[:, hc[hd]], bias[hc[hd]],
+                                  self.O[:, hc[hd]] if self.act else None) for hd in (0, 1)], b_kmajor=0,
+                                name="gemm_fwd")
+            o, coords_loc, coords = self._tail(self.O if self.act else Y0)
         # ---- backward -----------------------------------------------------------------------
         # every parameter gradient of the step -- the tail's dW / db / LayerNorm sums (collected from
         # its backward), dW_h += dout^h^T xa^h with dbias^h (the heads' column sums of dout), g_src
@@ -539,12 +550,12 @@ class ShardedTrainer:
         # launches over side lanes were the critical path (profiles/r03w_simprof_xagg_P8_rank0_timeline.txt)
         with ops.grouped_param_grads():
             coords_loc.backward(self.dcoords[r0:r1])
-        rs_own = self.rs[r0:r1]
         with torch.no_grad():
-            K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
-            # dxa^hd = dout^hd W_hd, both heads in one grouped launch
-            K.gemm_rows_grouped([(self.dout_l[:, hc[hd]], W[hc[hd]], self.dxa[:, hd * F:(hd + 1) * F], None, None)
-                                 for hd in (0, 1)], b_kmajor=1, name="gemm_dx")
+            if heads is None:
+                K.xagg_rows_bwd(self.act, o.grad, Y0, bias, self.dout_l, rs_own)
+                # dxa^hd = dout^hd W_hd, both heads in one grouped launch
+                K.gemm_rows_grouped([(self.dout_l[:, hc[hd]], W[hc[hd]], self.dxa[:, hd * F:(hd + 1) * F], None,
+                                      None) for hd in (0, 1)], b_kmajor=1, name="gemm_dx")
             heads = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
                       None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,

@@ -495,10 +495,13 @@ class HipKernels:
                                                    P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
                                                    _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
 
-    def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, coords=None):
+    def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, coords=None,
+                       heads=None):
         """The flagship's MLP tail forward in one launch (tail_fused.hip): returns (coords, saved)
         with saved = (Y1, st1, z1, Y2, st2, z2, y3, st3, z3); ``coords`` (contiguous [M, 3]): write
-        the output there (e.g. the rank's rows of the sharded step's all-gather buffer)."""
+        the output there (e.g. the rank's rows of the sharded step's all-gather buffer).
+        ``heads`` (``ops.TailHeads``): the head-fused form -- the input rows x (written) are
+        relu(xa^h W_h^T + b^h) of the xagg GATConv (hicgat_tail_fwd_fused_heads)."""
         M = x.shape[0]
         dev = x.device
         f = dict(dtype=torch.float32, device=dev)
@@ -511,16 +514,25 @@ class HipKernels:
         assert coords.shape == (M, 3) and coords.is_contiguous()
         ws = [W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4]
         assert all(t.is_contiguous() for t in ws) and x.stride(1) == 1
+        tail = [float(eps), P(Y1), P(st1), P(z1), P(Y2), P(st2), P(z2), P(y3), P(st3), P(z3), P(coords), _lib.stream(dev)]
         with _timed("tail_fwd_fused"):
-            _lib.check(self.lib.hicgat_tail_fwd_fused(P(x), x.stride(0), M, *[P(t) for t in ws], float(eps), P(Y1), P(st1),
-                                                      P(z1), P(Y2), P(st2), P(z2), P(y3), P(st3), P(z3), P(coords),
-                                                      _lib.stream(dev)), "hicgat_tail_fwd_fused")
+            if heads is None:
+                _lib.check(self.lib.hicgat_tail_fwd_fused(P(x), x.stride(0), M, *[P(t) for t in ws], *tail),
+                           "hicgat_tail_fwd_fused")
+            else:
+                h = heads
+                assert x.is_contiguous() and x.shape == (M, 512) and h.Y0.shape == (M, 512) and h.Y0.is_contiguous()
+                assert h.X4.shape[2] == M and h.X4.is_contiguous() and h.W.is_contiguous() and h.bias.is_contiguous()
+                _lib.check(self.lib.hicgat_tail_fwd_fused_heads(
+                    P(h.X4), h.X4.stride(2), h.X4.stride(0), P(h.W), P(h.bias), P(h.Y0), P(x), M, *[P(t) for t in ws],
+                    *tail), "hicgat_tail_fwd_fused_heads")
         return coords, (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)
 
-    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3):
+    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=None):
         """The tail's input-gradient chain in one launch (tail_fused.hip): returns (dx, dY1, dY2, dy3,
         (ws1, ws2, ws3)) -- the LayerNorm dgamma/dbeta partials stay in the workspaces
-        (``ln_relu_res_bwd_params``)."""
+        (``ln_relu_res_bwd_params``).  ``heads``: the head-fused form (dx None; the xagg GATConv's
+        dout, delta and dxa written into the ``ops.TailHeads`` buffers instead)."""
         Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = saved
         M = dcoords.shape[0]
         dev = dcoords.device
@@ -529,12 +541,26 @@ class HipKernels:
         ws = [_lib.workspace(self.lib.hicgat_tail_bwd_workspace_bytes(M, w), dev) for w in (256, 128, 64)]
         ts = [W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3]
         assert all(t.is_contiguous() for t in ts) and dcoords.is_contiguous()
+        wsa = [P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), P(ws[2]), ws[2].numel()]
         with _timed("tail_bwd_fused"):
-            _lib.check(self.lib.hicgat_tail_bwd_fused(
-                P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dx), P(dY1), P(dY2),
-                P(dy3), P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), P(ws[2]), ws[2].numel(), _lib.stream(dev)),
-                "hicgat_tail_bwd_fused")
+            if heads is None:
+                _lib.check(self.lib.hicgat_tail_bwd_fused(
+                    P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dx), P(dY1),
+                    P(dY2), P(dy3), *wsa, _lib.stream(dev)), "hicgat_tail_bwd_fused")
+            else:
+                h = heads
+                assert h.dout.shape == (M, 512) and h.dout.is_contiguous() and h.dxa.shape == (M, 1024)
+                assert h.dxa.is_contiguous() and h.rs.shape == (M, 8) and h.rs.is_contiguous()
+                dx = None
+                _lib.check(self.lib.hicgat_tail_bwd_fused_heads(
+                    P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dY1), P(dY2),
+                    P(dy3), *wsa, int(h.act), P(h.Y0), P(h.W), P(h.bias), P(h.dout), P(h.rs), P(h.dxa),
+                    _lib.stream(dev)), "hicgat_tail_bwd_fused_heads")
         return dx, dY1, dY2, dy3, ws
+
+    def tail_waves(self):
+        """Waves per workgroup of the fused tail kernels (hicgat_tail_bwd_waves)."""
+        return int(self.lib.hicgat_tail_bwd_waves())
 
     def tail_partial_rows(self, M):
         """Rows of LayerNorm partials hicgat_tail_bwd_fused leaves per workspace: one per wave."""

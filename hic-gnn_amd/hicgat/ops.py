@@ -668,14 +668,17 @@ class _FusedTailFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3, eps,
-                coords_out=None):
+                coords_out=None, heads=None):
         K = kernels.default()
         x = x.contiguous()
         W1c, b1c = _joined(Wa, Wal).contiguous(), _joined(ba, bal).contiguous()
         W2c, b2c = _joined(W1, W1al).contiguous(), _joined(b1, b1al).contiguous()
+        # heads: x's rows are formed (written) by the kernel from the xagg GATConv's aggregates
         coords, saved = K.tail_fwd_fused(x, W1c, b1c, ga.contiguous(), bea.contiguous(), W2c, b2c, g1.contiguous(),
                                          be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
-                                         be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out)
+                                         be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out,
+                                         heads=heads)
+        ctx.heads = heads
         if coords_out is not None:
             # the kernel wrote into the caller's buffer (e.g. the all-gather rows); the output is a
             # fresh tensor object over the same memory, so autograd sees a new output (no view or
@@ -700,7 +703,7 @@ class _FusedTailFn(torch.autograd.Function):
             dx, dY1, dY2, dy3, (ws1, ws2, ws3) = K.tail_bwd_fused(
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
-                g2.contiguous(), be2.contiguous())
+                g2.contiguous(), be2.contiguous(), heads=ctx.heads)
             rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per wave
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)
@@ -710,7 +713,7 @@ class _FusedTailFn(torch.autograd.Function):
             dga, dbea = _ln_param_grads(K, ga, bea, ws1, rows)
             dWa, dba, dWal, dbal = _dual_param_grads(K, Wa, ba, Wal, bal, dY1, x)
             return (dx if ctx.needs_input_grad[0] else None, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al,
-                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None, None)
+                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None, None, None)
         T = (True,) * 8
 
         def c(**kw):
@@ -726,7 +729,7 @@ class _FusedTailFn(torch.autograd.Function):
                                      saved_tensors=(x, Y1, st1, ga, bea), params=(Wa, ba, Wal, bal, ga, bea))
         dx, dWa, dba, dWal, dbal, dga, dbea, _ = _DualLnReluResFn.backward(ctx1, dz1)
         return (dx, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al, dg1, dbe1, dW2, db2, dg2, dbe2,
-                dW3, db3, None, None)
+                dW3, db3, None, None, None)
 
 
 def fused_tail_ok(model, x):
@@ -736,14 +739,36 @@ def fused_tail_ok(model, x):
             and model.norm_a.eps == model.norm1.eps == model.norm2.eps)
 
 
-def fused_tail(model, x, coords_out=None):
+class TailHeads:
+    """The xagg GATConv's operands of the head-fused tail kernels (hicgat_tail_{fwd,bwd}_fused_heads):
+    X4 [2, 2, M, 512] (xa^h = X4[h, 0]), lin_l's weight W [512, 512] and bias [512], and the buffers
+    they write: Y0 [M, 512] (the forward; the tail's input rows relu(Y0) go into ``fused_tail``'s x),
+    dout [M, 512], the own rows' row stats rs [M, 8] and dxa [M, 1024] (the backward)."""
+
+    def __init__(self, X4, W, bias, Y0, dout, rs, dxa, act=1):
+        self.X4, self.W, self.bias, self.Y0, self.dout, self.rs, self.dxa, self.act = X4, W, bias, Y0, dout, rs, dxa, act
+
+
+# HICGAT_TAIL_HEADS=0: the xagg step keeps its per-head GEMM launches, rows pass and dxa GEMMs
+TAIL_HEADS = os.environ.get("HICGAT_TAIL_HEADS", "1") != "0"
+
+
+def tail_heads_ok(model, x):
+    return TAIL_HEADS and FUSED_TAIL_BWD and fused_tail_ok(model, x) and kernels.default().tail_waves() == 8
+
+
+def fused_tail(model, x, coords_out=None, heads=None):
     """GATNetSelectiveResidualsUpdated.post_act on the fused forward (``fused_tail_ok`` first);
-    ``coords_out``: a contiguous [M, 3] buffer the coordinates are written into (and returned)."""
+    ``coords_out``: a contiguous [M, 3] buffer the coordinates are written into (and returned);
+    ``heads`` (``TailHeads``, ``tail_heads_ok`` first): x's rows are formed from the xagg GATConv's
+    aggregates in the same launch (x is written), and the backward writes the GATConv's dout /
+    delta / dxa instead of x's gradient."""
     m = model
     return _FusedTailFn.apply(x, m.densea.weight, m.densea.bias, m.align_densea.weight, m.align_densea.bias,
                               m.norm_a.weight, m.norm_a.bias, m.dense1.weight, m.dense1.bias, m.align_dense1.weight,
                               m.align_dense1.bias, m.norm1.weight, m.norm1.bias, m.dense2.weight, m.dense2.bias,
-                              m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps, coords_out)
+                              m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps, coords_out,
+                              heads)
 
 
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):

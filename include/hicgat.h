@@ -478,6 +478,30 @@ int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const fl
                           const float *be2, const float *g3, const float *be3, float *dx, float *dY1, float *dY2,
                           float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
                           size_t ws3_bytes, hicgat_stream_t stream);
+/* The head-fused forms for the sharded aggregate-first GATConv (hicgat.dist "xagg"; the GATConv of
+ * models.py:619 by linearity per head, then the tail): the forward forms the tail's input rows
+ * itself, Y0[:, 256h:256h+256] = xa^h W_h^T + b^h (xa^h = xa + h * xa_head_stride, [M][ld_xa]; W_h =
+ * rows 256h.. of lin_l's weight Wh [512][512]; bh [512]) and O = relu(Y0) (both [M][512], written),
+ * replacing the per-head GEMM launches and their slab sum; then the tail as hicgat_tail_fwd_fused.
+ * The backward runs the chain of hicgat_tail_bwd_fused and, instead of writing dx, the GATConv's rows
+ * backward and its input-gradient GEMM: dout = dx * (Y0 > 0) (act = 1; act = 0: dout = dx) into
+ * dout [M][512], delta^h = <dout^h, Y0^h - b^h> into row_stats[8r + 4 + h] (its [4:6] S3 values move
+ * to [6:8], as hicgat_xagg_rows_bwd does), dxa [M][1024] = [dout^0 W_0 | dout^1 W_1].  Both need
+ * hicgat_tail_bwd_waves() == 8 (else HICGAT_EUNSUPPORTED). */
+int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64_t xa_head_stride, const float *Wh,
+                                const float *bh, float *Y0, float *O, int M, const float *W1c, const float *b1c,
+                                const float *g1, const float *be1, const float *W2c, const float *b2c, const float *g2,
+                                const float *be2, const float *W3, const float *b3, const float *g3, const float *be3,
+                                const float *W4, const float *b4, float eps, float *Y1, float *st1, float *z1,
+                                float *Y2, float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
+                                hicgat_stream_t stream);
+int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
+                                const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
+                                const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
+                                const float *be2, const float *g3, const float *be3, float *dY1, float *dY2,
+                                float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
+                                size_t ws3_bytes, int act, const float *Y0, const float *Wh, const float *bh,
+                                float *dout, float *row_stats, float *dxa, hicgat_stream_t stream);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --

@@ -326,3 +326,46 @@ def test_world1_step_matches_float64_standin(mode, n):
     assert abs(lg - lc) <= 1e-5 * abs(lc)
     for k, (d, m, _) in per.items():
         assert d <= 2e-4 * m, (k, d, m)
+
+
+@pytest.mark.parametrize("n,world", [(3000, 1), (3000, 2)])
+def test_xagg_head_fused_tail_matches_separate_launches(n, world):
+    """The head-fused tail kernels (hicgat_tail_{fwd,bwd}_fused_heads: the xagg GATConv's per-head
+    GEMMs + bias / relu before the tail, its rows backward and dxa GEMMs after the tail's backward)
+    against the separate launches (grouped row GEMMs, xagg_rows_bwd), rank 0 of ``world`` simulated
+    ranks, two eager steps and two graph replays: the same loss to 1e-6, gradients to 1e-5 of their
+    max (the head GEMMs sum K in another order), and the captured form replays bit-equal to eager."""
+    from hicgat import ops
+    hicgat, adj, truth, x = _inputs(n, "cuda")
+    res = {}
+    saved = ops.TAIL_HEADS
+    try:
+        for heads in (False, True):
+            ops.TAIL_HEADS = heads
+            out = []
+            for graphed in (False, True):
+                torch.manual_seed(0)
+                model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+                tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, comm=hicgat.dist.SimComm(world, 0),
+                                                mode="xagg")
+                assert ops.tail_heads_ok(model, tr.O) == heads
+                losses, grads = [], []
+                if graphed:
+                    step = tr.captured(warmup=0)
+                else:
+                    tr.opt.enable_device_step()
+                    step = tr.step
+                for _ in range(2):
+                    losses.append(float(step()[0]))
+                    grads.append(tr.opt.grad.clone())
+                torch.cuda.synchronize()
+                out.append((losses, grads, tr.opt.flat.clone()))
+            (le, ge, pe), (lg, gg, pg) = out
+            assert le == lg and all(torch.equal(a, b) for a, b in zip(ge, gg)) and torch.equal(pe, pg), heads
+            res[heads] = out[0]
+    finally:
+        ops.TAIL_HEADS = saved
+    (l0, g0, _), (l1, g1, _) = res[False], res[True]
+    assert abs(l1[0] - l0[0]) <= 1e-6 * abs(l0[0]), (l0, l1)
+    assert (g1[0] - g0[0]).abs().max().item() <= 1e-5 * g0[0].abs().max().item()
+    assert abs(l1[1] - l0[1]) <= 1e-4 * abs(l0[1]), (l0, l1)
