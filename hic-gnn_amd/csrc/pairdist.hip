@@ -55,6 +55,15 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+#ifndef HICGAT_PD_SUPPORT_RIDES
+#define HICGAT_PD_SUPPORT_RIDES 1   // sharded shares: the support blocks in the tile launch (A/B builds: 0)
+#endif
+constexpr bool SUPPORT_RIDES = HICGAT_PD_SUPPORT_RIDES;
+
+#ifndef HICGAT_PD_ILV
+#define HICGAT_PD_ILV 1   // packed interior path: the four column pairs interleaved stage by stage
+#endif
+
 // v + the values of lanes l^16, l^32 and l^48 (ds_bpermute shuffles; a v_permlane16/32_swap form
 // measured slower: the loss chain 0.162 vs 0.157 ms, profiles/r04h_kbench_pairdist.txt)
 __device__ __forceinline__ float sum_rows4(float v) {
@@ -217,6 +226,57 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       tv[3] = f2{b.z, b.w};
     }
     f2 px = z2, py = z2, pz = z2;
+#if HICGAT_PD_ILV
+    // the four column pairs' chains stage by stage (every dependent packed op / v_rsq use then has
+    // independent work between it and its producer: no s_nop wait states in the issue stream); the
+    // arithmetic and its order per pair are those of the one-pair-at-a-time form below
+    f2 dx[4], dy[4], dz[4], d2[4], inv[4], r[4], w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      dx[h] = rx - cx2[h];
+      dy[h] = ry - cy2[h];
+      dz[h] = rz - cz2[h];
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dz[h], dz[h], f2{0x1.0p-100f, 0x1.0p-100f});
+#pragma unroll
+    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dy[h], dy[h], d2[h]);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dx[h], dx[h], d2[h]);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) inv[h] = f2{__builtin_amdgcn_rsqf(d2[h].x), __builtin_amdgcn_rsqf(d2[h].y)};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) r[h] = d2[h] * inv[h] - tv[h];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      L2 = __builtin_elementwise_fma(r[h], r[h], L2);
+      if (PEARSON) {
+        const f2 d = d2[h] * inv[h];
+        sd2 += d;
+        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
+        sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
+        st2 += tv[h];
+        stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) w[h] = r[h] * inv[h];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      px = __builtin_elementwise_fma(w[h], dx[h], px);
+      ax2[h] = __builtin_elementwise_fma(-w[h], dx[h], ax2[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      py = __builtin_elementwise_fma(w[h], dy[h], py);
+      ay2[h] = __builtin_elementwise_fma(-w[h], dy[h], ay2[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      pz = __builtin_elementwise_fma(w[h], dz[h], pz);
+      az2[h] = __builtin_elementwise_fma(-w[h], dz[h], az2[h]);
+    }
+#else
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const f2 dx = rx - cx2[h], dy = ry - cy2[h], dz = rz - cz2[h];
@@ -243,6 +303,7 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       ay2[h] = __builtin_elementwise_fma(-w, dy, ay2[h]);
       az2[h] = __builtin_elementwise_fma(-w, dz, az2[h]);
     }
+#endif
     if constexpr (RLDS) {
       rowpart[lr * kRowPad + tx] = make_float4(px.x + px.y, py.x + py.y, pz.x + pz.y, 0.f);
     } else {
@@ -281,15 +342,39 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
 #ifndef HICGAT_PD_BG_OCC
 #define HICGAT_PD_BG_OCC 1   // workgroups per CU the background form's register budget is set for
 #endif
-template <int MODE, bool VEC, bool PEARSON, bool BG = false>
+template <bool PEARSON>
+__device__ void support_block(const float *__restrict__ coords, float bg, int row_begin, int row_end,
+                              const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                              const float *__restrict__ val, const float *__restrict__ diag, float4 *__restrict__ corr,
+                              double *__restrict__ mom, const int *__restrict__ cmap, int blk);
+
+// The support pass riding in the background-form tile launch (SUP): blocks [ntiles, ntiles +
+// blocks) of the grid run pairdist_support_kernel's work for support block (blockIdx.x - ntiles).
+struct SupportArgs {
+  const int32_t *rowptr = nullptr, *col = nullptr;
+  const float *val = nullptr, *diag = nullptr;
+  float4 *corr = nullptr;
+  double *mom = nullptr;
+  int row_begin = 0, row_end = 0;
+  int64_t ntiles = 0;
+};
+
+template <int MODE, bool VEC, bool PEARSON, bool BG = false, bool SUP = false>
 __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
                                                             int64_t ldt, int64_t row0, int64_t col0,
                                                             int nb, int64_t t0,
                                                             float4 *__restrict__ part,
                                                             double *__restrict__ mom, float bg,
-                                                            const int *__restrict__ cmap = nullptr) {
+                                                            const int *__restrict__ cmap = nullptr,
+                                                            const SupportArgs sup = SupportArgs{}) {
   static_assert(!BG || (MODE == MODE_SYM && !VEC), "the background form is the training loss without a T image");
+  static_assert(!SUP || BG, "the support pass rides only in the background form's launch");
+  if (SUP && (int64_t)blockIdx.x >= sup.ntiles) {   // block-uniform
+    support_block<PEARSON>(coords, bg, sup.row_begin, sup.row_end, sup.rowptr, sup.col, sup.val, sup.diag, sup.corr,
+                           sup.mom, cmap, (int)(blockIdx.x - sup.ntiles));
+    return;
+  }
   // one dynamic LDS array: [T tile 128x128 fp32 (VEC only)] -- 64 KiB, 16-B aligned
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ float sc[2][BT][3];
@@ -586,17 +671,14 @@ __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__re
 //             diagonal's (0 - T_ii)^2 into the dg moment.
 // d is formed exactly as in the bulk's interior path.  Per-block moment records (fixed order).
 template <bool PEARSON>
-__global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__restrict__ coords, int N, float bg,
-                                                               int row_begin, int row_end,
-                                                               const int32_t *__restrict__ rowptr,
-                                                               const int32_t *__restrict__ col,
-                                                               const float *__restrict__ val,
-                                                               const float *__restrict__ diag,
-                                                               float4 *__restrict__ corr, double *__restrict__ mom,
-                                                               const int *__restrict__ cmap) {
+__device__ void support_block(const float *__restrict__ coords, float bg, int row_begin, int row_end,
+                                              const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                                              const float *__restrict__ val, const float *__restrict__ diag,
+                                              float4 *__restrict__ corr, double *__restrict__ mom,
+                                              const int *__restrict__ cmap, int blk) {
   __shared__ double mred[4][7];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = row_begin + blockIdx.x * 4 + wv;
+  const int i = row_begin + blk * 4 + wv;
   float gx = 0.f, gy = 0.f, gz = 0.f;
   double L = 0.0, sdt = 0.0, st = 0.0, stt = 0.0, dg = 0.0;   // the support's moment changes in fp64
   if (i < row_end) {   // wave-uniform
@@ -649,8 +731,20 @@ __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__re
   }
   __syncthreads();
   if (threadIdx.x < 7)
-    mom[(size_t)blockIdx.x * 8 + threadIdx.x] =
+    mom[(size_t)blk * 8 + threadIdx.x] =
         ((mred[0][threadIdx.x] + mred[1][threadIdx.x]) + mred[2][threadIdx.x]) + mred[3][threadIdx.x];
+}
+
+template <bool PEARSON>
+__global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__restrict__ coords, int N, float bg,
+                                                               int row_begin, int row_end,
+                                                               const int32_t *__restrict__ rowptr,
+                                                               const int32_t *__restrict__ col,
+                                                               const float *__restrict__ val,
+                                                               const float *__restrict__ diag,
+                                                               float4 *__restrict__ corr, double *__restrict__ mom,
+                                                               const int *__restrict__ cmap) {
+  support_block<PEARSON>(coords, bg, row_begin, row_end, rowptr, col, val, diag, corr, mom, cmap, blockIdx.x);
 }
 
 // D[i, j] = ||c_i - c_j||: one thread per element.
@@ -888,7 +982,31 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
   hipStream_t s = (hipStream_t)stream;
   // bulk: every pair i < j of the tile range at the background value (no T read); support: the
   // entries of rows [support_row_begin, support_row_end) that differ, and those rows' diagonal
-  if (nt > 0) {
+  // a rank's share (dcoords64: the sharded step): the support blocks ride in the tile launch (one
+  // launch fewer on the critical path; at N = 20000 on one GPU the support pass needs the occupancy
+  // of its own launch: 1.925 vs 1.915 ms per step)
+  const bool ride = dcoords64 && SUPPORT_RIDES && nt > 0 && sblocks > 0;
+  if (ride) {
+    SupportArgs sa;
+    sa.rowptr = rowptr;
+    sa.col = col;
+    sa.val = val;
+    sa.diag = diag;
+    sa.corr = corr;
+    sa.mom = mom + (size_t)tile_end * 8;
+    sa.row_begin = support_row_begin;
+    sa.row_end = support_row_end;
+    sa.ntiles = nt;
+    if (loss_kind == 1)
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true, true>), dim3(nt + sblocks), dim3(256), 0, s,
+                         coords, nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background,
+                         cmap, sa);
+    else
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true, true>), dim3(nt + sblocks), dim3(256), 0,
+                         s, coords, nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom,
+                         background, cmap, sa);
+    HICGAT_CHECK_LAUNCH();
+  } else if (nt > 0) {
     if (loss_kind == 1)
       hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(nt), dim3(256), 0, s, coords,
                          nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
@@ -897,7 +1015,7 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
                          nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
     HICGAT_CHECK_LAUNCH();
   }
-  if (sblocks > 0) {
+  if (sblocks > 0 && !ride) {
     if (loss_kind == 1)
       hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
                          support_row_begin, support_row_end, rowptr, col, val, diag, corr,

@@ -157,6 +157,7 @@ __global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16, NT1 = 32 / NW, NT2 = 16 / NW;   // 16-column tiles per wave: block 1 / block 2
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW: 4, 8 or 16 waves");
   // x rows (HEADS: xa^0 rows -> As, xa^1 rows -> Bs) -> LDS (rows past M: zeros)
   for (int e = tid; e < (HEADS ? 2 : 1) * RB * 128; e += 64 * NW) {
     const int hd = e / (RB * 128), r = (e >> 7) % RB, c4 = e & 127;
@@ -166,18 +167,19 @@ __global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
   }
   __syncthreads();
   if constexpr (HEADS) {
-    static_assert(NW == 8, "the head GEMMs take 4 waves per head");
-    const int hd = wv >> 2, n0 = 64 * (wv & 3);
-    f32x4 acc[H][4];
+    static_assert(NW == 8 || NW == 16, "the head GEMMs take NW / 2 waves per head");
+    constexpr int HW = NW / 2, NTH = 16 / HW;   // waves per head, 16-column tiles per wave
+    const int hd = wv / HW, n0 = 16 * NTH * (wv % HW);
+    f32x4 acc[H][NTH];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, 4, 512>(hd ? Bs : As, XS, Wh + (size_t)hd * 256 * 512, n0, acc, lane);
+      for (int t = 0; t < NTH; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows<RB, NTH, 512>(hd ? Bs : As, XS, Wh + (size_t)hd * 256 * 512, n0, acc, lane);
     __syncthreads();   // every wave is done with xa^0 / xa^1 before As takes relu(out)
     const int li = lane & 15, r0 = 4 * (lane >> 4);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < NTH; ++t) {
       const int c = 256 * hd + n0 + 16 * t + li;
       const float bb = bh[c];
 #pragma unroll
@@ -405,8 +407,8 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
   ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, m0, M, wv, lane);
   __syncthreads();
   // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 16 ND wv ..
-  constexpr int ND = 8 / NW, NT2 = 16 / NW, NT1 = 32 / NW;
-  {
+  constexpr int WD = NW < 8 ? NW : 8, ND = 8 / WD, NT2 = 16 / NW, NT1 = 32 / NW;   // dense2: WD waves
+  if (wv < WD) {
     f32x4 acc[H][ND];
 #pragma unroll
     for (int h = 0; h < H; ++h)
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     put_tiles<RB, NT1>(acc, 16 * NT1 * wv, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
   }
   if constexpr (HEADS) {
-    static_assert(NW == 8, "the dxa GEMMs take 4 waves per head");
+    static_assert(NW == 8 || NW == 16, "the dxa GEMMs take NW / 2 waves per head");
     __syncthreads();
     // rows: lane l holds float4 l (head 0) and 64 + l (head 1) of the row, as xagg_rows_bwd_kernel
     for (int rr = wv; rr < RB; rr += NW) {
@@ -480,14 +482,15 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
       }
     }
     __syncthreads();
-    const int hd = wv >> 2, n0 = 128 * (wv & 3);
-    f32x4 acc[H][8];
+    constexpr int HW = NW / 2, NTX = 32 / HW;   // waves per head, 16-column tiles per wave
+    const int hd = wv / HW, n0 = 16 * NTX * (wv % HW);
+    f32x4 acc[H][NTX];
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, 8, 256>(As + 256 * hd, XS, Wh + (size_t)hd * 256 * 512, 512, n0, acc, lane);
-    put_tiles<RB, 8>(acc, n0, nullptr, 0, dxa + 512 * hd, 1024, m0, M, lane);
+      for (int t = 0; t < NTX; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mfma_rows_t<RB, NTX, 256>(As + 256 * hd, XS, Wh + (size_t)hd * 256 * 512, 512, n0, acc, lane);
+    put_tiles<RB, NTX>(acc, n0, nullptr, 0, dxa + 512 * hd, 1024, m0, M, lane);
   }
 }
 
@@ -557,7 +560,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
                                            const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2,
                                            float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
                                            hicgat_stream_t stream) {
-  if (HICGAT_TAIL_WAVES != 8) return HICGAT_EUNSUPPORTED;
+  if (HICGAT_TAIL_WAVES < 8) return HICGAT_EUNSUPPORTED;
   TailHeads hh;
   hh.xa = xa;
   hh.xa_hs = xa_head_stride;
@@ -639,7 +642,7 @@ extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const fl
                                            size_t ws3_bytes, int act, const float *Y0, const float *Wh,
                                            const float *bh, float *dout, float *row_stats, float *dxa,
                                            hicgat_stream_t stream) {
-  if (HICGAT_TAIL_WAVES != 8) return HICGAT_EUNSUPPORTED;
+  if (HICGAT_TAIL_WAVES < 8) return HICGAT_EUNSUPPORTED;
   TailHeadsBwd hh;
   hh.act = act ? 1 : 0;
   hh.Y0 = Y0;

@@ -754,7 +754,7 @@ TAIL_HEADS = os.environ.get("HICGAT_TAIL_HEADS", "1") != "0"
 
 
 def tail_heads_ok(model, x):
-    return TAIL_HEADS and FUSED_TAIL_BWD and fused_tail_ok(model, x) and kernels.default().tail_waves() == 8
+    return TAIL_HEADS and FUSED_TAIL_BWD and fused_tail_ok(model, x) and kernels.default().tail_waves() >= 8
 
 
 def fused_tail(model, x, coords_out=None, heads=None):

@@ -6,6 +6,7 @@
 # steps (each under its own time limit; the script stops at the first failure):
 #   tests        pytest -m gpu (whole GPU suite)
 #   tests:<k>    pytest -m gpu -k <k>   (testsoft:<k>: test failures do not stop the later steps)
+#   testenv:<env>:<k> pytest -m gpu -k <k> under an environment assignment
 #   smoke        __graft_entry__.smoke()
 #   bench        default bench.py (N = 1, synth-20000, with the CPU baseline)
 #   bench2000    bench.py --workload synth-2000 --no-cpu-baseline
@@ -19,6 +20,7 @@
 #   kb:<jobs>:<libs> tools/kbench.py A/B of the named kernel jobs over the listed library builds
 #   simab:<env>  rank 0 of the simulated 8-rank xagg step (100 steps) under the environment assignment <env>
 #   probe[:<env>] tools/xagg_probe.py: rank 0's xagg kernels one by one (optionally under <env>)
+#   probegrads   the same plus the grouped parameter-gradient launches broken down by job
 #   simprof      rocprofv3 kernel trace of rank 0's share of the simulated 8-rank step (+ one step's timeline)
 #   align        the config-5 generalisation run (python -m hicgat.align) on chr19 1 mb -> 500 kb
 #   n2v          node2vec feature study (tools/n2v_study.py): embedding structure + K=3000 dSCC per max_waves / seed
@@ -43,6 +45,11 @@ for S in "$@"; do
         > gpurun_out/${T}_pytest_k.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_k.log
       # testsoft: test failures (rc 1) do not stop the later steps; a crash / timeout does
       if [ "${S%%:*}" = testsoft ]; then [ $rc -le 1 ] || exit $rc; else [ $rc -eq 0 ] || exit $rc; fi ;;
+    testenv:*)
+      # testenv:<env assignment>:<k>  pytest -m gpu -k <k> under the environment assignment (e.g. HICGAT_LIB=...)
+      R=${S#testenv:}; E=${R%%:*}; K=${R#*:}
+      env $E timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf -s --timeout 300 --timeout-method thread -k "$K" \
+        > gpurun_out/${T}_pytest_env.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_env.log; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || exit $?
       tail -1 gpurun_out/${T}_smoke.log ;;
@@ -97,10 +104,10 @@ for S in "$@"; do
       R=${S#kb:}; J=${R%%:*}; L=${R#*:}
       timeout -k 10 300 python tools/kbench.py --only "$J" --libs "$L" --reps 20 --rounds 3 > gpurun_out/${T}_kbench.txt 2>&1 || exit $?
       cat gpurun_out/${T}_kbench.txt | grep " med " ;;
-    probe|probe:*)
-      E=${S#probe}; E=${E#:}
-      env $E timeout -k 10 300 python tools/xagg_probe.py > gpurun_out/${T}_probe.txt 2>&1 || exit $?
-      cat gpurun_out/${T}_probe.txt | tail -12 ;;
+    probe|probe:*|probegrads)
+      E=${S#probe}; E=${E#:}; G=""; [ "$S" = probegrads ] && { E=""; G="--grads"; }
+      env $E timeout -k 10 300 python tools/xagg_probe.py $G > gpurun_out/${T}_probe.txt 2>&1 || exit $?
+      grep " us$" gpurun_out/${T}_probe.txt ;;
     simprof|simprof_ag|simprof_xa)
       M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--grads", action="store_true", help="break the grouped parameter-gradient launches down by job")
     a = ap.parse_args()
     import bench
     import hicgat
@@ -38,6 +39,18 @@ def main():
     model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
     tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, mode="xagg",
                               comm=hdist.SimComm(a.world, a.rank))
+    rec = []
+    if a.grads:   # record the grouped launch's job lists of one eager step
+        K0 = tr.K
+        orig = K0.param_grads_grouped
+
+        def spy(w, c, target=None):
+            rec.append((list(w), list(c), target))
+            return orig(w, c, target)
+        K0.param_grads_grouped = spy
+        tr.opt.enable_device_step()
+        tr.step()
+        K0.param_grads_grouped = orig
     step = tr.captured(warmup=2)
     for _ in range(a.steps):
         step()
@@ -65,11 +78,22 @@ def main():
                                                                    tr.rs, dz, tr.ns, tr.gpart))
     res["dxa grouped GEMM"] = timeit(lambda: K.gemm_rows_grouped(
         [(tr.dout_l[:, hc[hd]], W[hc[hd]], tr.dxa[:, hd * F:(hd + 1) * F], None, None) for hd in (0, 1)], b_kmajor=1))
+    if rec:
+        w, c, tg = rec[-1]
+        Kp = tr.K
+        res["grads: both launches"] = timeit(lambda: Kp.param_grads_grouped(w, c, tg))
+        res["grads: weight-gradient jobs only (+ their slab sums)"] = timeit(lambda: Kp.param_grads_grouped(w, [], tg))
+        for k, job in enumerate(c):
+            res[f"grads: colsum job {k} {tuple(job[0].shape)}{' weighted' if len(job) > 3 else ''}"] = \
+                timeit(lambda job=job: Kp.param_grads_grouped([], [job], tg))
+        for k, job in enumerate(w):
+            res[f"grads: wgrad job {k} dy {tuple(job[0].shape)} x {tuple(job[1].shape)}"] = \
+                timeit(lambda job=job: Kp.param_grads_grouped([job], [], tg))
     print(f"rank {a.rank} of {a.world}: rows {tr.local_rows}, nnz {tr.local_nnz}, dxa finite "
           f"{bool(torch.isfinite(tr.dxa).all())}, |dxa| max {float(tr.dxa.abs().max()):.3e}, "
           f"denormal frac {float(((tr.dxa.abs() < 1.2e-38) & (tr.dxa != 0)).float().mean()):.3e}")
     for k, v in res.items():
-        print(f"{k:32s} {v:9.1f} us")
+        print(f"{k:48s} {v:9.1f} us")
 
 
 if __name__ == "__main__":
