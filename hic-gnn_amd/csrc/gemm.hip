@@ -323,6 +323,10 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
+#ifndef HICGAT_TALL_LG0_ROWS
+#define HICGAT_TALL_LG0_ROWS 1024   // grouped column sums: jobs taller than this use one lane per row group
+#endif
+constexpr int64_t TALL_LG0_ROWS = HICGAT_TALL_LG0_ROWS;
 #ifndef HICGAT_GROUP_DB
 #define HICGAT_GROUP_DB 0   // 1: double-buffered LDS in the grouped weight-gradient tiles (A/B builds)
 #endif
@@ -616,7 +620,9 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     J.cols = cols;
     J.accumulate = acc;
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : 2;
+    // lanes per row group: short chains per lane for tall jobs (a rank's weighted sums over its 2 700
+    // rows: 11 rows per lane at lg 0 instead of 42 at lg 2, two rounds of loads instead of six)
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : rows <= TALL_LG0_ROWS ? 2 : 0;
     J.blk0 = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
     blk += (int)((cols + per - 1) / per);

@@ -60,10 +60,6 @@ __device__ __forceinline__ float sum16(float v) {
 #endif
 constexpr bool SUPPORT_RIDES = HICGAT_PD_SUPPORT_RIDES;
 
-#ifndef HICGAT_PD_ILV
-#define HICGAT_PD_ILV 1   // packed interior path: the four column pairs interleaved stage by stage
-#endif
-
 // v + the values of lanes l^16, l^32 and l^48 (ds_bpermute shuffles; a v_permlane16/32_swap form
 // measured slower: the loss chain 0.162 vs 0.157 ms, profiles/r04h_kbench_pairdist.txt)
 __device__ __forceinline__ float sum_rows4(float v) {
@@ -226,57 +222,6 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       tv[3] = f2{b.z, b.w};
     }
     f2 px = z2, py = z2, pz = z2;
-#if HICGAT_PD_ILV
-    // the four column pairs' chains stage by stage (every dependent packed op / v_rsq use then has
-    // independent work between it and its producer: no s_nop wait states in the issue stream); the
-    // arithmetic and its order per pair are those of the one-pair-at-a-time form below
-    f2 dx[4], dy[4], dz[4], d2[4], inv[4], r[4], w[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      dx[h] = rx - cx2[h];
-      dy[h] = ry - cy2[h];
-      dz[h] = rz - cz2[h];
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dz[h], dz[h], f2{0x1.0p-100f, 0x1.0p-100f});
-#pragma unroll
-    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dy[h], dy[h], d2[h]);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) d2[h] = __builtin_elementwise_fma(dx[h], dx[h], d2[h]);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) inv[h] = f2{__builtin_amdgcn_rsqf(d2[h].x), __builtin_amdgcn_rsqf(d2[h].y)};
-#pragma unroll
-    for (int h = 0; h < 4; ++h) r[h] = d2[h] * inv[h] - tv[h];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      L2 = __builtin_elementwise_fma(r[h], r[h], L2);
-      if (PEARSON) {
-        const f2 d = d2[h] * inv[h];
-        sd2 += d;
-        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
-        sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
-        st2 += tv[h];
-        stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) w[h] = r[h] * inv[h];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      px = __builtin_elementwise_fma(w[h], dx[h], px);
-      ax2[h] = __builtin_elementwise_fma(-w[h], dx[h], ax2[h]);
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      py = __builtin_elementwise_fma(w[h], dy[h], py);
-      ay2[h] = __builtin_elementwise_fma(-w[h], dy[h], ay2[h]);
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      pz = __builtin_elementwise_fma(w[h], dz[h], pz);
-      az2[h] = __builtin_elementwise_fma(-w[h], dz[h], az2[h]);
-    }
-#else
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const f2 dx = rx - cx2[h], dy = ry - cy2[h], dz = rz - cz2[h];
@@ -303,7 +248,6 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       ay2[h] = __builtin_elementwise_fma(-w, dy, ay2[h]);
       az2[h] = __builtin_elementwise_fma(-w, dz, az2[h]);
     }
-#endif
     if constexpr (RLDS) {
       rowpart[lr * kRowPad + tx] = make_float4(px.x + px.y, py.x + py.y, pz.x + pz.y, 0.f);
     } else {

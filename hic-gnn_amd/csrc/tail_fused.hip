@@ -129,11 +129,12 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
 
 // RB rows per workgroup (the launch uses 16), NW waves: every GEMM stage splits its output columns
 // over the waves (a column's k order, hence its bits, do not depend on NW), the LayerNorm rows too.
-// NW = 8: two waves per SIMD, so one wave's weight loads and LDS reads hide under the other's MFMAs
-// (with 4, one wave per SIMD, every latency of the chain is exposed; a rank's shard at P = 8 has
-// 157 workgroups for 256 CUs, one each).
+// NW = 16: four waves per SIMD, so the waves' weight loads and LDS reads hide under each other's
+// MFMAs (with 4, one wave per SIMD, every latency of the chain is exposed; 8: 52 vs 62 us for the
+// P = 8 shard's forward; 16: rank step 0.438-0.440 vs 0.448 ms -- a rank's shard at P = 8 has 169
+// workgroups for 256 CUs, one each).  The LayerNorm parameter partials are one row per wave.
 #ifndef HICGAT_TAIL_WAVES
-#define HICGAT_TAIL_WAVES 8
+#define HICGAT_TAIL_WAVES 16   // 16: 0.438 / 0.440 vs 0.448 ms per P = 8 rank step (profiles/r04k_sim_ab.txt)
 #endif
 // HEADS (the sharded aggregate-first GATConv, gat_xagg.hip): the tail's input rows are formed here
 // from the two heads' aggregates, out^h = xa^h W_h^T + b^h (xa^h = x + h * xa_hs, row stride ldx; W_h

@@ -295,8 +295,9 @@ class _GATConvFn(torch.autograd.Function):
         else:
             K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
         side_flush(after=fork)
-        # after the gathers: the GAT column sums, then lin_l's dW on this stream (beside the side
-        # stream's first-block dW)
+        # after the gathers: the GAT column sums, then lin_l's dW on this stream (with the held
+        # first-block dW: BIG_GROUP).  The column sums on a side stream beside the grouped dW launch:
+        # 1.964 / 1.970 vs 1.877 / 1.872 ms per step (profiles/r04l_ab_single_gpu.txt)
         if use_sinks:
             K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
                          accumulate=True)
