@@ -63,6 +63,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ p, const 
 
 __global__ void step_increment_kernel(int64_t *step_ctr) { *step_ctr += 1; }
 
+// zero_grad + the device step count's advance in one launch (the step's first; its Adam then runs
+// with counted = 1)
+__global__ __launch_bounds__(256) void step_begin_kernel(float *__restrict__ grad, int64_t n,
+                                                         int64_t *__restrict__ step_ctr) {
+  if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] = step_ctr[0] + 1;
+  const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) reinterpret_cast<float4 *>(grad)[i] = z;
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) grad[i] = 0.f;
+}
+
 }  // namespace hicgat
 
 using namespace hicgat;
@@ -126,4 +137,14 @@ extern "C" int hicgat_adam_step_table(float *param, const float *grad, float *ex
                                       int64_t table_len, int64_t *step_counter, hicgat_stream_t stream) {
   return hicgat_adam_step_table_ex(param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, table, table_len,
                                    step_counter, 0, stream);
+}
+
+extern "C" int hicgat_step_begin(float *grad, int64_t n, int64_t *step_counter, hicgat_stream_t stream) {
+  if (n < 0 || (n > 0 && !grad)) return HICGAT_EINVAL;
+  if (grad && (reinterpret_cast<uintptr_t>(grad) & 15)) return HICGAT_EINVAL;
+  if (n == 0 && !step_counter) return HICGAT_OK;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, 1024));
+  hipLaunchKernelGGL(step_begin_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, grad, n, step_counter);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
 }

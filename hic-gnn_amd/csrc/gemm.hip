@@ -323,10 +323,6 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
-#ifndef HICGAT_TALL_LG0_ROWS
-#define HICGAT_TALL_LG0_ROWS 1024   // grouped column sums: jobs taller than this use one lane per row group
-#endif
-constexpr int64_t TALL_LG0_ROWS = HICGAT_TALL_LG0_ROWS;
 #ifndef HICGAT_GROUP_DB
 #define HICGAT_GROUP_DB 0   // 1: double-buffered LDS in the grouped weight-gradient tiles (A/B builds)
 #endif
@@ -397,32 +393,26 @@ __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
     const bool vec = J.vec;
     const float *p = J.src + c;
     const float *w = J.wt;
-    int64_t r = r0;
-    for (; r + 8 <= r1; r += 8) {
+    // 8 rows per round, every load of a round issued before its adds (a short job's 3-4 rows --
+    // the split-K slabs -- are one round trip, not one per row); rows added in order
+    for (int64_t r = r0; r < r1; r += 8) {
       float4 v[8];
       float wv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        v[u] = ld4(p + (r + u) * J.ld, vec, c, J.cols);
-        wv[u] = w ? w[(r + u) * J.ldw] : 1.f;
+        const bool in = r + u < r1;
+        v[u] = in ? ld4(p + (r + u) * J.ld, vec, c, J.cols) : make_float4(0.f, 0.f, 0.f, 0.f);
+        wv[u] = (w && in) ? w[(r + u) * J.ldw] : 1.f;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
+        if (r + u >= r1) break;
         if (w) {
           s.x = fmaf(wv[u], v[u].x, s.x); s.y = fmaf(wv[u], v[u].y, s.y);
           s.z = fmaf(wv[u], v[u].z, s.z); s.w = fmaf(wv[u], v[u].w, s.w);
         } else {
           s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
         }
-      }
-    }
-    for (; r < r1; ++r) {
-      const float4 v = ld4(p + r * J.ld, vec, c, J.cols);
-      if (w) {
-        const float wr = w[r * J.ldw];
-        s.x = fmaf(wr, v.x, s.x); s.y = fmaf(wr, v.y, s.y); s.z = fmaf(wr, v.z, s.z); s.w = fmaf(wr, v.w, s.w);
-      } else {
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
     }
   }
@@ -620,9 +610,9 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     J.cols = cols;
     J.accumulate = acc;
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
-    // lanes per row group: short chains per lane for tall jobs (a rank's weighted sums over its 2 700
-    // rows: 11 rows per lane at lg 0 instead of 42 at lg 2, two rounds of loads instead of six)
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : rows <= TALL_LG0_ROWS ? 2 : 0;
+    // lanes per row group (one lane per group for the tallest jobs, uncoalesced, measured slower:
+    // P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : 2;
     J.blk0 = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
     blk += (int)((cols + per - 1) / per);

@@ -29,25 +29,43 @@ namespace hicgat {
 constexpr int XS = 516;         // LDS row stride (floats) of the 512-wide buffers
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// The compiler's scheduler sinks the ring's weight loads next to the MFMAs that use them (one group
+// in flight: every L2 latency exposed); a scheduling barrier after each group's loads keeps them R
+// groups ahead (HICGAT_TAIL_SCHED_PIN=0: the compiler's placement, A/B builds): P = 8 rank step
+// 0.426-0.427 vs 0.431-0.432 ms, synth-2000 0.597 vs 0.604 ms; R = 8: 0.442 (profiles/r04n_sim_ab.txt)
+#ifndef HICGAT_TAIL_SCHED_PIN
+#define HICGAT_TAIL_SCHED_PIN 1
+#endif
+#if HICGAT_TAIL_SCHED_PIN
+#define HICGAT_TAIL_SCHED() __builtin_amdgcn_sched_barrier(0)
+#else
+#define HICGAT_TAIL_SCHED() ((void)0)
+#endif
+
+#ifndef HICGAT_TAIL_RING
+#define HICGAT_TAIL_RING 4   // weight groups in flight per wave (the prefetch ring's depth)
+#endif
+
 // acc[h][t] (h < RB/16 row halves, t < NT) += A[RB x K] (LDS, row stride lda) x B^T, B = the weight
-// rows n0 + 16t + (l & 15) (K columns).  The weights of group g + 4 are loaded right after group g's
-// MFMAs, so three groups of MFMAs cover every load (a ring of 4 float4 sets).
+// rows n0 + 16t + (l & 15) (K columns).  The weights of group g + R are loaded right after group g's
+// MFMAs, so R - 1 groups of MFMAs cover every load (a ring of R float4 sets, R = HICGAT_TAIL_RING).
 template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
                                           f32x4 (&acc)[RB / 16][NT], int lane) {
-  constexpr int G = K / 16, H = RB / 16;
-  static_assert(G % 4 == 0, "K: a multiple of 64");
+  constexpr int G = K / 16, H = RB / 16, R = G < HICGAT_TAIL_RING ? G : HICGAT_TAIL_RING;
+  static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
   const float *arow = As + li * lda + kq;
-  float4 b[4][NT];
+  float4 b[R][NT];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < R; ++q)
 #pragma unroll
     for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * q);
-  for (int g0 = 0; g0 < G; g0 += 4) {
+  HICGAT_TAIL_SCHED();   // the ring's loads stay issued here, ahead of their MFMAs
+  for (int g0 = 0; g0 < G; g0 += R) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < R; ++q) {
       const int g = g0 + q;
       float4 a[H];
 #pragma unroll
@@ -61,10 +79,11 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
           acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t].z, acc[h][t], 0, 0, 0);
           acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t].w, acc[h][t], 0, 0, 0);
         }
-      if (g + 4 < G) {
+      if (g + R < G) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + 4));
+        for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + R));
       }
+      HICGAT_TAIL_SCHED();
     }
   }
 }
@@ -141,8 +160,20 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
 // = rows 256h .. of lin_l's weight Wh [512][512]), written as Y0 (pre-activation) and O = relu(Y0)
 // (the tail's input, kept for the backward's weight gradients) -- the per-head GEMM launches and
 // their slab sum leave the step.  Waves 0-3 take head 0's 256 columns, 4-7 head 1's.
+// waves per SIMD pinned to one workgroup's (NW / 4): a shard's grid has at most one workgroup per
+// CU, and without the pin the compiler schedules for the occupancy the LDS would admit (two
+// workgroups, 64 VGPRs at NW = 16) and sinks every weight load next to its MFMAs -- the prefetch ring
+// collapses to one group in flight (HICGAT_TAIL_PIN=0 keeps that form for A/B)
+#ifndef HICGAT_TAIL_PIN
+#define HICGAT_TAIL_PIN 1
+#endif
+#if HICGAT_TAIL_PIN
+#define HICGAT_TAIL_WPE __attribute__((amdgpu_waves_per_eu(HICGAT_TAIL_WAVES / 4, HICGAT_TAIL_WAVES / 4)))
+#else
+#define HICGAT_TAIL_WPE
+#endif
 template <int RB, int NW, bool HEADS = false>
-__global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
+__global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
     const float *__restrict__ b2c, const float *__restrict__ g2, const float *__restrict__ be2,
@@ -256,21 +287,22 @@ __global__ __launch_bounds__(64 * NW) void tail_fwd_kernel(
 template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int lda, const float *__restrict__ W, int ldw,
                                             int n0, f32x4 (&acc)[RB / 16][NT], int lane) {
-  constexpr int G = K / 16, H = RB / 16;
-  static_assert(G % 4 == 0, "K: a multiple of 64");
+  constexpr int G = K / 16, H = RB / 16, R = G < HICGAT_TAIL_RING ? G : HICGAT_TAIL_RING;
+  static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wcol = W + (size_t)kq * ldw + n0 + li;
   const float *arow = As + li * lda + kq;
-  float b[4][NT][4];
+  float b[R][NT][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < R; ++q)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * q + j) * ldw + 16 * t];
-  for (int g0 = 0; g0 < G; g0 += 4) {
+  HICGAT_TAIL_SCHED();
+  for (int g0 = 0; g0 < G; g0 += R) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < R; ++q) {
       const int g = g0 + q;
       float4 a[H];
 #pragma unroll
@@ -284,12 +316,13 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
           acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t][2], acc[h][t], 0, 0, 0);
           acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t][3], acc[h][t], 0, 0, 0);
         }
-      if (g + 4 < G) {
+      if (g + R < G) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * (g + 4) + j) * ldw + 16 * t];
+          for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * (g + R) + j) * ldw + 16 * t];
       }
+      HICGAT_TAIL_SCHED();
     }
   }
 }
@@ -316,13 +349,15 @@ __device__ __forceinline__ void put_tiles(const f32x4 (&acc)[RB / 16][NT], int n
 // LayerNorm + ReLU (+ residual) backward of rows wv, wv + 4, ... (ln_relu_res_bwd_kernel's
 // arithmetic): dz from LDS (Dz, stride ldd), y / stats from global; dy (and dres = dz beside it when
 // RES) into LDS (Gs, stride lds: [dy | dres]) and the global dY rows ([M][W or 2W]); the wave's
-// dgamma / dbeta partials into its slot of part ([slots][2][W], hicgat_ln_relu_res_bwd_params).
+// dgamma / dbeta partials, summed over the workgroup's waves, into row ``slot`` of part ([slots][2][W],
+// hicgat_ln_relu_res_bwd_params).
 template <int RB, int W, bool RES, int NW = 4>
 __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ldd, const float *__restrict__ y,
                                             int64_t ldy, const float2 *__restrict__ stats,
                                             const float *__restrict__ gamma, const float *__restrict__ beta,
                                             float *__restrict__ Gs, int lds, float *__restrict__ dY,
-                                            float *__restrict__ part, int slot, int m0, int M, int wv, int lane) {
+                                            float *__restrict__ part, int slot, float *__restrict__ red, int m0,
+                                            int M, int wv, int lane) {
   constexpr int V = W / 64, LDY = RES ? 2 * W : W;
   float g_[V], b_[V], pg[V], pb[V];
 #pragma unroll
@@ -362,11 +397,21 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
       if (live) dY[(size_t)row * LDY + q * 64 + lane] = v;
     }
   }
+  // the NW waves' partials added in wave order through LDS (red: [NW][2W] floats), one [2W] row per
+  // workgroup (slot = blockIdx.x): at 16 waves a wave holds one row, and per-wave rows would double the
+  // grouped column sum's input
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    part[((size_t)slot * 2 + 0) * W + q * 64 + lane] = pg[q];
-    part[((size_t)slot * 2 + 1) * W + q * 64 + lane] = pb[q];
+    red[(wv * 2 + 0) * W + q * 64 + lane] = pg[q];
+    red[(wv * 2 + 1) * W + q * 64 + lane] = pb[q];
   }
+  __syncthreads();
+  for (int c = wv * 64 + lane; c < 2 * W; c += NW * 64) {
+    float v = red[c];
+    for (int w = 1; w < NW; ++w) v += red[w * 2 * W + c];
+    part[(size_t)slot * 2 * W + c] = v;
+  }
+  __syncthreads();   // red is reused by the next call
 }
 
 
@@ -376,7 +421,7 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
 // xagg_rows_bwd does), then dxa^h = dout^h W_h ([RB x 256] [256 x 512], waves 0-3 head 0, 4-7 head 1)
 // into dxa [M][1024].
 template <int RB, int NW, bool HEADS = false>
-__global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
+__global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
     const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
     const float2 *__restrict__ st3, const float *__restrict__ W4, const float *__restrict__ W3,
@@ -390,8 +435,9 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // dz3, dz2, dz1 rows
   float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
+  float *Rs = lds_tail + 2 * RB * XS;   // [NW][2W] LayerNorm parameter partials (W <= 256)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int slot = blockIdx.x * NW + wv;
+  const int slot = blockIdx.x;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16;
   // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
@@ -405,7 +451,7 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     As[r * XS + c] = s;
   }
   __syncthreads();
-  ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, m0, M, wv, lane);
+  ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 16 ND wv ..
   constexpr int WD = NW < 8 ? NW : 8, ND = 8 / WD, NT2 = 16 / NW, NT1 = 32 / NW;   // dense2: WD waves
@@ -419,7 +465,7 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     put_tiles<RB, ND>(acc, 16 * ND * wv, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
-  ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, m0, M, wv, lane);
+  ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // block 2 backward: dz1 = [dy2 | dres2] [W_1; W_1al] ([RB x 256] [256 x 256]), wave wv: columns 16 NT2 wv ..
   {
@@ -432,7 +478,7 @@ __global__ __launch_bounds__(64 * NW) void tail_bwd_kernel(
     put_tiles<RB, NT2>(acc, 16 * NT2 * wv, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
-  ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, m0, M, wv, lane);
+  ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // block 1 backward: dx = [dy1 | dres1] [W_a; W_al] ([RB x 512] [512 x 512]), wave wv: columns 16 NT1 wv ..
   {
@@ -576,7 +622,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
 extern "C" int hicgat_tail_bwd_waves(void) { return HICGAT_TAIL_WAVES; }
 
 extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
-  return M <= 0 ? 16 : (size_t)HICGAT_TAIL_WAVES * ((M + 15) / 16) * 2 * W * sizeof(float);
+  return M <= 0 ? 16 : (size_t)((M + 15) / 16) * 2 * W * sizeof(float);   // one [2W] row per workgroup
 }
 
 namespace {
@@ -594,6 +640,8 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
                     size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
                     const TailHeadsBwd &hh, hipStream_t stream) {
   constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
+  // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
+  constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
   if (M < 0) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
   const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
@@ -609,10 +657,10 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
     return HICGAT_EINVAL;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
+                                               kBwdLds) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
   hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
-                     (size_t)2 * RB * XS * sizeof(float), stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
+                     (size_t)kBwdLds, stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
                      Y2, reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c,
                      W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1),
                      static_cast<float *>(ws2), static_cast<float *>(ws3), hh.act, hh.Y0, hh.Wh, hh.bh, hh.dout,

@@ -563,8 +563,8 @@ class HipKernels:
         return int(self.lib.hicgat_tail_bwd_waves())
 
     def tail_partial_rows(self, M):
-        """Rows of LayerNorm partials hicgat_tail_bwd_fused leaves per workspace: one per wave."""
-        return int(self.lib.hicgat_tail_bwd_waves()) * (-(-M // 16))
+        """Rows of LayerNorm partials hicgat_tail_bwd_fused leaves per workspace: one per workgroup."""
+        return -(-M // 16)
 
     def ln_workspace(self, W, device):
         return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)
@@ -580,6 +580,11 @@ class HipKernels:
                                                           float(eps), P(table), table.shape[0], P(step_ctr),
                                                           int(bool(counted)), _lib.stream(flat.device)),
                        "hicgat_adam_step_table_ex")
+
+    def step_begin(self, grad, step_ctr=None):
+        """zero_grad of the flat gradient buffer + (step_ctr) the device step count's advance, one launch."""
+        _lib.check(self.lib.hicgat_step_begin(P(grad), grad.numel(), P(step_ctr), _lib.stream(grad.device)),
+                   "hicgat_step_begin")
 
     def adam(self, flat, grad, m, v, n, lr, b1, b2, eps, step):
         with _timed("adam"):

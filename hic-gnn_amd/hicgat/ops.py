@@ -619,7 +619,7 @@ def _dual_param_grads(K, W1, b1, W2, b2, dY, x):
 
 
 def _ln_param_grads(K, gamma, beta, ws, rows):
-    """A LayerNorm's dgamma / dbeta = the column sums of the first ``rows`` per-wave partial rows
+    """A LayerNorm's dgamma / dbeta = the column sums of the first ``rows`` per-workgroup partial rows
     [dgamma | dbeta] that hicgat_tail_bwd_fused left in ``ws``: into the (adjacent) sinks as queued
     side work (ONE colsum launch over the live rows, its size as the lane-balancing work) or new
     tensors (returned)."""
@@ -705,7 +705,7 @@ class _FusedTailFn(torch.autograd.Function):
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
                 g2.contiguous(), be2.contiguous(), heads=ctx.heads)
-            rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per wave
+            rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per workgroup
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)
             dW2, db2 = _wb_grad_to(K, W2, b2, dy3, z2)

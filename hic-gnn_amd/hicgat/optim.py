@@ -53,8 +53,16 @@ class FlatAdam:
         return self
 
     def zero_grad(self, set_to_none=False):
-        """Zero the flat gradient buffer (``set_to_none`` is ignored: the ``.grad`` views stay)."""
-        self.grad.zero_()
+        """Zero the flat gradient buffer (``set_to_none`` is ignored: the ``.grad`` views stay).  With
+        the device step count on (and a GPU buffer) the zeroing launch also advances the count, and
+        the next ``step()`` reads it without its own increment launch."""
+        if getattr(self, "step_ctr", None) is not None and self.grad.is_cuda:
+            kern = self.kern if self.kern is not None else kernels.default()
+            # a second zero_grad before the step only zeroes (the count advances once per step)
+            kern.step_begin(self.grad, None if getattr(self, "_counted", False) else self.step_ctr)
+            self._counted = True
+        else:
+            self.grad.zero_()
         self._reattach()
 
     def _reattach(self):
@@ -76,6 +84,8 @@ class FlatAdam:
         (``kernels.xagg_logits(step_ctr=...)``), so Adam reads it without an increment launch."""
         self._reattach()
         self.step_count += 1
+        counted = counted or getattr(self, "_counted", False)
+        self._counted = False
         kern = self.kern if self.kern is not None else kernels.default()
         if getattr(self, "step_ctr", None) is not None:
             kern.adam_table(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.betas[0],

@@ -467,9 +467,10 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
  * input), dY1 [M][512] = [dy | dres] of block 1, dY2 [M][256] of block 2, dy3 [M][64] (dense2's output
  * gradient) -- the inputs of the weight-gradient GEMMs -- and each LayerNorm's dgamma/dbeta partials
  * into ws1 / ws2 / ws3: rows
- * [0, hicgat_tail_bwd_waves() ceil(M/16)) of a [.][2W] = [dgamma | dbeta] matrix, one per wave
- * (their column sums, e.g. hicgat_colsum, are dgamma / dbeta); each workspace at least
- * hicgat_tail_bwd_workspace_bytes(M, W) for W = 256 / 128 / 64. */
+ * [0, ceil(M/16)) of a [.][2W] = [dgamma | dbeta] matrix, one per 16-row workgroup (its waves'
+ * partials added in wave order; the rows' column sums, e.g. hicgat_colsum, are dgamma / dbeta); each
+ * workspace at least hicgat_tail_bwd_workspace_bytes(M, W) for W = 256 / 128 / 64.
+ * hicgat_tail_bwd_waves(): the waves per workgroup of both tail kernels. */
 int hicgat_tail_bwd_waves(void);
 size_t hicgat_tail_bwd_workspace_bytes(int M, int W);
 int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
@@ -566,6 +567,9 @@ int hicgat_adam_step_table(float *param, const float *grad, float *exp_avg, floa
 int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                               int64_t n, double beta1, double beta2, double eps, const float *table,
                               int64_t table_len, int64_t *step_counter, int counted, hicgat_stream_t stream);
+/* A step's first launch: grad[0, n) = 0 (zero_grad, HiC-GNN_main.py:124) and, with step_counter
+ * (NULL: none), *step_counter += 1 (the step's Adam then uses counted = 1).  grad 16-B aligned. */
+int hicgat_step_begin(float *grad, int64_t n, int64_t *step_counter, hicgat_stream_t stream);
 #ifdef __cplusplus
 }
 #endif
