@@ -323,6 +323,20 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
+#ifndef HICGAT_WEIGHTED_LG1_ROWS
+#define HICGAT_WEIGHTED_LG1_ROWS 1024   // weighted column-sum jobs taller than this: 2 lanes per row group
+#endif
+constexpr int64_t WEIGHTED_LG1_ROWS = HICGAT_WEIGHTED_LG1_ROWS;
+// The job a block belongs to: the number of later job starts <= b, every start read at a constant
+// offset of the kernel argument block (one batch of scalar loads instead of one dependent load per
+// job scanned; measured even at P = 8, profiles/r04p_sim_ab.txt)
+template <int KMAX>
+__device__ __forceinline__ int find_job(const int (&start)[KMAX], int n, int b) {
+  int q = 0;
+#pragma unroll
+  for (int k = 1; k < KMAX; ++k) q += (k < n && b >= start[k]) ? 1 : 0;
+  return q;
+}
 #ifndef HICGAT_GROUP_DB
 #define HICGAT_GROUP_DB 0   // 1: double-buffered LDS in the grouped weight-gradient tiles (A/B builds)
 #endif
@@ -336,12 +350,12 @@ struct WJob {
   int M, N, K, kchunk, tm, tn, wg0, accumulate, vec;
 };
 struct WJobs {
+  int start[kMaxWJobs];   // job k's first workgroup (= j[k].wg0), contiguous for find_job
   WJob j[kMaxWJobs];
   int n;
 };
 __global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(const WJobs jobs) {
-  int q = 0;
-  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].wg0) ++q;   // block-uniform scalar scan
+  const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const WJob &J = jobs.j[q];
   const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
   const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
@@ -369,6 +383,7 @@ struct CJob {
   int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (6: 4 groups ... 2: 64 groups)
 };
 struct CJobs {
+  int start[kMaxCJobs];   // job k's first block (= j[k].blk0)
   CJob j[kMaxCJobs];
   int n;
 };
@@ -378,8 +393,7 @@ __device__ __forceinline__ float4 ld4(const float *p, bool vec, int64_t c, int64
 }
 __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
   __shared__ float4 red[256];
-  int q = 0;
-  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].blk0) ++q;
+  const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const CJob &J = jobs.j[q];
   // a job of many rows (LayerNorm partial rows, g_src's partial rows) takes 16 or 64 row groups of
   // 16 / 4 lanes per block, a short one (split-K slabs) 4 groups of 64 lanes: the in-order chain of
@@ -464,13 +478,14 @@ struct RJob {
   int M, N, K, kchunk, tm, tn, wg0, blk0;
 };
 struct RJobs {
+  int start[kMaxRJobs];   // job k's first GEMM workgroup (= j[k].wg0)
+  int rstart[kMaxRJobs];  // job k's first reduce block (= j[k].blk0)
   RJob j[kMaxRJobs];
   int n, splits;
 };
 template <bool B_KM>
 __global__ __launch_bounds__(256, HICGAT_GEMM_OCC64) void gemm_rows_grouped_kernel(const RJobs jobs) {
-  int q = 0;
-  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].wg0) ++q;
+  const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const RJob &J = jobs.j[q];
   const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
   const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
@@ -481,8 +496,7 @@ __global__ __launch_bounds__(256, HICGAT_GEMM_OCC64) void gemm_rows_grouped_kern
       direct ? nullptr : J.slab, (int64_t)J.M * J.N, 0, nullptr, bx, by, bz, direct ? J.cr : nullptr, J.ldr);
 }
 __global__ __launch_bounds__(256) void rows_reduce_kernel(const RJobs jobs) {
-  int q = 0;
-  while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.j[q + 1].blk0) ++q;
+  const int q = find_job(jobs.rstart, jobs.n, (int)blockIdx.x);
   const RJob &J = jobs.j[q];
   const int64_t e = ((int64_t)(blockIdx.x - J.blk0) * 256 + threadIdx.x) * 4;   // element (row-major M x N)
   const int64_t MN = (int64_t)J.M * J.N;
@@ -554,8 +568,10 @@ extern "C" int hicgat_gemm_rows_grouped(const hicgat_gemm_job *jobs, int n, int 
     J.slab = slab;
     slab += (size_t)splits * a.M * a.N;
     J.wg0 = wg;
+    rj.start[rj.n - 1] = wg;
     wg += J.tm * J.tn * splits;
     J.blk0 = blk;
+    rj.rstart[rj.n - 1] = blk;
     blk += (int)(((int64_t)a.M * a.N / 4 + 255) / 256);
   }
   hipStream_t s = (hipStream_t)stream;
@@ -612,8 +628,9 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
     // lanes per row group (one lane per group for the tallest jobs, uncoalesced, measured slower:
     // P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : 2;
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? 1 : 2;
     J.blk0 = blk;
+    cj.start[cj.n - 1] = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
     blk += (int)((cols + per - 1) / per);
     return HICGAT_OK;
@@ -649,6 +666,7 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
       used += need;
     }
     J.wg0 = wg;
+    wj.start[wj.n - 1] = wg;
     wg += J.tm * J.tn * sp;
     if (sp > 1) {
       const int64_t stride = (int64_t)a.M * a.N + a.M;
