@@ -327,6 +327,9 @@ constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
 #define HICGAT_WEIGHTED_LG1_ROWS 1024   // weighted column-sum jobs taller than this: 2 lanes per row group
 #endif
 constexpr int64_t WEIGHTED_LG1_ROWS = HICGAT_WEIGHTED_LG1_ROWS;
+#ifndef HICGAT_WEIGHTED_LG
+#define HICGAT_WEIGHTED_LG 1   // log2 lanes per row group of those jobs (2: 0.425-0.427 ms, 1: 0.422-0.423 at P = 8)
+#endif
 // The job a block belongs to: the number of later job starts <= b, every start read at a constant
 // offset of the kernel argument block (one batch of scalar loads instead of one dependent load per
 // job scanned; measured even at P = 8, profiles/r04p_sim_ab.txt)
@@ -628,7 +631,7 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
     // lanes per row group (one lane per group for the tallest jobs, uncoalesced, measured slower:
     // P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? 1 : 2;
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? HICGAT_WEIGHTED_LG : 2;
     J.blk0 = blk;
     cj.start[cj.n - 1] = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
