@@ -485,36 +485,27 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
   float sx = 0.f, sy = 0.f, sz = 0.f;
   if (gi < N) {
     const int R = gi / BT, lr = gi % BT;
-    // 8 tiles J per round, every load of a round issued before its adds (J in order)
-    for (int J0 = grp; J0 < nb; J0 += 8 * kRedGroups) {
-      float4 a[8], b[8], c[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int J = J0 + u * kRedGroups;
-        a[u] = b[u] = c[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (J >= nb) continue;
-        int64_t trow, tcol;
-        if (mode == MODE_SYM) {
-          trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
-          tcol = J <= R ? tri_start(J, nb) + (R - J) : -1;
-        } else {
-          trow = (int64_t)R * nb + J;
-          tcol = (int64_t)J * nb + R;
-        }
-        // slab of tile t: [row partials | ncol column-partial rows], (1 + ncol) x BT float4
-        const size_t st = (size_t)(1 + ncol) * BT;
-        if (trow >= t0 && trow < t1) a[u] = part[(size_t)trow * st + lr];
-        if (tcol >= t0 && tcol < t1) {
-          b[u] = part[(size_t)tcol * st + BT + lr];
-          if (ncol == 2) c[u] = part[(size_t)tcol * st + 2 * BT + lr];
-        }
+#pragma unroll 2
+    for (int J = grp; J < nb; J += kRedGroups) {
+      int64_t trow, tcol;
+      if (mode == MODE_SYM) {
+        trow = J >= R ? tri_start(R, nb) + (J - R) : -1;
+        tcol = J <= R ? tri_start(J, nb) + (R - J) : -1;
+      } else {
+        trow = (int64_t)R * nb + J;
+        tcol = (int64_t)J * nb + R;
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        sx += a[u].x; sy += a[u].y; sz += a[u].z;
-        sx += b[u].x; sy += b[u].y; sz += b[u].z;
-        sx += c[u].x; sy += c[u].y; sz += c[u].z;
+      // slab of tile t: [row partials | ncol column-partial rows], (1 + ncol) x BT float4
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+      const size_t st = (size_t)(1 + ncol) * BT;
+      if (trow >= t0 && trow < t1) a = part[(size_t)trow * st + lr];
+      if (tcol >= t0 && tcol < t1) {
+        b = part[(size_t)tcol * st + BT + lr];
+        if (ncol == 2) c = part[(size_t)tcol * st + 2 * BT + lr];
       }
+      sx += a.x; sy += a.y; sz += a.z;
+      sx += b.x; sy += b.y; sz += b.z;
+      sx += c.x; sy += c.y; sz += c.z;
     }
   }
   red[grp][lr64] = make_float4(sx, sy, sz, 0.f);
