@@ -535,6 +535,42 @@ def test_adam_bit_exact_vs_torch_cpu_restatement():
         assert np.array_equal(params[0].detach().cpu().numpy(), p), step
 
 
+@pytest.mark.parametrize("zero_calls", [1, 2])
+def test_adam_device_step_count_paths_bit_exact(zero_calls):
+    """The graph-replayable Adam (device step count, host-tabulated constants) on the two paths that
+    advance the count here -- zero_grad's one-launch zero + count (hicgat_step_begin; a second
+    zero_grad in the same step must not count twice) and Adam's own increment -- against the
+    host-constant Adam and the CPU restatement, bit for bit.  (The xagg step's count in its first
+    launch is covered by the sharded graph-replay-equals-eager tests in test_gpu_dist.py.)"""
+    import hicgat
+    from oracle import loop as ol
+    rng = np.random.default_rng(1)
+    n = 4099
+    p0 = rng.standard_normal(n).astype(np.float32)
+    opts = []
+    for mode in ("host", "zero_grad", "adam_increment"):
+        params = [torch.nn.Parameter(torch.tensor(p0, device=DEV))]
+        opt = hicgat.FlatAdam(params, lr=1e-3)
+        if mode != "host":
+            opt.enable_device_step()
+        opts.append((mode, opt, params))
+    p, m, v = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for step in range(1, 6):
+        g = rng.standard_normal(n).astype(np.float32)
+        for mode, opt, _ in opts:
+            if mode == "zero_grad":
+                for _ in range(zero_calls):
+                    opt.zero_grad()
+                assert float(opt.grad.abs().max()) == 0.0
+            opt.grad[:n].copy_(torch.tensor(g))
+            opt.step()
+            if mode != "host":
+                assert int(opt.step_ctr.item()) == step, (mode, step)
+        p, m, v = ol.adam_reference_step(p, g, m, v, step)
+        for mode, _, params in opts:
+            assert np.array_equal(params[0].detach().cpu().numpy(), p), (mode, step)
+
+
 # ---------------------------------------------------------------- models vs reference fixtures
 def _oracle_exact(name, fx, g):
     """The oracle model with the fixture's weights, distances by the exact formula."""

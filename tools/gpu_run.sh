@@ -16,6 +16,7 @@
 #   pmc_traffic  two PMC passes (FETCH_SIZE, WRITE_SIZE) of an eager bench -> <tag>_pmc_traffic.json
 #   pmc_mfma     one PMC pass (MFMA busy cycles, F32 MFMA MOPs, GRBM_GUI_ACTIVE) -> <tag>_pmc_mfma.json
 #   pmc_mfma2000 the same on synth-2000 (dense-tile MFMA aggregation)
+#   pmc_mfma_sim the same for rank 0 of the simulated 8-rank xagg step
 #   simrank      per-rank compute of the sharded step at P = 2, 4, 8 (bench.py --simulate-world; _ag: allgather
 #                form, _xa: aggregate-first form, _au: bench.py's default "auto")
 #   kb:<jobs>:<libs> tools/kbench.py A/B of the named kernel jobs over the listed library builds
@@ -90,6 +91,14 @@ for S in "$@"; do
         python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/${T}_${S}.log 2>&1 || exit $?
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json $W \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --eager" \
+        "$COMMIT" || exit $? ;;
+    pmc_mfma_sim)
+      # the MFMA counters of rank 0's share of the simulated 8-rank xagg step (graph replay, 3 steps)
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
+        -d gpurun_out/${T}_${S} -o run --output-format csv -- \
+        python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 3 --warmup 2 > gpurun_out/${T}_${S}.log 2>&1 || exit $?
+      python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json sim-P8-rank0 \
+        "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 3 --warmup 2" \
         "$COMMIT" || exit $? ;;
     simrank|simrank_ag|simrank_xa|simrank_au)
       M=slab; [ "$S" = simrank_ag ] && M=allgather; [ "$S" = simrank_xa ] && M=xagg; [ "$S" = simrank_au ] && M=auto
