@@ -127,34 +127,22 @@ __device__ __forceinline__ void agg_bwd_src_row(
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
     float *__restrict__ dh, float *__restrict__ da_src);
 
-// Persistent when the grid is smaller than the row-block count (HICGAT_SRC_WGS per CU): each
-// workgroup walks row blocks b, b + gridDim.x, ... (the same XCD for all of them), so the CUs keep
-// free slots for the parameter-gradient GEMMs the side stream runs beside this pass.
+// One workgroup per 4 rows (a persistent grid of 2-3 workgroups per CU, leaving slots to the side
+// stream's GEMMs, measured the same step or slower and was removed).
 // REMAP: the XCD-aware block order (each XCD a contiguous row range: the rows of a banded Hi-C
 // neighbourhood share that XCD's L2).  Off (plain round-robin over the XCDs) for the multi-GPU "slab"
 // pass, whose heavy rows -- the rank's own diagonal block -- are contiguous: under the remap they
 // would all land on one XCD.
-template <bool SPLIT = false, bool PERSIST = false, bool REMAP = true>
+template <bool SPLIT = false, bool REMAP = true>
 __global__ __launch_bounds__(256) void agg_bwd_src_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout, int64_t ldq,
     const float *__restrict__ att_s, const float *__restrict__ att_d, float ns,
     float *__restrict__ dh, float *__restrict__ da_src) {
-  const int nblk = (row_end - row_begin + 3) / 4;
-  if constexpr (!PERSIST) {
-    const int r = row_begin + (REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wave_in_block();
-    if (r < row_end)
-      agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh,
-                             da_src);
-  } else {
-    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-      const int r = row_begin + xcd_remap(b, nblk) * 4 + wave_in_block();
-      if (r < row_end)
-        agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh,
-                               da_src);
-    }
-  }
+  const int r = row_begin + (REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wave_in_block();
+  if (r < row_end)
+    agg_bwd_src_row<SPLIT>(r, rowptr, col, h, a_src, a_dst, row_stats, ldr, dout, ldq, att_s, att_d, ns, dh, da_src);
 }
 
 template <bool SPLIT>
@@ -375,7 +363,7 @@ __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict
 // Grid of the source pass: one workgroup per 4 rows.  (A persistent grid of 2-3 workgroups per CU,
 // leaving slots to the side stream's GEMMs, measured the same step or slower)
 #define HICGAT_SRC_LAUNCH(SPLIT_, rows_, ...)                                                              \
-  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_, false>), dim3(((rows_) + 3) / 4), dim3(256), 0,    \
+  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<SPLIT_>), dim3(((rows_) + 3) / 4), dim3(256), 0,           \
                      __VA_ARGS__)
 
 // The gather half of hicgat_gat_agg_bwd_src_tiled (gat_tiles.hip): the sparse remainder's shares.
@@ -450,7 +438,7 @@ extern "C" int hicgat_gat_agg_bwd_src_ex(const int32_t *rowptr, const int32_t *c
       !dh || !da_src)
     return HICGAT_EINVAL;
   const int rows = row_end - row_begin;
-  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<false, false, false>), dim3((rows + 3) / 4), dim3(256), 0,
+  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<false, false>), dim3((rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst, row_stats, ld_stats, dout,
                      ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();
