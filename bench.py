@@ -289,21 +289,6 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
-# Modeled collectives of the sharded step (bench.py --simulate-world).  NOT measured here (the pool's
-# GPU boxes have one GPU): assumptions, stated in the JSON line.  RCCL on one MI355X node: 7 xGMI
-# links per GPU (MI355X_MICROARCH.md / SURVEY 5: ~153 GB/s each); a collective costs a latency
-# term plus bytes over the bus bandwidth it sustains.
-RCCL_LAT_US = 12.0         # small-message latency of one RCCL collective inside a captured graph
-RCCL_BUS_GBS = 300.0       # sustained bus bandwidth of an all-reduce / all-gather over 8 ranks
-
-
-def _coll_us(kind, nbytes, P):
-    """Time of one collective over P ranks: all_gather moves (P-1)/P of the buffer into each rank,
-    all_reduce 2 (P-1)/P of it (ring / tree bus-bandwidth convention)."""
-    f = (P - 1) / P * (2.0 if kind == "all_reduce" else 1.0)
-    return RCCL_LAT_US + f * nbytes / (RCCL_BUS_GBS * 1e3)
-
-
 def simulate_world(args):
     """Per-rank compute of the P-rank sharded step on ONE GPU: each rank's share (its rows, edges,
     slab, tiles and support rows) with the collectives left out, graph-captured, timed like the
@@ -315,13 +300,16 @@ def simulate_world(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     wl = build_workload(args.workload, args.seed, dev)
-    rank_ms, rank_med, shards = [], [], []
+    rank_ms, rank_med, rank_ms_bare, shards = [], [], [], []
     truth = wl["truth"]
-    for r in (range(P) if args.sim_rank is None else [args.sim_rank]):
+    emulate = args.sim_comm == "emulate"
+    sim_coll = {}
+
+    def timed_rank(r, emu):
         torch.manual_seed(0)
         model = hicgat.MODELS[args.model]().to(dev)
         tr = hdist.ShardedTrainer(model, wl["x"], wl["adj"], truth, lr=1e-3, kind=args.loss,
-                                  mode=mode, comm=hdist.SimComm(P, r))
+                                  mode=mode, comm=hdist.SimComm(P, r, emulate=emu))
         step = tr.captured(warmup=max(1, args.warmup - 1) if args.warmup >= 2 else max(1, args.warmup))
         if args.warmup >= 2:
             step()       # the last warm-up step: the graph's first replay
@@ -333,29 +321,38 @@ def simulate_world(args):
             evs[k + 1].record()
         torch.cuda.synchronize()
         per = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+        if emu and not sim_coll:
+            # the emulated collectives of one eager step, timed on their streams
+            hdist.COMM_TIMERS = {}
+            tr.step()
+            torch.cuda.synchronize()
+            sim_coll.update(hdist.comm_report())
+            hdist.COMM_TIMERS = None
+        return per, tr, step, model
+
+    for r in (range(P) if args.sim_rank is None else [args.sim_rank]):
+        per, tr, step, model = timed_rank(r, emulate)
         rank_ms.append(float(np.mean(per)))
         rank_med.append(float(np.median(per)))
+        if emulate and not args.no_bare:
+            del step, tr, model
+            torch.cuda.empty_cache()
+            bare, tr, step, model = timed_rank(r, False)
+            rank_ms_bare.append(float(np.mean(bare)))
+        elif not emulate:
+            rank_ms_bare.append(rank_ms[-1])
         shards.append({"rows": tr.local_rows, "nnz": tr.local_nnz, "slab_nnz": getattr(tr, "slab_nnz", None),
                        "tiles": tr.t1 - tr.t0, "support_rows": (tr.s1 - tr.s0) if tr.sf is not None else None})
-        log(f"[sim] P={P} rank {r}: {rank_ms[-1]:.4f} ms/step (median {rank_med[-1]:.4f}) {shards[-1]}")
+        log(f"[sim] P={P} rank {r}: {rank_ms[-1]:.4f} ms/step (median {rank_med[-1]:.4f}; without collectives "
+            f"{rank_ms_bare[-1] if rank_ms_bare else float('nan'):.4f}) {shards[-1]}")
         del step, tr, model
         torch.cuda.empty_cache()
     n, D = wl["n"], D_FEAT
-    grad_bytes = 4 * 601475
-    R = max(s["rows"] for s in shards)
-    coll = {"coords_all_gather": _coll_us("all_gather", P * R * 3 * 4, P),
-            "loss_all_reduce": _coll_us("all_reduce", (12 + 3 * n) * 8, P),     # the fp64 [stats | dcoords] buffer
-            "grad_all_reduce_gat_bucket": _coll_us("all_reduce", 4 * (512 * 512 + 3 * 512), P)}
-    if mode == "xagg":
-        # nothing big runs after the flush in the xagg step: the tail's bucket (issued first, on the comm
-        # stream) and the GATConv's queue on the communicator one after the other.  In the slab form the
-        # tail's bucket runs beside lin_l's dW GEMM (replicated over all rows) and stays off the path
-        coll["grad_all_reduce_tail_bucket"] = _coll_us("all_reduce", grad_bytes - 4 * (512 * 512 + 3 * 512), P)
-    if mode == "allgather":
-        coll["h_all_gather"] = _coll_us("all_gather", P * R * D * 4, P)
-        coll["pack_all_gather"] = _coll_us("all_gather", P * R * (D + 8) * 4, P)
-    exposed_us = sum(coll.values())
-    model_ms = max(rank_ms) + exposed_us * 1e-3
+    coll = {k: hdist.coll_us(kind, nbytes, Pm) for k, (kind, nbytes, Pm) in hdist.MODELED.items()}
+    serial_ms = max(rank_ms_bare) + sum(coll.values()) * 1e-3 if rank_ms_bare else None
+    # emulated: rank_ms holds the collectives (their time, overlap and CU footprint) -- the model is the
+    # slowest rank; left out: the round-4 model, the slowest rank + every collective added serially
+    model_ms = max(rank_ms) if emulate else serial_ms
     result = {
         "metric": f"training steps/sec ({args.model}, fwd+loss+bwd+Adam) -- MODELED {P}-GPU step",
         "value": 1e3 / model_ms, "unit": "steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -363,12 +360,21 @@ def simulate_world(args):
         "dtype": "fp32", "data": "synthetic (power-law Hi-C contacts, 0.1*N(0,1) features, random-init weights seed 0)",
         "config": {"workload": args.workload, "n_nodes": n, "nnz_with_self_loops": wl["adj"].device_nnz,
                    "parallelism": f"dst-row shard x{P} ({mode}), SIMULATED one rank at a time on 1 GPU"},
-        "simulated": {"world": P, "mode": mode, "rank_ms": rank_ms, "rank_median_ms": rank_med,
-                      "shards": shards, "collectives_us": coll, "exposed_collectives_us": exposed_us,
-                      "model_ms_per_step": model_ms,
-                      "assumptions": {"rccl_latency_us": RCCL_LAT_US, "rccl_bus_GBps": RCCL_BUS_GBS,
-                                      "note": "rank_ms measured (graph replay of the rank's share, collectives "
-                                              "left out); collectives modeled, not measured (1-GPU box)"}},
+        "simulated": {"world": P, "mode": mode, "collectives": "emulated" if emulate else "left out",
+                      "rank_ms": rank_ms, "rank_median_ms": rank_med,
+                      "rank_ms_without_collectives": rank_ms_bare or None,
+                      "shards": shards, "collectives_us": coll, "collectives_detail": sim_coll,
+                      "serial_model_ms": serial_ms, "model_ms_per_step": model_ms,
+                      "assumptions": {"rccl_latency_us": hdist.RCCL_LAT_US, "rccl_bus_GBps": hdist.RCCL_BUS_GBS,
+                                      "emulated_collective_workgroups": hdist.SIM_COMM_WGS,
+                                      "emulated_collective_threads": hdist.SIM_COMM_THREADS,
+                                      "note": "rank_ms measured (graph replay of the rank's share); each collective "
+                                              "EMULATED on the stream it is issued on by a kernel holding "
+                                              "emulated_collective_workgroups workgroups resident for the modeled "
+                                              "time (latency + bytes / bus bandwidth, not measured: 1-GPU box), so "
+                                              "overlap with other streams and CU contention are in rank_ms; "
+                                              "serial_model_ms = slowest rank without collectives + all modeled "
+                                              "collectives added serially (the round-4 model)"}},
     }
     print(json.dumps(result), flush=True)
 
@@ -379,7 +385,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="synth-20000", choices=["synth-20000", "synth-2000"])
-    ap.add_argument("--loss", default="mse", choices=["mse", "combined"])
+    ap.add_argument("--loss", default="mse", choices=["mse", "combined", "contrastive"])
     ap.add_argument("--model", default="GATNetSelectiveResidualsUpdated",
                     choices=["GATNetSelectiveResidualsUpdated", "GATNetHeadsChanged3LayersLeakyReLUv2", "Net"],
                     help="the flagship (default), the v2 GAT model or the SAGE baseline Net (SURVEY 8(f) f1); "
@@ -392,6 +398,11 @@ def main():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="one GPU: time each rank's share of a P-rank sharded step, collectives left out")
     ap.add_argument("--sim-rank", type=int, default=None, help="--simulate-world: only this rank (profiling)")
+    ap.add_argument("--sim-comm", default="emulate", choices=["emulate", "none"],
+                    help="--simulate-world: emulate each collective on its stream (default) or leave them out and "
+                         "add them serially (the round-4 model)")
+    ap.add_argument("--no-bare", action="store_true",
+                    help="--simulate-world: skip the second timing of each rank without the collectives")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5)
@@ -444,8 +455,8 @@ def main():
         raise SystemExit("the sharded step covers the GAT models (Net is the single-GPU f1 baseline)")
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     graph_error = None
+    from hicgat import dist as hdist
     if world > 1 or args.selftest_cpu:
-        from hicgat import dist as hdist
         runner = hdist.ShardedTrainer(model, wl["x"], wl["adj"], wl["truth"], lr=1e-3, kind=args.loss, kern=kern,
                                       mode=args.dist_mode)
         wl["truth"] = None                      # each rank keeps only its band (runner.tband)
@@ -533,11 +544,31 @@ def main():
                         "headline value replays the steps back to back"}
     # per-kernel HIP events: an eager pass of the same length right after the timed region
     kernels.TIMERS = {} if timed_events else None
-    if timed_events:
+    sharded = world > 1 or args.selftest_cpu
+    if sharded:
+        hdist.COMM_TIMERS = {}      # and every collective of the same eager pass, on its stream
+    if timed_events or sharded:
         for k in range(args.steps):
             eager_step()
         sync()
     timers, kernels.TIMERS = kernels.TIMERS or {}, None
+    comm = None
+    if sharded:
+        meas = hdist.comm_report()
+        hdist.COMM_TIMERS = None
+        # the communicator's own rank count: an all-reduce of a one per rank
+        one = torch.ones(1, dtype=torch.float32, device=dev if dev.type == "cuda" else "cpu")
+        torch.distributed.all_reduce(one)
+        pg = torch.distributed.distributed_c10d._get_default_group()
+        comm = {"backend": torch.distributed.get_backend(), "world_size": torch.distributed.get_world_size(),
+                "process_group_size": pg.size(), "ranks_counted_by_all_reduce": int(round(float(one.item()))),
+                "measured_us": {k: {"calls": v["calls"], "avg_us": v["avg_us"], "min_us": v["min_us"],
+                                    "bytes": v["bytes"], "kind": v["kind"]} for k, v in meas.items()},
+                "modeled_us": {k: v["modeled_us"] for k, v in meas.items()},
+                "model_assumptions": {"rccl_latency_us": hdist.RCCL_LAT_US, "rccl_bus_GBps": hdist.RCCL_BUS_GBS},
+                "note": "eager pass of the same steps after the timed region: events around each collective on the "
+                        "stream it is issued on (gloo: host wall time); a collective's time includes waiting for the "
+                        "slowest rank to arrive"}
     elapsed = t1 - t0
     if world > 1 or args.selftest_cpu:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
@@ -550,7 +581,6 @@ def main():
         ms = [a.elapsed_time(b) for a, b in ev]
         kern_t[name] = dict(launches=len(ms), avg_ms=float(np.mean(ms)), total_ms=float(np.sum(ms)))
     n, nnz = wl["n"], wl["adj"].device_nnz
-    sharded = world > 1 or args.selftest_cpu
     n_loc = runner.local_rows if sharded else n
     nnz_loc = runner.local_nnz if sharded else nnz
     cands = [k for k in ("gat_agg_fwd", "gat_agg_bwd_dst", "gat_agg_bwd_rows", "gat_agg_bwd_src", "sage_agg",
@@ -631,6 +661,8 @@ def main():
         "gemm": gemm_block(args.workload, kern_t) if not args.selftest_cpu else None,
         "kernels": kern_t,
     }
+    if comm is not None:
+        result["collectives"] = comm
     if sharded:
         result["shard"] = {"mode": runner.mode, "rows_per_rank": [int(v) for v in runner.plan.counts],
                            "nnz_per_rank": [int(v) for v in runner.plan.nnz]}

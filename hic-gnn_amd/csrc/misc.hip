@@ -12,3 +12,33 @@ extern "C" const char *hicgat_strerror(int code) {
     default: return "unknown hicgat error";
   }
 }
+
+// ---- measurement infrastructure: an emulated collective (bench.py --simulate-world) --------------
+// One rank's share of the sharded step runs on one GPU with each RCCL collective replaced by this
+// kernel on the stream the collective would be issued on: `workgroups` workgroups of `threads`
+// threads that stay resident for `us` microseconds of wall time (the steady 100 MHz counter), so a
+// captured step shows the modeled collective's duration, its ordering against the kernels around
+// it (overlap on a side / comm stream) and the CU slots an RCCL kernel would hold (contention).
+// Every wave leaves once its own clock passes the deadline: the grid always drains.
+__global__ __launch_bounds__(1024) void sim_collective_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" int hicgat_sim_collective(float us, int workgroups, int threads, hicgat_stream_t stream) {
+  if (!(us >= 0.f) || us > 1e6f || workgroups < 1 || workgroups > 4096 || threads < 64 || threads > 1024 ||
+      threads % 64)
+    return HICGAT_EINVAL;
+  static int khz = 0;   // the steady counter's rate (kHz): 100 MHz on MI300-class parts
+  if (khz == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) !=
+                                                hipSuccess || v <= 0)
+      return HICGAT_ELAUNCH;
+    khz = v;
+  }
+  const long long ticks = (long long)((double)us * 1e-3 * (double)khz);
+  hipLaunchKernelGGL(sim_collective_kernel, dim3(workgroups), dim3(threads), 0, (hipStream_t)stream, ticks);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

@@ -1,7 +1,8 @@
 // All-pairs 3-D distance, MSE + Pearson moments and their gradient on gfx950 (a7, a8, a9).
 //
 // Reference: out = torch.cdist(c, c, p=2) (models.py:661) -> MSELoss()(out, truth)
-// (HiC-GNN_main.py:127) and scipy pearsonr of the triu pairs (HiC_GAT_generalize_directly.py:220).
+// (HiC-GNN_main.py:127), scipy pearsonr of the triu pairs (HiC_GAT_generalize_directly.py:220), and
+// the contrastive loss 0.1 * mean_{i<j} |T_ij - D_ij| (train_and_test_same_res_GAT_node2vec.py:107-134).
 // The reference materialises D [N, N] (and its grad) in HBM; the fused kernel here streams the
 // truth matrix once, only its upper-triangle 128x128 tiles, and never stores D.
 //
@@ -12,6 +13,7 @@
 // ty through LDS).  Partials go to a [tile][2][128] float4 slab and a second kernel adds, per row,
 // the slabs of every tile touching it in a fixed order: bitwise reproducible, no float atomics.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -23,6 +25,11 @@ constexpr int BT = 128;
 #define HICGAT_PD_UNROLL 2   // rows per iteration of the packed interior loop (LDS reads of the next row in flight)
 #endif
 enum { MODE_SYM = 0, MODE_FULL = 1 };
+// loss kinds (include/hicgat.h): the KIND template parameter below
+enum { KIND_MSE = HICGAT_LOSS_MSE, KIND_COMBINED = HICGAT_LOSS_COMBINED, KIND_CONTRASTIVE = HICGAT_LOSS_CONTRASTIVE };
+
+// d|r|/dr = sign(r) with sign(0) = 0 (torch.abs's backward, sgn), times inv = 1/d
+__device__ __forceinline__ float sgn_inv(float r, float inv) { return r == 0.f ? 0.f : copysignf(inv, r); }
 
 __host__ __device__ inline int pd_nb(int N) { return (N + BT - 1) / BT; }
 __host__ __device__ inline int64_t tri_start(int64_t I, int64_t nb) { return I * nb - I * (I - 1) / 2; }
@@ -94,12 +101,13 @@ struct TileAcc {
 // bounds, i < j on the diagonal, the diagonal moment); interior tiles take MASK = false and do
 // no per-pair selection at all.  d2 == 0 (coincident points) gives inv = 1e30, d = 0 and a finite
 // w times dx = dy = dz = 0, i.e. no gradient -- torch's _euclidean_dist_backward masks it too.
-template <int MODE, bool VEC, bool PEARSON, bool MASK, int K0, int K1, bool BG = false, bool RLDS = false>
+template <int MODE, bool VEC, int KIND, bool MASK, int K0, int K1, bool BG = false, bool RLDS = false>
 __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t ldt, int64_t row0, int64_t col0,
                                           int N, int I, int J, float bg,
                                           const float *tile, const float (*sc)[BT][3], int tx, int ty,
                                           const float *cx, const float *cy, const float *cz, const int *gj,
                                           float4 *__restrict__ prow, TileAcc &A, float4 *rowpart) {
+  constexpr bool PEARSON = KIND == KIND_COMBINED, ABSL = KIND == KIND_CONTRASTIVE;
 #pragma unroll 1
   for (int k = K0; k < K1; ++k) {
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
@@ -137,10 +145,11 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
         const float r = d - tt;
         if (MASK) {
           bool valid = gi < N && gj[q] < N;
-          if (!BG && valid && gi == gj[q]) A.dg = fmaf(tt, tt, A.dg);   // (D_ii - T_ii)^2 = T_ii^2
+          // (D_ii - T_ii)^2 = T_ii^2 (MSE over all N^2 entries; the contrastive loss is over i < j only)
+          if (!BG && !ABSL && valid && gi == gj[q]) A.dg = fmaf(tt, tt, A.dg);
           valid = valid && (I != J || gi < gj[q]);
           if (valid) {
-            A.L = fmaf(r, r, A.L);
+            A.L = ABSL ? A.L + fabsf(r) : fmaf(r, r, A.L);
             if (PEARSON) {
               A.sd += d;
               A.sdd = fmaf(d, d, A.sdd);
@@ -149,9 +158,9 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
               A.stt = fmaf(tt, tt, A.stt);
             }
           }
-          w = valid ? r * inv : 0.f;
+          w = valid ? (ABSL ? sgn_inv(r, inv) : r * inv) : 0.f;
         } else {
-          A.L = fmaf(r, r, A.L);
+          A.L = ABSL ? A.L + fabsf(r) : fmaf(r, r, A.L);
           if (PEARSON) {
             A.sd += d;
             A.sdd = fmaf(d, d, A.sdd);
@@ -159,7 +168,7 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
             A.st += tt;
             A.stt = fmaf(tt, tt, A.stt);
           }
-          w = r * inv;
+          w = ABSL ? sgn_inv(r, inv) : r * inv;
         }
       } else {
         w = tt * inv;
@@ -188,10 +197,11 @@ __device__ __forceinline__ void tile_rows(const float *__restrict__ T, int64_t l
 // v_pk_{add,mul,fma}_f32 (two pairs per instruction); v_rsq stays scalar.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-template <bool PEARSON, int K0, int K1, bool BG = false, bool RLDS = false>
+template <int KIND, int K0, int K1, bool BG = false, bool RLDS = false>
 __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const float (*sc)[BT][3], int tx, int ty,
                                              const float *cx, const float *cy, const float *cz,
                                              float4 *__restrict__ prow, TileAcc &A, float4 *rowpart) {
+  constexpr bool PEARSON = KIND == KIND_COMBINED, ABSL = KIND == KIND_CONTRASTIVE;
   f2 cx2[4], cy2[4], cz2[4], ax2[4], ay2[4], az2[4];
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
@@ -232,7 +242,8 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       const f2 inv = f2{__builtin_amdgcn_rsqf(d2.x), __builtin_amdgcn_rsqf(d2.y)};
       const f2 d = d2 * inv;
       const f2 r = d - tv[h];
-      L2 = __builtin_elementwise_fma(r, r, L2);
+      if constexpr (ABSL) L2 += __builtin_elementwise_abs(r);
+      else L2 = __builtin_elementwise_fma(r, r, L2);
       if (PEARSON) {
         sd2 += d;
         sdd2 = __builtin_elementwise_fma(d, d, sdd2);
@@ -240,7 +251,7 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
         st2 += tv[h];
         stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
       }
-      const f2 w = r * inv;
+      const f2 w = ABSL ? f2{sgn_inv(r.x, inv.x), sgn_inv(r.y, inv.y)} : r * inv;
       px = __builtin_elementwise_fma(w, dx, px);
       py = __builtin_elementwise_fma(w, dy, py);
       pz = __builtin_elementwise_fma(w, dz, pz);
@@ -280,13 +291,14 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
 
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
-// PEARSON: also the d / t moments of the Pearson term (combined loss only).
+// KIND: KIND_MSE: sum (d - t)^2; KIND_COMBINED: also the d / t moments of the Pearson term;
+// KIND_CONTRASTIVE: sum |d - t| and w = sgn(d - t) / d.
 // BG: the background form (T = bg at every pair; no T read, no diagonal term -- the support pass,
 // pairdist_support_kernel, adds the entries that differ and the diagonal).
 #ifndef HICGAT_PD_BG_OCC
 #define HICGAT_PD_BG_OCC 1   // workgroups per CU the background form's register budget is set for
 #endif
-template <bool PEARSON>
+template <int KIND>
 __device__ void support_block(const float *__restrict__ coords, float bg, int row_begin, int row_end,
                               const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
                               const float *__restrict__ val, const float *__restrict__ diag, float4 *__restrict__ corr,
@@ -303,7 +315,7 @@ struct SupportArgs {
   int64_t ntiles = 0;
 };
 
-template <int MODE, bool VEC, bool PEARSON, bool BG = false, bool SUP = false>
+template <int MODE, bool VEC, int KIND, bool BG = false, bool SUP = false>
 __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
                                                             int64_t ldt, int64_t row0, int64_t col0,
@@ -315,7 +327,7 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   static_assert(!BG || (MODE == MODE_SYM && !VEC), "the background form is the training loss without a T image");
   static_assert(!SUP || BG, "the support pass rides only in the background form's launch");
   if (SUP && (int64_t)blockIdx.x >= sup.ntiles) {   // block-uniform
-    support_block<PEARSON>(coords, bg, sup.row_begin, sup.row_end, sup.rowptr, sup.col, sup.val, sup.diag, sup.corr,
+    support_block<KIND>(coords, bg, sup.row_begin, sup.row_end, sup.rowptr, sup.col, sup.val, sup.diag, sup.corr,
                            sup.mom, cmap, (int)(blockIdx.x - sup.ntiles));
     return;
   }
@@ -388,18 +400,18 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   constexpr bool PK = (VEC || BG) && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 0, 4, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
-    else tile_rows<MODE, VEC, PEARSON, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
+    if constexpr (PK) tile_rows_pk<KIND, 0, 4, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
+    else tile_rows<MODE, VEC, KIND, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 0, 4, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
+    tile_rows<MODE, VEC, KIND, true, 0, 4, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
   if (HICGAT_PD_DBG == 2) {
   } else if (interior) {
-    if constexpr (PK) tile_rows_pk<PEARSON, 4, 8, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
-    else tile_rows<MODE, VEC, PEARSON, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
+    if constexpr (PK) tile_rows_pk<KIND, 4, 8, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
+    else tile_rows<MODE, VEC, KIND, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
-    tile_rows<MODE, VEC, PEARSON, true, 4, 8, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
+    tile_rows<MODE, VEC, KIND, true, 4, 8, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   }
 
   // column partials: reduce over the 4 ty of this wave (lanes l, l^16, l^32, l^48), then waves
@@ -415,6 +427,7 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
       colred[wv][tx * 4 + (q & 3) + (q >> 2) * 64] = make_float4(A.ax[q], A.ay[q], A.az[q], 0.f);
   }
   if (MODE == MODE_SYM) {
+    constexpr bool PEARSON = KIND == KIND_COMBINED;
     double m[7] = {A.L, A.sd, A.sdd, A.sdt, A.st, A.stt, A.dg};
 #pragma unroll
     for (int c = 0; c < 7; ++c) {
@@ -534,8 +547,22 @@ __global__ __launch_bounds__(1024) void pairdist_reduce_kernel(const float4 *__r
   }
 }
 
-// stats[7..10] and loss from the (all-reduced) moments stats[0..6]: mse, pearson r, alpha, total.
+// stats[7..10] and loss from the (all-reduced) moments stats[0..6]: mse, pearson r, alpha, total;
+// contrastive: stats[7] = mean_{i<j} |T - D| (fp64, as the reference's float64 truth makes it),
+// stats[8] = NaN, stats[9] = 0.1, stats[10] = total = 0.1 * stats[7].
 __device__ void finalize_stats(int N, int loss_kind, double *__restrict__ stats, float *__restrict__ loss) {
+  if (loss_kind == KIND_CONTRASTIVE) {
+    const double M = 0.5 * (double)N * (double)(N - 1);
+    const double mae = M > 0.0 ? stats[0] / M : 0.0;
+    const double total = 0.1 * mae;
+    stats[7] = mae;
+    stats[8] = NAN;
+    stats[9] = 0.1;
+    stats[10] = total;
+    stats[11] = 0.0;
+    if (loss) loss[0] = (float)total;
+    return;
+  }
   const double n2 = (double)N * (double)N;
   const double mse = (2.0 * stats[0] + stats[6]) / n2;
   const double M = 0.5 * (double)N * (double)(N - 1);
@@ -613,13 +640,16 @@ __global__ __launch_bounds__(64) void moments_finalize_kernel(const double *__re
 //   moments   over j > i only (each pair once, in fp64), the support's change of the bulk's terms:
 //             L += (d - t)^2 - (d - bg)^2, sdt += d (t - bg), st += t - bg, stt += t^2 - bg^2; and the
 //             diagonal's (0 - T_ii)^2 into the dg moment.
+// Contrastive (KIND_CONTRASTIVE): corr[i] = sum_j (sgn(d - t) - sgn(d - bg)) / d * (c_i - c_j), and
+// L += |d - t| - |d - bg| over j > i; no diagonal term (the loss is over i < j only).
 // d is formed exactly as in the bulk's interior path.  Per-block moment records (fixed order).
-template <bool PEARSON>
+template <int KIND>
 __device__ void support_block(const float *__restrict__ coords, float bg, int row_begin, int row_end,
                                               const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
                                               const float *__restrict__ val, const float *__restrict__ diag,
                                               float4 *__restrict__ corr, double *__restrict__ mom,
                                               const int *__restrict__ cmap, int blk) {
+  constexpr bool PEARSON = KIND == KIND_COMBINED, ABSL = KIND == KIND_CONTRASTIVE;
   __shared__ double mred[4][7];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = row_begin + blk * 4 + wv;
@@ -637,14 +667,14 @@ __device__ void support_block(const float *__restrict__ coords, float bg, int ro
       const float d2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, 0x1.0p-100f)));
       const float inv = __builtin_amdgcn_rsqf(d2);
       const float d = d2 * inv;
-      const float w = (bg - t) * inv;
+      const float w = ABSL ? sgn_inv(d - t, inv) - sgn_inv(d - bg, inv) : (bg - t) * inv;
       gx = fmaf(w, dx, gx);
       gy = fmaf(w, dy, gy);
       gz = fmaf(w, dz, gz);
       if (j > i) {
         const double dd = d, td = t, bd = bg;
         const double r = dd - td, rb = dd - bd;
-        L += r * r - rb * rb;
+        L += ABSL ? fabs(r) - fabs(rb) : r * r - rb * rb;
         if (PEARSON) {
           sdt += dd * (td - bd);
           st += td - bd;
@@ -652,7 +682,7 @@ __device__ void support_block(const float *__restrict__ coords, float bg, int ro
         }
       }
     }
-    if (lane == 0) {
+    if (lane == 0 && !ABSL) {
       const float ti = diag[i];
       dg = (double)ti * (double)ti;
     }
@@ -679,7 +709,7 @@ __device__ void support_block(const float *__restrict__ coords, float bg, int ro
         ((mred[0][threadIdx.x] + mred[1][threadIdx.x]) + mred[2][threadIdx.x]) + mred[3][threadIdx.x];
 }
 
-template <bool PEARSON>
+template <int KIND>
 __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__restrict__ coords, int N, float bg,
                                                                int row_begin, int row_end,
                                                                const int32_t *__restrict__ rowptr,
@@ -688,7 +718,7 @@ __global__ __launch_bounds__(256) void pairdist_support_kernel(const float *__re
                                                                const float *__restrict__ diag,
                                                                float4 *__restrict__ corr, double *__restrict__ mom,
                                                                const int *__restrict__ cmap) {
-  support_block<PEARSON>(coords, bg, row_begin, row_end, rowptr, col, val, diag, corr, mom, cmap, blockIdx.x);
+  support_block<KIND>(coords, bg, row_begin, row_end, rowptr, col, val, diag, corr, mom, cmap, blockIdx.x);
 }
 
 // D[i, j] = ||c_i - c_j||: one thread per element.
@@ -722,6 +752,14 @@ extern "C" int64_t hicgat_pairdist_num_tiles(int N, int mode) {
 // per tile: a (1 + ncol) x 128 float4 partial slab and ncol x 8 fp64 moments (ncol = 1: one column
 // slab per tile)
 static int pd_ncol(int) { return 1; }
+
+// the per-pair gradient factor the reduction applies: MSE over N^2 entries of the symmetric D
+// (each pair twice, d(d - t)^2 = 2 (d - t)): 4 / N^2; contrastive: 0.1 / M, M = N (N - 1) / 2 pairs --
+// float32(0.1 / M), the value the reference's autograd hands to cdist's backward
+static float loss_scale(int N, int loss_kind) {
+  if (loss_kind == KIND_CONTRASTIVE) return N > 1 ? (float)(0.1 / (0.5 * (double)N * (double)(N - 1))) : 0.f;
+  return (float)(4.0 / ((double)N * (double)N));
+}
 
 extern "C" size_t hicgat_pairdist_workspace_bytes(int N, int mode) {
   const int64_t tiles = hicgat_pairdist_num_tiles(N, mode);
@@ -772,10 +810,10 @@ extern "C" int hicgat_pairdist_bwd(const float *coords, const float *G, int N, i
   const bool vec = (ldg % 4 == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) &&
                    ldg >= (int64_t)nb * BT;
   if (vec)
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true, false>), dim3(tiles), dim3(256), kTileLds,
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, true, KIND_MSE>), dim3(tiles), dim3(256), kTileLds,
                        (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, 0.f);
   else
-    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false, false>), dim3(tiles), dim3(256), 0,
+    hipLaunchKernelGGL((pairdist_tile_kernel<MODE_FULL, false, KIND_MSE>), dim3(tiles), dim3(256), 0,
                        (hipStream_t)stream, coords, G, N, ldg, (int64_t)0, (int64_t)0, nb, (int64_t)0, part, mom, 0.f);
   HICGAT_CHECK_LAUNCH();
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3((N + 63) / 64), dim3(1024), 0,
@@ -790,7 +828,7 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
                                               int64_t tile_begin, int64_t tile_end, int loss_kind,
                                               double *stats, float *loss, float *dcoords, void *workspace,
                                               size_t workspace_bytes, hicgat_stream_t stream) {
-  if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N < 0 || loss_kind < KIND_MSE || loss_kind > KIND_CONTRASTIVE) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !T || !stats || !workspace) return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_pairdist_workspace_bytes(N, HICGAT_PD_TRI)) return HICGAT_EINVAL;
@@ -815,20 +853,26 @@ extern "C" int hicgat_pairdist_mse_fused_band(const float *coords, const float *
   const bool vec = (ldt % 4 == 0) && (t_col0 % 4 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                    ldt >= (int64_t)nb * BT - t_col0;
   if (nt > 0) {
-    // the Pearson moments only for the combined loss (loss_kind 1); MSE needs sum (d - t)^2 only
-#define HICGAT_PD_SYM(V, P)                                                                          \
-  hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, P>), dim3(nt), dim3(256), V ? kTileLds : 0, \
+    // the Pearson moments only for the combined loss; MSE needs sum (d - t)^2 only
+#define HICGAT_PD_SYM(V, KD)                                                                          \
+  hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, V, KD>), dim3(nt), dim3(256), V ? kTileLds : 0, \
                      (hipStream_t)stream, coords, T, N, ldt, t_row0, t_col0, nb, tile_begin, part, mom, 0.f)
-    if (vec && loss_kind == 1) HICGAT_PD_SYM(true, true);
-    else if (vec) HICGAT_PD_SYM(true, false);
-    else if (loss_kind == 1) HICGAT_PD_SYM(false, true);
-    else HICGAT_PD_SYM(false, false);
+#define HICGAT_PD_KINDS(V)                                                  \
+  if (loss_kind == KIND_COMBINED) HICGAT_PD_SYM(V, KIND_COMBINED);          \
+  else if (loss_kind == KIND_CONTRASTIVE) HICGAT_PD_SYM(V, KIND_CONTRASTIVE); \
+  else HICGAT_PD_SYM(V, KIND_MSE)
+    if (vec) {
+      HICGAT_PD_KINDS(true);
+    } else {
+      HICGAT_PD_KINDS(false);
+    }
+#undef HICGAT_PD_KINDS
 #undef HICGAT_PD_SYM
     HICGAT_CHECK_LAUNCH();
   }
   // row / column partials -> dcoords (when wanted) and, in the same launch, kMomBlocks blocks of
   // tile-moment partials; then one small launch: partials -> stats[0..6] -> mse / r / alpha / total
-  const float scale = (float)(4.0 / ((double)N * (double)N));
+  const float scale = loss_scale(N, loss_kind);
   const int row_blocks = dcoords ? (N + 63) / 64 : 0;
   double *mpart = mom + (size_t)tiles * 8;
   hipLaunchKernelGGL(pairdist_reduce_kernel, dim3(row_blocks + kMomBlocks), dim3(1024), 0, (hipStream_t)stream, part,
@@ -853,7 +897,7 @@ extern "C" int hicgat_pairdist_mse_fused(const float *coords, const float *T, in
 
 extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss,
                                         hicgat_stream_t stream) {
-  if (N <= 0 || !stats || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N <= 0 || !stats || loss_kind < KIND_MSE || loss_kind > KIND_CONTRASTIVE) return HICGAT_EINVAL;
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, N, loss_kind,
                      stats, loss);
   HICGAT_CHECK_LAUNCH();
@@ -872,7 +916,7 @@ __global__ __launch_bounds__(256) void finalize_rows_kernel(int N, int loss_kind
 
 extern "C" int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64,
                                              int row_begin, int row_end, float *dcoords, hicgat_stream_t stream) {
-  if (N <= 0 || !stats || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N <= 0 || !stats || loss_kind < KIND_MSE || loss_kind > KIND_CONTRASTIVE) return HICGAT_EINVAL;
   if (row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   const int64_t n3 = 3 * (int64_t)(row_end - row_begin);
   if (n3 > 0 && (!dc64 || !dcoords)) return HICGAT_EINVAL;
@@ -901,7 +945,7 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
                                                           int loss_kind, double *stats, float *loss, float *dcoords,
                                                           double *dcoords64, void *workspace,
                                                           size_t workspace_bytes, hicgat_stream_t stream) {
-  if (N < 0 || (loss_kind != 0 && loss_kind != 1)) return HICGAT_EINVAL;
+  if (N < 0 || loss_kind < KIND_MSE || loss_kind > KIND_CONTRASTIVE) return HICGAT_EINVAL;
   if (N == 0) return HICGAT_OK;
   if (!coords || !rowptr || !col || !val || !diag || !stats || !workspace) return HICGAT_EINVAL;
   if (workspace_bytes < hicgat_pairdist_support_workspace_bytes(N)) return HICGAT_EINVAL;
@@ -930,8 +974,8 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
   // launch fewer on the critical path; at N = 20000 on one GPU the support pass needs the occupancy
   // of its own launch: 1.881 / 1.884 vs 1.875 / 1.877 ms per step, profiles/r04u_ab_single_gpu.txt)
   const bool ride = dcoords64 && SUPPORT_RIDES && nt > 0 && sblocks > 0;
+  SupportArgs sa;
   if (ride) {
-    SupportArgs sa;
     sa.rowptr = rowptr;
     sa.col = col;
     sa.val = val;
@@ -941,36 +985,26 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
     sa.row_begin = support_row_begin;
     sa.row_end = support_row_end;
     sa.ntiles = nt;
-    if (loss_kind == 1)
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true, true>), dim3(nt + sblocks), dim3(256), 0, s,
+  }
+  const auto tiles_for = [&](auto kind_c) {
+    constexpr int KD = decltype(kind_c)::value;
+    if (ride)
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, KD, true, true>), dim3(nt + sblocks), dim3(256), 0, s,
                          coords, nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background,
                          cmap, sa);
-    else
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true, true>), dim3(nt + sblocks), dim3(256), 0,
-                         s, coords, nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom,
-                         background, cmap, sa);
-    HICGAT_CHECK_LAUNCH();
-  } else if (nt > 0) {
-    if (loss_kind == 1)
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, true, true>), dim3(nt), dim3(256), 0, s, coords,
+    else if (nt > 0)
+      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, KD, true>), dim3(nt), dim3(256), 0, s, coords,
                          nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
-    else
-      hipLaunchKernelGGL((pairdist_tile_kernel<MODE_SYM, false, false, true>), dim3(nt), dim3(256), 0, s, coords,
-                         nullptr, N, (int64_t)0, (int64_t)0, (int64_t)0, nb, tile_begin, part, mom, background, cmap);
-    HICGAT_CHECK_LAUNCH();
-  }
-  if (sblocks > 0 && !ride) {
-    if (loss_kind == 1)
-      hipLaunchKernelGGL(pairdist_support_kernel<true>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
-                         support_row_begin, support_row_end, rowptr, col, val, diag, corr,
-                         mom + (size_t)tile_end * 8, cmap);
-    else
-      hipLaunchKernelGGL(pairdist_support_kernel<false>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
-                         support_row_begin, support_row_end, rowptr, col, val, diag, corr,
-                         mom + (size_t)tile_end * 8, cmap);
-    HICGAT_CHECK_LAUNCH();
-  }
-  const float scale = (float)(4.0 / ((double)N * (double)N));
+    if (sblocks > 0 && !ride)
+      hipLaunchKernelGGL(pairdist_support_kernel<KD>, dim3(sblocks), dim3(256), 0, s, coords, N, background,
+                         support_row_begin, support_row_end, rowptr, col, val, diag, corr, mom + (size_t)tile_end * 8,
+                         cmap);
+  };
+  if (loss_kind == KIND_COMBINED) tiles_for(std::integral_constant<int, KIND_COMBINED>{});
+  else if (loss_kind == KIND_CONTRASTIVE) tiles_for(std::integral_constant<int, KIND_CONTRASTIVE>{});
+  else tiles_for(std::integral_constant<int, KIND_MSE>{});
+  HICGAT_CHECK_LAUNCH();
+  const float scale = loss_scale(N, loss_kind);
   const int row_blocks = (dcoords || dcoords64) ? (N + 63) / 64 : 0;
   // dcoords64: the caller all-reduces [stats | dcoords64] and finalizes (hicgat_pairdist_finalize_rows),
   // so a small share's moments go straight into stats[0..6] (stats[7..11] and loss are left alone)

@@ -144,6 +144,7 @@ SIGNATURES = {
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
     "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_int, c_p]),
     "hicgat_step_begin": (c_int, [c_p, c_i64, c_p, c_p]),
+    "hicgat_sim_collective": (c_int, [c_f, c_int, c_int, c_p]),
 }
 
 

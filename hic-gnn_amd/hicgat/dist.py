@@ -207,8 +207,70 @@ class ShardPlan:
         return I0 * TILE, min(self.N, (I1 + 1) * TILE), I0 * TILE
 
 
+# ---- the collective model (bench.py --simulate-world) --------------------------------------------
+# NOT measured on this pool (one-GPU boxes): stated assumptions.  RCCL on one MI355X node: 7 xGMI
+# links per GPU (~153 GB/s each); a collective costs a latency term plus its bytes over the
+# bus bandwidth it sustains (ring convention).  ``bench.py --gpus N`` reports the measured time of
+# every collective beside these figures (``COMM_TIMERS``), so the first multi-GPU run checks them.
+RCCL_LAT_US = 12.0         # small-message latency of one RCCL collective inside a captured graph
+RCCL_BUS_GBS = 300.0       # sustained bus bandwidth of an all-reduce / all-gather over 8 ranks
+# CU footprint of an emulated collective: RCCL launches one workgroup per channel; 16 channels of
+# 256 threads is the assumption for these (<= 2.4 MB) messages on an 8-GPU xGMI node
+SIM_COMM_WGS = int(os.environ.get("HICGAT_SIM_COMM_WGS", "16"))
+SIM_COMM_THREADS = 256
+
+
+def coll_us(kind, nbytes, P):
+    """Modeled time of one collective over P ranks: all_gather moves (P-1)/P of the buffer into each
+    rank, all_reduce 2 (P-1)/P of it (ring / tree bus-bandwidth convention)."""
+    f = (P - 1) / P * (2.0 if kind == "all_reduce" else 1.0)
+    return RCCL_LAT_US + f * nbytes / (RCCL_BUS_GBS * 1e3)
+
+
+# name -> list of (start, end) torch.cuda.Event pairs (or host seconds for CPU tensors) around every
+# collective; bench.py sets it to {} for its eager per-kernel pass (None: off)
+COMM_TIMERS = None
+MODELED = {}    # name -> (kind, bytes) of the last call of that collective (for the report)
+
+
+def _record(name, kind, t, P, fn):
+    MODELED[name] = (kind, t.numel() * t.element_size(), P)
+    if COMM_TIMERS is None:
+        return fn()
+    if t.is_cuda:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        COMM_TIMERS.setdefault(name, []).append((e0, e1))
+        return out
+    import time
+    t0 = time.perf_counter()
+    out = fn()
+    COMM_TIMERS.setdefault(name, []).append(time.perf_counter() - t0)
+    return out
+
+
+def comm_report():
+    """{name: {"calls", "avg_us", "modeled_us", "bytes", "kind"}} of the collectives timed since
+    ``COMM_TIMERS`` was set (after a device sync)."""
+    out = {}
+    for name, rec in (COMM_TIMERS or {}).items():
+        if rec and isinstance(rec[0], tuple):
+            us = [a.elapsed_time(b) * 1e3 for a, b in rec]
+        else:
+            us = [1e6 * v for v in rec]
+        kind, nbytes, P = MODELED.get(name, (None, None, None))
+        out[name] = {"calls": len(us), "avg_us": float(np.mean(us)), "min_us": float(np.min(us)),
+                     "kind": kind, "bytes": nbytes,
+                     "modeled_us": coll_us(kind, nbytes, P) if kind else None}
+    return out
+
+
 class DistComm:
-    """Collectives over a torch.distributed group (RCCL = backend "nccl" on ROCm, or gloo)."""
+    """Collectives over a torch.distributed group (RCCL = backend "nccl" on ROCm, or gloo).
+    ``name`` labels each call for ``COMM_TIMERS`` / ``comm_report``."""
 
     def __init__(self, group=None):
         self.group = group
@@ -216,33 +278,52 @@ class DistComm:
         self.rank = dist.get_rank(group)
         self.nccl = dist.get_backend(group) == "nccl"
 
-    def all_gather_inplace(self, buf, own):
+    def all_gather_inplace(self, buf, own, name="all_gather"):
         """All-gather where this rank's input ``own`` is its own chunk of ``buf`` (RCCL in place)."""
         if self.nccl:
-            dist.all_gather_into_tensor(buf, own, group=self.group)
+            fn = lambda: dist.all_gather_into_tensor(buf, own, group=self.group)   # noqa: E731
         else:
-            dist.all_gather(list(buf.chunk(self.P)), own.clone(), group=self.group)
+            fn = lambda: dist.all_gather(list(buf.chunk(self.P)), own.clone(), group=self.group)   # noqa: E731
+        _record(name, "all_gather", buf, self.P, fn)
 
-    def all_reduce(self, t):
-        dist.all_reduce(t, group=self.group)
+    def all_reduce(self, t, name="all_reduce"):
+        _record(name, "all_reduce", t, self.P, lambda: dist.all_reduce(t, group=self.group))
 
     def all_gather_list(self, out, t):
         dist.all_gather(out, t, group=self.group)
 
 
 class SimComm:
-    """ONE rank of a P-rank job with the collectives left out (bench.py --simulate-world): the
-    rank's kernels run exactly as in the real step, on its real shard, so their time is the
-    per-rank compute of a P-GPU step; the buffers the collectives would fill keep their contents."""
+    """ONE rank of a P-rank job on one GPU (bench.py --simulate-world): the rank's kernels run
+    exactly as in the real step, on its real shard; each collective is EMULATED where it would be
+    issued -- ``hicgat_sim_collective`` holds ``SIM_COMM_WGS`` workgroups resident for the modeled
+    time (``coll_us`` of the real buffer's bytes) on that stream -- so a captured rank step shows
+    the collectives' time, their overlap with kernels on other streams and their CU footprint.
+    ``emulate=False``: the collectives are left out (the round-4 model added them serially).  The
+    buffers the collectives would fill keep their contents."""
 
-    def __init__(self, P, rank):
+    def __init__(self, P, rank, emulate=True):
         self.P, self.rank, self.nccl, self.group = P, rank, True, None
+        self.emulate = emulate
 
-    def all_gather_inplace(self, buf, own):
-        pass
+    def _emulate(self, name, kind, t):
+        if not self.emulate or not getattr(t, "is_cuda", False):
+            MODELED[name] = (kind, t.numel() * t.element_size(), self.P)
+            return
 
-    def all_reduce(self, t):
-        pass
+        def fn():
+            from . import _lib
+            lib = _lib.lib()
+            _lib.check(lib.hicgat_sim_collective(float(coll_us(kind, t.numel() * t.element_size(), self.P)),
+                                                 SIM_COMM_WGS, SIM_COMM_THREADS, _lib.stream(t.device)),
+                       "hicgat_sim_collective")
+        _record(name, kind, t, self.P, fn)
+
+    def all_gather_inplace(self, buf, own, name="all_gather"):
+        self._emulate(name, "all_gather", buf)
+
+    def all_reduce(self, t, name="all_reduce"):
+        self._emulate(name, "all_reduce", t)
 
 
 class ShardedTrainer:
@@ -259,7 +340,9 @@ class ShardedTrainer:
         self.group = group
         self.P = P = self.comm.P
         self.rank = rank = self.comm.rank
-        self.kind = {"mse": 0, "combined": 1}[kind]
+        self.kind = ops.LOSS_KINDS[kind]
+        if kind == "contrastive":
+            truth = truth.upper()      # the contrastive loss reads truth[triu] as given
         self.mode = mode
         dev = model.conv.lin_l.weight.device
         self.cuda = dev.type == "cuda"
@@ -343,6 +426,10 @@ class ShardedTrainer:
         # da_dst for every r: 0 there, so only the owner adds da_dst_r * att_dst into dh_r)
         self.rs = torch.zeros((N if mode == "xagg" else rows, 4 * self.H), **f32)
         self.coords_buf = torch.zeros((P * R, 3), **f32)
+        # step()'s coordinates in global row order (the loss reads the padded all-gather layout
+        # through gidx; the reorder runs on a side stream beside the loss, off the critical path)
+        self.coords_glob = torch.zeros((N, 3), **f32)
+        self._glob_ev = None
         if isinstance(self.comm, SimComm):
             # the other ranks' coordinates, which the all-gather would bring: any spread-out values
             g = torch.Generator().manual_seed(rank)
@@ -362,6 +449,7 @@ class ShardedTrainer:
         cut = (max(ends) + 3) // 4 * 4
         self.grad_split = cut if (firsts and min(firsts) >= cut) else None
         self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
+        self.coord_stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
@@ -391,7 +479,7 @@ class ShardedTrainer:
             K.fused_loss(coords, self.tband, N, self.kind, self.t0, self.t1, self.stats, self.loss, self.dcoords,
                          row0=self.trow0, col0=self.tcol0)
             self.dc64.copy_(self.dcoords)
-        self.comm.all_reduce(self.red)
+        self.comm.all_reduce(self.red, name="loss_all_reduce")
         # finalize + this rank's rows of dcoords narrowed to fp32, one launch
         K.loss_finalize(N, self.kind, self.stats, self.loss, dc64=self.dc64, r0=self.r0, r1=self.r1,
                         dcoords=self.dcoords)
@@ -411,10 +499,20 @@ class ShardedTrainer:
         else:
             coords_loc = self.model.post_act(o) if self.act else self.model.tail(o)
             own.copy_(coords_loc.detach())
-        self.comm.all_gather_inplace(self.coords_buf, self._own(self.coords_buf))
+        self.comm.all_gather_inplace(self.coords_buf, self._own(self.coords_buf), name="coords_all_gather")
         # direct: the loss reads the padded buffer through gidx (no reorder launch); the returned
         # coordinates are then in that layout (``global_coords`` reorders them)
-        coords = self.coords_buf if self.direct_coords else self.coords_buf.index_select(0, self.gidx)
+        if self.direct_coords:
+            coords = self.coords_buf
+            cur = torch.cuda.current_stream()
+            self.coord_stream.wait_stream(cur)
+            with torch.cuda.stream(self.coord_stream):
+                torch.index_select(self.coords_buf, 0, self.gidx, out=self.coords_glob)
+                self._glob_ev = torch.cuda.Event()
+                self._glob_ev.record()
+        else:
+            coords = self.coords_buf.index_select(0, self.gidx)
+            self.coords_glob.copy_(coords)
         self._loss(coords)
         return o, coords_loc, coords
 
@@ -423,6 +521,8 @@ class ShardedTrainer:
         return self.coords_buf.index_select(0, self.gidx)
 
     def step(self):
+        """One training step; returns (loss, stats, coords) with coords [N, 3] in global row order
+        (the coordinates the step's loss was evaluated on)."""
         if self.mode == "xagg" and self.cuda:
             self.opt._reattach()     # the gradient buffer is zeroed by the step's first launch (xagg_logits)
         else:
@@ -436,7 +536,10 @@ class ShardedTrainer:
             coords, tail_done = self._step_allgather()
         self._grad_allreduce(tail_done)
         self.opt.step(counted=self._ctr() is not None)
-        return self.loss, self.stats, coords
+        if self._glob_ev is not None:
+            torch.cuda.current_stream().wait_event(self._glob_ev)
+            self._glob_ev = None
+        return self.loss, self.stats, self.coords_glob
 
     def _ctr(self):
         """The optimizer's device step count when the xagg step's first launch advances it (HIP path,
@@ -450,7 +553,7 @@ class ShardedTrainer:
         lin_l's dW GEMM) and the GATConv's; the optimizer's stream waits for both."""
         g, cut = self.opt.grad, self.grad_split
         if cut is None:
-            self.comm.all_reduce(g)
+            self.comm.all_reduce(g, name="grad_all_reduce")
             return
         if self.cuda:
             cs = self.comm_stream
@@ -460,12 +563,12 @@ class ShardedTrainer:
             else:                       # no side stream in use: the tail's gradients are on this one
                 cs.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(cs):
-                self.comm.all_reduce(g[cut:])
-            self.comm.all_reduce(g[:cut])
+                self.comm.all_reduce(g[cut:], name="grad_all_reduce_tail_bucket")
+            self.comm.all_reduce(g[:cut], name="grad_all_reduce_gat_bucket")
             torch.cuda.current_stream().wait_stream(cs)
         else:
-            self.comm.all_reduce(g[cut:])
-            self.comm.all_reduce(g[:cut])
+            self.comm.all_reduce(g[cut:], name="grad_all_reduce_tail_bucket")
+            self.comm.all_reduce(g[:cut], name="grad_all_reduce_gat_bucket")
 
     def _side_event(self):
         """Events after the side streams' queued work (the tail's dW GEMMs), or None (CPU)."""
@@ -484,7 +587,7 @@ class ShardedTrainer:
         # ---- backward -----------------------------------------------------------------------
         tail_done = None
         dout = self.pack[:, :D]
-        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
+        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT, hold_big=False):
             coords_loc.backward(self.dcoords[r0:r1])
             self.gbuf[r0:r1].copy_(o.grad)
             K.agg_bwd_rows(r0, r1, self.act, self.gbuf, self.out, bias, self.out2, dout, self.rs)
@@ -576,14 +679,14 @@ class ShardedTrainer:
         W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
         # ---- forward ------------------------------------------------------------------------
         K.linear_att(self.x_loc, W, al, ar, h=self.h[q0:q1])
-        self.comm.all_gather_inplace(self.h, self._own(self.h))
+        self.comm.all_gather_inplace(self.h, self._own(self.h), name="h_all_gather")
         a_src, a_dst = K.att_logits(self.h, al, ar)
         K.agg_fwd_act(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, self.bias.detach(), self.ns, self.act,
                       self.out, self.out2, self.rs)
         o, coords_loc, coords = self._tail()
         # ---- backward -----------------------------------------------------------------------
         tail_done = None
-        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT):
+        with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT, hold_big=False):
             coords_loc.backward(self.dcoords[self.r0:self.r1])
             dout, rs_all = self.pack[:, :D], self.pack[:, D:]
             self.gbuf[q0:q1].copy_(o.grad)
@@ -593,7 +696,7 @@ class ShardedTrainer:
             if not self.act:
                 dout[q0:q1].copy_(self.gbuf[q0:q1])
             rs_all[q0:q1].copy_(self.rs[q0:q1])
-            self.comm.all_gather_inplace(self.pack, self._own(self.pack))
+            self.comm.all_gather_inplace(self.pack, self._own(self.pack), name="pack_all_gather")
             K.agg_bwd_src(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, rs_all, dout, al, ar, self.ns,
                           self.dh, self.da_src)
             ops.side_flush(after=fork, lanes=SIDE_LANES)

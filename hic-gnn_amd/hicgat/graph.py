@@ -439,6 +439,18 @@ class Truth:
     def dense(self):
         return self.buf[:, :self.n]
 
+    def upper(self):
+        """The target the contrastive loss sees: truth[triu] AS GIVEN in both triangles (that loss reads
+        the upper-triangle entries themselves, not their symmetric mean) -- ``self`` when the source was
+        symmetric; otherwise a second Truth, built once and cached."""
+        if self.raw is None:
+            return self
+        if getattr(self, "_upper", None) is None:
+            t = self.raw.to(self.buf.device)
+            u = torch.triu(t, 1)
+            self._upper = Truth(u + u.t(), background=None if self.support is None else self.support.background)
+        return self._upper
+
     def scoring(self):
         """The matrix whose upper triangle the reference scores dSCC against (HiC-GNN_main.py:135-139
         takes truth[triu] as given): the target before symmetrisation when it was asymmetric."""

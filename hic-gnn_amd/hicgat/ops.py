@@ -32,7 +32,7 @@ def _sink(p):
 # L2-bound aggregation backward instead of in series with it; in a captured step the fork and join
 # are graph edges.  Only sink-bound gradients (``_sink``) go to the side stream -- a gradient that
 # is returned to autograd is consumed on the backward's stream and must be produced there.
-_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": [], "grouped": 0, "jobs": []}
+_SIDE = {"on": 0, "streams": {}, "mains": {}, "hold": [], "queue": [], "grouped": 0, "jobs": [], "no_big": 0}
 _SIDE_LOCK = threading.Lock()
 OVERLAP_DEFAULT = True
 # The tail's parameter-gradient launches (split-K dW GEMMs with their bias sums, the LayerNorm
@@ -132,6 +132,12 @@ def grouped_param_grads():
         _SIDE["grouped"] += 1
     try:
         yield
+    except BaseException:
+        # a failed backward: drop the collected descriptors, so no later grouped_flush adds this
+        # step's partial dW / db into another step's gradient
+        with _SIDE_LOCK:
+            _SIDE["jobs"].clear()
+        raise
     finally:
         with _SIDE_LOCK:
             _SIDE["grouped"] -= 1
@@ -173,17 +179,30 @@ def side_join():
 
 
 @contextlib.contextmanager
-def overlapped_param_grads(enabled=None):
+def overlapped_param_grads(enabled=None, hold_big=True):
     """``with overlapped_param_grads(): loss.backward()`` -- parameter gradients overlap the rest
-    of the backward and are complete (ordered before the caller's stream) on exit."""
+    of the backward and are complete (ordered before the caller's stream) on exit.
+
+    ``hold_big=False``: no BIG_GROUP holding -- for a backward that has no ``_GATConvFn`` to issue
+    the held jobs with lin_l's dW (the sharded step runs the GATConv backward itself; a held job
+    would otherwise be issued by ``side_join`` on the main stream, after the caller recorded the
+    side streams' completion for its gradient all-reduce)."""
     if not (OVERLAP_DEFAULT if enabled is None else enabled):
         yield
         return
     side_begin()
+    if not hold_big:
+        with _SIDE_LOCK:
+            _SIDE["no_big"] += 1
     try:
         yield
     finally:
-        side_join()
+        try:
+            side_join()
+        finally:
+            if not hold_big:
+                with _SIDE_LOCK:
+                    _SIDE["no_big"] -= 1
 
 
 def _param_launch(fn, *keep, small=False, work=0, job=None):
@@ -192,7 +211,8 @@ def _param_launch(fn, *keep, small=False, work=0, job=None):
     else now on the side stream.  ``keep`` are the tensors ``fn`` reads (held until the join).
     ``job``: the same work as a descriptor for ``grouped_flush`` -- ("w", dy, x, dW, db) for
     dW += dy^T x (and db += column sums of dy), ("c", src, dst) for dst += column sums of src."""
-    if job is not None and (_SIDE["grouped"] or (BIG_GROUP > 0 and _SIDE["on"] and work >= BIG_GROUP)):
+    if job is not None and (_SIDE["grouped"] or (BIG_GROUP > 0 and _SIDE["on"] and not _SIDE["no_big"]
+                                                 and work >= BIG_GROUP)):
         with _SIDE_LOCK:
             _SIDE["jobs"].append((job, keep))
         return
@@ -840,10 +860,15 @@ def backward_from_loss(loss):
     torch.autograd.backward(loss, grad_tensors=seed)
 
 
+LOSS_KINDS = {"mse": 0, "combined": 1, "contrastive": 2}   # include/hicgat.h loss_kind
+
+
 def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
-    """MSE(cdist(coords), truth) [kind="mse", HiC-GNN_main.py:127] or
+    """MSE(cdist(coords), truth) [kind="mse", HiC-GNN_main.py:127],
     MSE + alpha*(1 - pearson) [kind="combined", HiC_GAT_generalize_directly.py:219-225] with the
-    gradient of the MSE only (the Pearson term is a detached host value in the reference).
+    gradient of the MSE only (the Pearson term is a detached host value in the reference), or
+    0.1 * mean_{i<j} |T_ij - D_ij| [kind="contrastive", train_and_test_same_res_GAT_node2vec.py:107-134:
+    differentiable; its fp64 value in stats[10], the returned scalar is its fp32 rounding].
 
     ``truth`` is a ``graph.Truth`` (stored symmetric; an asymmetric target is folded into the
     equivalent symmetric form there); with a background + support form (``truth.support``, e.g.
@@ -853,7 +878,9 @@ def fused_dist_loss(coords, truth, kind="mse", tile_range=(0, -1), stats=None):
     _dev_check(coords)
     if stats is None:
         stats = torch.empty(12, dtype=torch.float64, device=coords.device)
-    kind_i = {"mse": 0, "combined": 1}[kind]
+    kind_i = LOSS_KINDS[kind]
+    if kind == "contrastive":
+        truth = truth.upper()       # the contrastive loss reads truth[triu] as given
     t0, t1 = int(tile_range[0]), int(tile_range[1])
     # the background + support form (no truth stream) when the truth has one and all tiles are wanted
     whole = t0 == 0 and t1 in (-1, kernels.default().num_tiles(truth.n))

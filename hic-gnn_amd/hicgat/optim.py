@@ -94,6 +94,13 @@ class FlatAdam:
         kern.adam(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.numel, self.lr, self.betas[0],
                   self.betas[1], self.eps, self.step_count)
 
+    def sync_step_count(self):
+        """Bring the host ``step_count`` up to the device count: replays of a captured step advance
+        only ``step_ctr`` (the host count stops at the capture), so read it back once after a run."""
+        if getattr(self, "step_ctr", None) is not None:
+            self.step_count = int(self.step_ctr.item())
+        return self.step_count
+
     def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
+        return {"step": self.sync_step_count(), "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
                 "lr": self.lr, "betas": self.betas, "eps": self.eps}

@@ -8,7 +8,9 @@ Loop semantics kept from HiC-GNN_main.py:117-132:
 The step runs the fused distance/loss kernel (the N x N matrix is never stored) and FlatAdam; the
 loss comparison is the one device->host sync per step, as in the reference.  ``steps=K`` runs a
 fixed number of steps instead (the deterministic parity protocol of SURVEY.md section 8(d)).
-``loss="combined"`` is the HiC_GAT_generalize_directly.py:206-239 objective (MSE + alpha*(1-r)).
+``loss="combined"`` is the HiC_GAT_generalize_directly.py:206-239 objective (MSE + alpha*(1-r));
+``loss="contrastive"`` the train_and_test_same_res_GAT_node2vec.py:98-134 one (0.1 * mean_{i<j}
+|T - D|, float64 as the reference's float64 truth makes it: the lossdiff rule reads that fp64 value).
 """
 import argparse
 import ast
@@ -62,8 +64,9 @@ def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_
     while (diff > thresh if steps is None else len(hist) < steps) and len(hist) < max_steps:
         if use_graph and replay is None and len(hist) >= GRAPH_WARMUP:
             replay = CapturedStep(step, warmup=0)     # captured, not run: the replay below is this step
-        val, _, coords = replay() if replay is not None else step()
-        lv = float(val.item())                        # the one device -> host read per step
+        val, st, coords = replay() if replay is not None else step()
+        # the one device -> host read per step (the contrastive total is float64 in the reference)
+        lv = float(st[10].item()) if loss == "contrastive" else float(val.item())
         diff = abs(old - lv)
         old = lv
         hist.append(lv)
@@ -74,6 +77,7 @@ def train(model, data, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", max_
                       f"Loss Diff: {diff}")
         if on_step is not None:
             on_step(len(hist), lv)
+    opt.sync_step_count()     # replays advanced only the device count
     return opt, hist
 
 
@@ -114,7 +118,7 @@ def main(argv=None):
     p.add_argument("-th", "--threshold", type=float, default=1e-8)
     p.add_argument("--steps", type=int, default=None, help="fixed step count instead of the threshold rule")
     p.add_argument("--model", default="GATNetSelectiveResidualsUpdated", choices=sorted(MODELS))
-    p.add_argument("--loss", default="mse", choices=["mse", "combined"])
+    p.add_argument("--loss", default="mse", choices=["mse", "combined", "contrastive"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--out", default=None, help="prefix for <out>_weights.pt / _structure.pdb / _log.txt")
     p.add_argument("--no-kr", action="store_true", help="the input is already KR-normalised (skip KRnorm)")

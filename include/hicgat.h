@@ -30,6 +30,9 @@ extern "C" {
 
 typedef void *hicgat_stream_t;
 
+/* loss_kind of the fused distance / loss entry points */
+enum { HICGAT_LOSS_MSE = 0, HICGAT_LOSS_COMBINED = 1, HICGAT_LOSS_CONTRASTIVE = 2 };
+
 enum {
   HICGAT_OK = 0,
   HICGAT_EINVAL = -1,   /* bad size / null pointer / misaligned buffer */
@@ -264,8 +267,13 @@ int hicgat_pairdist_bwd(const float *coords, const float *G, int N, int64_t ldg,
  *     9 alpha = min(1, 0.1 + 1/(mse + 1e-6)), 10 total = mse + alpha*(1 - r), 11 reserved;
  *   loss_kind 0 (the MSE of HiC-GNN_main.py) forms moments 0 and 6 only: 1..5 are 0, r (8) is NaN
  *     and 9..10 are not meaningful; loss_kind 1 (combined loss) forms all of them;
- *   loss[1] (float32): mse (loss_kind 0) or total (loss_kind 1);
- *   dcoords [N,3] = d(mse)/dcoords restricted to the tile range (sum over ranks = full gradient).
+ *   loss_kind 2 (HICGAT_LOSS_CONTRASTIVE, train_and_test_same_res_GAT_node2vec.py:107-134:
+ *     0.1 * mean_{i<j} |T_ij - D_ij|) forms moment 0 = sum_{i<j} |d - t| only (6 = 0: no diagonal
+ *     term); finalized: 7 = mean |d - t| (fp64), 8 = NaN, 9 = 0.1, 10 = total = 0.1 * [7];
+ *   loss[1] (float32): mse (loss_kind 0), total (loss_kind 1) or fp32(total) (loss_kind 2);
+ *   dcoords [N,3] = d(loss)/dcoords restricted to the tile range (sum over ranks = full gradient):
+ *     d(mse) (loss_kind 0, 1: the Pearson term carries no gradient in the reference) or
+ *     float32(0.1 / M) * sum_j sign(d_ij - t_ij) (c_i - c_j) / d_ij, sign(0) = 0 (loss_kind 2).
  * workspace: hicgat_pairdist_workspace_bytes(N, HICGAT_PD_TRI). */
 int hicgat_pairdist_mse_fused(const float *coords, const float *T, int N, int64_t ldt,
                               int64_t tile_begin, int64_t tile_end, int loss_kind, double *stats,
@@ -570,6 +578,14 @@ int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, f
 /* A step's first launch: grad[0, n) = 0 (zero_grad, HiC-GNN_main.py:124) and, with step_counter
  * (NULL: none), *step_counter += 1 (the step's Adam then uses counted = 1).  grad 16-B aligned. */
 int hicgat_step_begin(float *grad, int64_t n, int64_t *step_counter, hicgat_stream_t stream);
+
+/* ---- measurement infrastructure (no reference counterpart) ----------------------------------
+ * An emulated collective for the simulated P-rank step (bench.py --simulate-world,
+ * hicgat.dist.SimComm): `workgroups` x `threads` threads resident on the device for `us`
+ * microseconds of wall time, enqueued where the RCCL call would be, so the captured rank step
+ * shows the modeled collective's duration, its overlap with the kernels on other streams and the
+ * CU slots it holds.  Not used by the training path. */
+int hicgat_sim_collective(float us, int workgroups, int threads, hicgat_stream_t stream);
 #ifdef __cplusplus
 }
 #endif

@@ -5,6 +5,9 @@
 * ``combined_loss``       -- ``HiC_GAT_generalize_directly.py:206-225``: MSE + alpha*(1 - r), r the
                              float64 Pearson of the upper-triangle distances, *no gradient* through
                              r, alpha = min(1, 0.1 + 1/(mse + 1e-6)).
+* ``contrastive_loss``    -- ``train_and_test_same_res_GAT_node2vec.py:107-134``: 0.1 * mean over the
+                             upper triangle (offset 1) of |truth - cdist(coords)|, truth float64, so
+                             the difference and the mean are float64; differentiable (no MSE term).
 * ``train``               -- ``HiC-GNN_main.py:117-132`` loop (Adam lr 1e-3, |dloss| <= thresh stop),
                              with an optional fixed step count.
 * ``dscc``                -- ``HiC-GNN_main.py:135-139``: Spearman of the triu distances.
@@ -35,6 +38,20 @@ def combined_loss(out, coords, truth):
     return mse + alpha * (1 - r), mse, r, alpha
 
 
+def contrastive_loss(coords, truth):
+    """``train_and_test_same_res_GAT_node2vec.py:107-134``: ``idx = triu_indices(n, n, offset=1)``;
+    ``dist_truth = truth[idx]`` (float64), ``dist_out = cdist(coords, coords)[idx]`` (float32);
+    ``0.0 + 0.1 * mean(abs(dist_truth - dist_out))`` -- float64, its gradient cast back to float32 at
+    ``dist_out``.  cdist in ``gat.CDIST_MODE`` (the reference's default mode; tests against the
+    exact-distance kernels switch it, as for the MSE)."""
+    from . import gat
+    n = truth.shape[0]
+    idx = torch.triu_indices(n, n, offset=1)
+    dist_truth = truth[idx[0], idx[1]].to(torch.float64)
+    dist_out = torch.cdist(coords, coords, p=2, compute_mode=gat.CDIST_MODE)[idx[0], idx[1]]
+    return 0.0 + 0.1 * torch.mean(torch.abs(dist_truth - dist_out))
+
+
 def dscc(coords, truth):
     """``HiC-GNN_main.py:135-139``: Spearman(truth triu, cdist(coords) triu)."""
     n = truth.shape[0]
@@ -57,6 +74,8 @@ def train(model, x, adj, truth, lr=1e-3, thresh=1e-8, steps=None, loss="mse", ma
         if loss == "mse":
             out = model(x, adj)
             val = mse_loss(out, truth)
+        elif loss == "contrastive":
+            val = contrastive_loss(model.get_model(x, adj), truth)
         else:
             coords = model.get_model(x, adj)
             out = torch.cdist(coords, coords, p=2)

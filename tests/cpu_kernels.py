@@ -22,6 +22,11 @@ def _rows(rowptr, r0, r1):
     return row, col_idx
 
 
+def _scale(n, kind):
+    """The per-pair gradient factor of hicgat's loss reduction (pairdist.hip loss_scale)."""
+    return float(np.float32(0.1 / (n * (n - 1) / 2))) if kind == 2 else 4.0 / (n * n)
+
+
 def _tri(I, J, nb):
     return I * nb - I * (I - 1) // 2 + (J - I)
 
@@ -326,7 +331,7 @@ class CpuKernels:
         d = diff.norm(dim=1)
         t = Tb[ii - row0, jj - col0]
         r = d - t
-        stats[0] = (r * r).sum()
+        stats[0] = r.abs().sum() if kind == 2 else (r * r).sum()
         stats[1] = d.sum()
         stats[2] = (d * d).sum()
         stats[3] = (d * t).sum()
@@ -335,8 +340,8 @@ class CpuKernels:
         dii = torch.arange(n)
         dtile = _tri(dii // BT, dii // BT, nb)
         dkeep = (dtile >= t0) & (dtile < t1)
-        stats[6] = (Tb[dii[dkeep] - row0, dii[dkeep] - col0] ** 2).sum()
-        w = torch.where(d > 0, r / d, torch.zeros_like(d)) * (4.0 / (n * n))
+        stats[6] = (Tb[dii[dkeep] - row0, dii[dkeep] - col0] ** 2).sum() if kind != 2 else 0.0
+        w = torch.where(d > 0, (torch.sign(r) if kind == 2 else r) / d, torch.zeros_like(d)) * _scale(n, kind)
         g = torch.zeros((n, 3), dtype=torch.float64)
         g.index_add_(0, ii, w.unsqueeze(1) * diff)
         g.index_add_(0, jj, -w.unsqueeze(1) * diff)
@@ -358,14 +363,14 @@ class CpuKernels:
         d = diff.norm(dim=1)
         r = d - bg
         m = torch.zeros(7, dtype=torch.float64)
-        m[0] = (r * r).sum()
+        m[0] = r.abs().sum() if kind == 2 else (r * r).sum()
         m[1] = d.sum()
         m[2] = (d * d).sum()
         m[3] = (d * bg).sum()
         m[4] = bg * d.numel()
         m[5] = bg * bg * d.numel()
         g = torch.zeros((n, 3), dtype=torch.float64)
-        w = torch.where(d > 0, r / d, torch.zeros_like(d))
+        w = torch.where(d > 0, (torch.sign(r) if kind == 2 else r) / d, torch.zeros_like(d))
         g.index_add_(0, ii, w.unsqueeze(1) * diff)
         g.index_add_(0, jj, -w.unsqueeze(1) * diff)
         rp = sf.rowptr.long()
@@ -374,16 +379,20 @@ class CpuKernels:
         t = sf.val_buf.double()[ei]
         sdiff = c[si] - c[sj]
         sd = sdiff.norm(dim=1)
-        g.index_add_(0, si, torch.where(sd > 0, (bg - t) / sd, torch.zeros_like(sd)).unsqueeze(1) * sdiff)
+        sw = torch.sign(sd - t) - torch.sign(sd - bg) if kind == 2 else bg - t
+        g.index_add_(0, si, torch.where(sd > 0, sw / sd, torch.zeros_like(sd)).unsqueeze(1) * sdiff)
         up = sj > si
         su, tu = sd[up], t[up]
-        m[0] += ((su - tu) ** 2 - (su - bg) ** 2).sum()
+        if kind == 2:
+            m[0] += ((su - tu).abs() - (su - bg).abs()).sum()
+        else:
+            m[0] += ((su - tu) ** 2 - (su - bg) ** 2).sum()
         m[3] += (su * (tu - bg)).sum()
         m[4] += (tu - bg).sum()
         m[5] += (tu * tu - bg * bg).sum()
-        m[6] = (sf.diag.double()[s0:s1] ** 2).sum()
+        m[6] = (sf.diag.double()[s0:s1] ** 2).sum() if kind != 2 else 0.0
         stats[:7] = m
-        gf = (g * (4.0 / (n * n))).float()
+        gf = (g * _scale(n, kind)).float()
         dcoords.copy_(gf.to(dcoords.dtype).view_as(dcoords))
         self.loss_finalize(n, kind, stats, loss)
 
@@ -391,8 +400,13 @@ class CpuKernels:
         if dc64 is not None:
             dcoords[r0:r1].copy_(dc64[r0:r1])
         s = stats.double()
-        mse = (2 * float(s[0]) + float(s[6])) / (n * n)
         M = n * (n - 1) / 2
+        if kind == 2:        # contrastive: 0.1 * mean_{i<j} |t - d| (fp64)
+            mae = float(s[0]) / M
+            stats[7], stats[8], stats[9], stats[10] = mae, float("nan"), 0.1, 0.1 * mae
+            loss.fill_(0.1 * mae)
+            return
+        mse = (2 * float(s[0]) + float(s[6])) / (n * n)
         cov = float(s[3]) - float(s[1]) * float(s[4]) / M
         vd = float(s[2]) - float(s[1]) ** 2 / M
         vt = float(s[5]) - float(s[4]) ** 2 / M

@@ -30,6 +30,16 @@ def test_bench_gpus2_self_launches_two_ranks():
     rows, nnz = res["shard"]["rows_per_rank"], res["shard"]["nnz_per_rank"]
     assert sum(rows) == 400 and abs(nnz[0] - nnz[1]) <= 0.02 * sum(nnz)
     assert res["value"] > 0 and res["final_loss"] == res["final_loss"]
+    # every collective of the step timed in the eager pass, with its modeled time beside it
+    col = res["collectives"]
+    assert col["world_size"] == 2 and col["process_group_size"] == 2 and col["ranks_counted_by_all_reduce"] == 2
+    assert col["backend"] == "gloo"
+    names = {"coords_all_gather", "loss_all_reduce", "grad_all_reduce_gat_bucket", "grad_all_reduce_tail_bucket"}
+    assert names <= set(col["measured_us"]), col["measured_us"].keys()
+    for k, v in col["measured_us"].items():
+        assert v["calls"] == 2 and v["avg_us"] > 0 and v["min_us"] <= v["avg_us"], (k, v)
+        assert v["kind"] in ("all_gather", "all_reduce") and v["bytes"] > 0, (k, v)
+        assert col["modeled_us"][k] > 0, k
 
 
 @pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") not in (None, ""), reason="GPU box")

@@ -110,13 +110,13 @@ def _close(a, b, stats_rtol=1e-9, loss_rtol=1e-6, grad_rtol=1e-5):
     Shards of the same form share the forward bit for bit up to the coordinates (stats to 1e-9);
     the aggregate-first form rounds the GATConv output differently (fp32: the north star's 1e-5)."""
     assert abs(b["losses"][0] - a["losses"][0]) <= loss_rtol * abs(a["losses"][0])
-    assert torch.allclose(b["stats"][:9], a["stats"][:9], rtol=stats_rtol)
+    assert torch.allclose(b["stats"][:9], a["stats"][:9], rtol=stats_rtol, equal_nan=True)
     g1, g2 = a["grad1"], b["grad1"]
     assert (g2 - g1).abs().max().item() <= grad_rtol * g1.abs().max().item()
     np.testing.assert_allclose(b["losses"], a["losses"], rtol=1e-3)
 
 
-@pytest.mark.parametrize("kind", ["mse", "combined"])
+@pytest.mark.parametrize("kind", ["mse", "combined", "contrastive"])
 def test_sharded_step_equals_single_rank(tmp_path, kind):
     one = _run(1, 300, kind, tmp_path)
     two = _run(2, 300, kind, tmp_path)
@@ -164,10 +164,12 @@ def test_auto_form_at_four_and_eight_ranks_equals_single_rank(tmp_path, world):
     assert int(held[:, 5].sum()) == int(full[5])     # (the xagg form has no slab structure: column 4 is -1)
 
 
-def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
+@pytest.mark.parametrize("kind", ["mse", "contrastive"])
+def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path, kind):
     """The manual backward of ShardedTrainer (CpuKernels, P = 1) vs the oracle model trained by
-    autograd + torch Adam with exact distances: same losses, same parameters."""
-    one = _run(1, 300, "mse", tmp_path)
+    autograd + torch Adam with exact distances: same losses, same parameters.  "contrastive": the
+    f5 loss (train_and_test_same_res_GAT_node2vec.py:107-134) through the background + support form."""
+    one = _run(1, 300, kind, tmp_path)
     hicgat, adj, truth, x = _setup(300)
     from oracle import gat as og
     from oracle import loop as ol
@@ -176,7 +178,7 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
         torch.manual_seed(0)
         ref = og.GATNetSelectiveResidualsUpdated()
         radj = (adj.storage.rowptr(), adj.storage.col())
-        hist = ol.train(ref, x, radj, truth.dense().double(), steps=STEPS)
+        hist = ol.train(ref, x, radj, truth.dense().double(), steps=STEPS, loss=kind)
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
     assert abs(one["losses"][0] - hist[0]) <= 1e-6 * hist[0]
@@ -187,7 +189,10 @@ def test_single_rank_sharded_step_equals_autograd_oracle(tmp_path):
     try:
         torch.manual_seed(0)
         ref = og.GATNetSelectiveResidualsUpdated()
-        ol.mse_loss(ref(x, radj), truth.dense().double()).backward()
+        if kind == "contrastive":
+            ol.contrastive_loss(ref.get_model(x, radj), truth.dense().double()).backward()
+        else:
+            ol.mse_loss(ref(x, radj), truth.dense().double()).backward()
     finally:
         og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
     model = hicgat.GATNetSelectiveResidualsUpdated()

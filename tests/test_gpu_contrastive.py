@@ -1,0 +1,308 @@
+"""GPU: the differentiable contrastive loss on the fused pairdist kernel.
+
+Reference: ``train_and_test_same_res_GAT_node2vec.py:98-134`` -- the flagship
+GATNetSelectiveResidualsUpdated trained on ``0.0 + 0.1 * mean(|truth[triu] - cdist(coords)[triu]|)``
+(``idx = triu_indices(n, n, offset=1)``), truth = ``cont2dist(y, conversion = 1)`` in float64, so the
+difference and the mean are float64; there is no MSE term in the loss that is optimised.  The
+oracle restatement is ``oracle.loop.contrastive_loss`` (pinned to the reference formula in
+tests/test_contrastive_host.py).
+
+Tolerances: the loss to 1e-6 relative (its fp64 value, stats[10]); coordinate gradients to 1e-5 of
+their max PLUS, per row, 2 x scale for every pair of that row whose |d - t| is within 1e-6 of the
+distance (d |r| / dr = sign(r) is decided by rounding there: the kernel's 1-2 ulp distance or the
+truth's fp32 storage can put such a pair on the other side, and its whole +-scale term flips); model
+gradients 2e-4 of each tensor's max (fp32 reassociation), as for the MSE.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import hicgat  # noqa: F401  (fails loudly if libhicgat.so is missing)
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def _exact():
+    from oracle import gat as og
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+
+
+def _mm():
+    from oracle import gat as og
+    og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+
+
+def _oracle_loss_grad(c, truth64):
+    """oracle.loop.contrastive_loss (exact cdist) and its autograd gradient w.r.t. the fp32 coords."""
+    from oracle import loop as ol
+    cr = c.detach().cpu().float().clone().requires_grad_(True)
+    _exact()
+    try:
+        lr = ol.contrastive_loss(cr, truth64.cpu().double())
+        lr.backward()
+    finally:
+        _mm()
+    return float(lr), cr.grad
+
+
+def _flip_allowance(c, truth64, scale, rel=1e-6):
+    """Per row: 2 x scale x (pairs of the row whose sign(d - t) rounding can decide), float64."""
+    cd = c.detach().double().to(DEV)
+    t = truth64.to(DEV).double()
+    d = torch.cdist(cd, cd, compute_mode="donot_use_mm_for_euclid_dist")
+    near = (d - t).abs() <= rel * torch.maximum(d, t.abs())
+    near.fill_diagonal_(False)
+    return (2.0 * scale * near.sum(1).double()).cpu(), int(near.sum()) // 2
+
+
+def _check_dcoords(g_dev, g_ref, allow, label):
+    g_dev, g_ref = g_dev.double().cpu(), g_ref.double().cpu()
+    excess = ((g_dev - g_ref).abs() - allow[:, None]).clamp_min(0.0)
+    worst = float(excess.max()) / max(float(g_ref.abs().max()), 1e-30)
+    assert worst <= 1e-5, (label, worst)
+    return worst
+
+
+@pytest.mark.parametrize("n,form", [(2, "dense"), (3, "dense"), (58, "dense"), (129, "dense"), (400, "dense"),
+                                    (1000, "dense"), (58, "support"), (129, "support"), (400, "support"),
+                                    (1000, "support")])
+def test_fused_contrastive_loss_matches_oracle(n, form):
+    """loss_kind 2 of the fused kernel against the oracle on random coordinates: "dense" -- a
+    random symmetric truth (the T-image tile path); "support" -- cont2dist(y, 1) of a sparse contact
+    map, whose background (1.0 off the contact set) the tile pass assumes while the support pass
+    adds the contacts (the form the training step runs)."""
+    import hicgat
+    rng = np.random.default_rng(n)
+    if form == "dense":
+        t = rng.random((n, n))
+        t = (t + t.T) / 2
+        np.fill_diagonal(t, 0)
+        truth64 = torch.tensor(t, dtype=torch.float64)
+        tr = hicgat.Truth(truth64.to(DEV))
+    else:
+        from oracle import graph as ogr
+        a = (rng.random((n, n)) < 0.05) * rng.integers(1, 50, (n, n)).astype(np.float64)
+        a = np.triu(a, 1)
+        a = a + a.T
+        truth64 = ogr.cont2dist(torch.tensor(a), 1)
+        tr = hicgat.Truth.from_contacts(torch.tensor(a, device=DEV), 1)
+        assert tr.support is not None
+    c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32))
+    l_ref, g_ref = _oracle_loss_grad(c, truth64)
+    cm = c.to(DEV).requires_grad_(True)
+    lm, stats = hicgat.ops.fused_dist_loss(cm, tr, "contrastive")
+    lm.backward()
+    st = stats.cpu().numpy()
+    assert abs(st[10] - l_ref) <= 1e-6 * l_ref, (st[10], l_ref)
+    assert abs(st[7] - 10 * l_ref) <= 1e-6 * 10 * l_ref and np.isnan(st[8]) and st[9] == 0.1
+    assert abs(float(lm) - l_ref) <= 1e-6 * l_ref
+    M = n * (n - 1) / 2
+    scale = float(np.float32(0.1 / M))
+    allow, flips = _flip_allowance(c, truth64, scale)
+    w = _check_dcoords(cm.grad, g_ref, allow, f"{form} n={n}")
+    print(f"{form} n={n}: loss {st[10]:.10g} vs {l_ref:.10g}; dcoords excess {w:.1e} ({flips} near-tie pairs)")
+    # translation invariance: the gradient sums to 0
+    assert float(cm.grad.sum(0).abs().max()) <= 1e-5 * max(float(cm.grad.abs().max()), 1e-30) * n
+
+
+def test_contrastive_tile_ranges_and_support_rows_sum_to_whole():
+    """The multi-GPU contract for loss_kind 2: disjoint bulk-tile ranges + support-row blocks (what
+    each rank of hicgat.dist computes) add up to the whole call."""
+    import hicgat
+    from hicgat import _lib
+    n = 900
+    rng = np.random.default_rng(1)
+    a = (rng.random((n, n)) < 0.03) * rng.integers(1, 50, (n, n)).astype(np.float64)
+    a = np.triu(a, 1)
+    a = a + a.T
+    tr = hicgat.Truth.from_contacts(torch.tensor(a, device=DEV), 1)
+    sf = tr.support
+    K = hicgat.kernels.default()
+    c = torch.tensor(rng.standard_normal((n, 3)).astype(np.float32), device=DEV)
+    tiles = _lib.load().hicgat_pairdist_num_tiles(n, 1)
+
+    def part(t0, t1, s0, s1):
+        stats = torch.zeros(12, dtype=torch.float64, device=DEV)
+        loss = torch.zeros((), dtype=torch.float32, device=DEV)
+        dc = torch.zeros((n, 3), dtype=torch.float64, device=DEV)
+        K.fused_loss_support_range(c, sf, n, 2, t0, t1, s0, s1, stats, loss, dc)
+        return stats[:7].cpu(), dc.cpu()
+
+    whole_s, whole_g = part(0, tiles, 0, n)
+    acc_s, acc_g = torch.zeros(7, dtype=torch.float64), torch.zeros((n, 3), dtype=torch.float64)
+    for (t0, t1), (s0, s1) in zip([(0, tiles // 3), (tiles // 3, tiles // 2), (tiles // 2, tiles)],
+                                  [(0, 200), (200, 201), (201, n)]):
+        s, g = part(t0, t1, s0, s1)
+        acc_s += s
+        acc_g += g
+    assert torch.allclose(acc_s, whole_s, rtol=1e-12)
+    assert _rel(acc_g, whole_g) < 1e-6
+
+
+@pytest.mark.timeout(600)
+def test_contrastive_synth2000_training_step_matches_oracle():
+    """One full training step with the contrastive loss (forward + loss + backward + Adam) of the
+    flagship on the dense synth-2000 graph (BASELINE configs[1], 4.0 M edges) against the CPU oracle
+    from the same seed, truth = cont2dist(y, 1) as in the reference script: the fp64 loss 1e-5,
+    coordinates 1e-5, every gradient 2e-4 of its max, the Adam update where it is not
+    rounding-sensitive."""
+    import hicgat
+    from hicgat import synth
+    from oracle import gat as og
+    from oracle import graph as ogr
+    from oracle import loop as ol
+    n = 2000
+    i, j, cc = synth.contact_pairs(n, density=None, seed=0)
+    A = synth.dense_contacts(n, i, j, cc, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 1)
+    x = synth.features(n, seed=0)
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+    loss, stats, coords = hicgat.train.train_step(model, opt, torch.tensor(x, device=DEV), adj, tr, "contrastive")
+    torch.cuda.synchronize()
+    l_dev = float(stats[10])
+    grads = {k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()}
+    params = {k: p.detach().cpu().clone() for k, p in model.named_parameters()}
+
+    d = ogr.load_input(A.cpu().numpy(), x)
+    t_ref = ogr.cont2dist(d["y"], 1)
+    torch.manual_seed(0)
+    ref = og.GATNetSelectiveResidualsUpdated()
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    _exact()
+    try:
+        radj = (torch.tensor(d["rowptr"]), torch.tensor(d["col"]))
+        c_ref = ref.get_model(d["x"], radj)
+        l_ref = ol.contrastive_loss(c_ref, t_ref)
+        l_ref.backward()
+    finally:
+        _mm()
+    rel_l = abs(l_dev - l_ref.item()) / l_ref.item()
+    rel_c = _rel(coords.detach().cpu(), c_ref.detach())
+    print(f"contrastive loss {l_dev:.10g} vs oracle {l_ref.item():.10g} (rel {rel_l:.2e}); coords rel {rel_c:.2e}")
+    assert l_ref.dtype == torch.float64
+    assert rel_l < 1e-5 and rel_c < 1e-5
+    gscale = max(p.grad.abs().max().item() for p in ref.parameters())
+    worst = {}
+    for k, pr in ref.named_parameters():
+        if pr.grad.abs().max().item() < 1e-3 * gscale:
+            assert grads[k].abs().max().item() < 1e-3 * gscale, k
+            continue
+        worst[k] = _rel(grads[k], pr.grad)
+    print("grad max |err| / max |ref|:", {k: f"{v:.1e}" for k, v in worst.items()})
+    assert max(worst.values()) < 2e-4, worst
+    ropt.step()
+    for k, pr in ref.named_parameters():
+        g_ref = pr.grad
+        sig = (g_ref.abs() > 1e-3 * g_ref.abs().max()) & (g_ref.abs() > 1e-6)
+        if sig.any():
+            assert float((params[k] - pr.detach()).abs()[sig].max()) < 1e-6, k
+
+
+def _oracle_states(ref, x, radj, truth, K):
+    """The oracle contrastive loop (torch Adam lr 1e-3), 1 thread: the parameters before every step,
+    the step's fp64 loss and its gradients."""
+    from oracle import loop as ol
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    out = []
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        for _ in range(K):
+            opt.zero_grad()
+            state = {k: p.detach().clone() for k, p in ref.named_parameters()}
+            val = ol.contrastive_loss(ref.get_model(x, radj), truth)
+            val.backward()
+            out.append((state, float(val.item()), {k: p.grad.detach().clone() for k, p in ref.named_parameters()}))
+            opt.step()
+    finally:
+        torch.set_num_threads(threads)
+    return out
+
+
+def test_contrastive_train_loop_tracks_oracle():
+    """The contrastive training loop on chr19 1 mb (cont2dist(y, 1), the reference's conversion),
+    fixed K = 25 (hicgat.train.train(loss="contrastive")) against the oracle loop: teacher-forced
+    from every state the oracle visits (loss 1e-5, gradients 2e-4 of their max), and free-running
+    steps 1-2 to 1e-5 with the rest inside 2x the oracle's own 1/2/4/8-thread spread (two steps of
+    lookahead, as for the MSE loop)."""
+    import hicgat
+    from oracle import gat as og
+    from oracle import loop as ol
+    from conftest import load_golden
+    mfx = load_golden("model_GATNetSelectiveResidualsUpdated.npz")
+    g = load_golden("graph_chr19_1mb.npz")
+    K = 25
+    x_h, truth_h = torch.tensor(mfx["x"]), torch.tensor(g["truth1"], dtype=torch.float64)
+    radj = (torch.tensor(g["rowptr"]), torch.tensor(g["col"]))
+    _exact()
+    try:
+        hist = {}
+        threads = torch.get_num_threads()
+        try:
+            for th in (1, 2, 4, 8):
+                torch.set_num_threads(th)
+                torch.manual_seed(0)
+                hist[th] = np.array(ol.train(og.GATNetSelectiveResidualsUpdated(), x_h, radj, truth_h, steps=K,
+                                             loss="contrastive"))
+        finally:
+            torch.set_num_threads(threads)
+        ref_hist = hist[1]
+        spread = np.max([np.abs(h - ref_hist) / ref_hist for h in hist.values()], axis=0)
+        torch.manual_seed(0)
+        states = _oracle_states(og.GATNetSelectiveResidualsUpdated(), x_h, radj, truth_h, K)
+    finally:
+        _mm()
+    assert np.array_equal([s[1] for s in states], ref_hist)
+    y = torch.tensor(g["matrix"], device=DEV)
+    y.fill_diagonal_(0)
+    data = hicgat.Data(x=torch.tensor(mfx["x"], device=DEV), edge_index=hicgat.Adj.from_dense_device(y), y=y)
+    tr = hicgat.Truth.from_contacts(y, 1)
+    assert torch.equal(tr.dense().cpu(), truth_h.float())
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    _, dev_hist = hicgat.train.train(model, data, tr, steps=K, loss="contrastive")
+    rel = np.abs(np.array(dev_hist) - ref_hist) / ref_hist
+    # teacher forcing
+    opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+    params = dict(model.named_parameters())
+    wl = wg = 0.0
+    for state, l_ref, g_ref in states:
+        with torch.no_grad():
+            for k, v in state.items():
+                params[k].copy_(v)
+        opt.zero_grad()
+        val, st, _ = model.loss(data.x, data.edge_index, tr, "contrastive")
+        val.backward()
+        wl = max(wl, abs(float(st[10]) - l_ref) / l_ref)
+        gscale = max(float(v.abs().max()) for v in g_ref.values())
+        for k, gr in g_ref.items():
+            gd = params[k].grad.detach().cpu()
+            if float(gr.abs().max()) < 1e-3 * gscale:
+                assert float(gd.abs().max()) < 1e-3 * gscale, k
+                continue
+            wg = max(wg, _rel(gd, gr))
+    np.set_printoptions(precision=2, linewidth=200)
+    print(f"teacher-forced over {K} states: loss rel {wl:.2e}, grad rel {wg:.2e}")
+    print("free-running rel", rel)
+    print("oracle spread   ", spread)
+    assert wl < 1e-5 and wg < 2e-4, (wl, wg)
+    assert rel[0] < 1e-5 and rel[1] < 1e-5, rel[:3]
+    run_rel, run_spread = np.maximum.accumulate(rel), np.maximum.accumulate(spread)
+    ahead = run_spread[np.minimum(np.arange(len(spread)) + 2, len(spread) - 1)]
+    assert np.all(run_rel <= 2 * ahead + 1e-4), (rel, spread)

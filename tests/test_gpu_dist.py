@@ -50,24 +50,32 @@ def _single_gpu_steps(n, steps=2):
     """The single-GPU flagship step (hicgat.train.train_step, seed-0 weights) on the same inputs:
     (losses, gradients after step 1, flat parameters after step 1, the model, the optimizer, the
     kink masks of step 1 -- tests/kinks.py, from the GATConv pre-relu output of the step-1 weights)."""
-    from kinks import kink_masks
     hicgat, adj, truth, x = _inputs(n, "cuda")
     torch.manual_seed(0)
     model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
     opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)   # the trainer's flat layout
+    masks, counts, bounds = _kink_info(hicgat, model, x, adj, truth)
+    losses, g1, p1, c1 = [], None, None, None
+    for k in range(steps):
+        loss, _, coords = hicgat.train.train_step(model, opt, x, adj, truth)
+        losses.append(float(loss))
+        if k == 0:
+            g1, p1, c1 = opt.grad.clone(), opt.flat.clone(), coords.detach().clone()
+    return dict(loss=losses, grad1=g1, flat1=p1, coords1=c1, model=model, opt=opt, masks=masks, kinks=counts,
+                bounds=bounds, inputs=(x, adj, truth))
+
+
+def _kink_info(hicgat, model, x, adj, truth):
+    """tests/kinks.py's masks and flipped-term bounds of the step at the model's current weights."""
+    from kinks import kink_bounds
     c = model.conv
     with torch.no_grad():
         out_pre = hicgat.ops.gat_conv(x, c.lin_l.weight, c.att_l, c.att_r, c.bias, adj)
-    masks, counts = kink_masks(model, out_pre)
-    del out_pre
-    losses, g1, p1 = [], None, None
-    for k in range(steps):
-        loss, _, _ = hicgat.train.train_step(model, opt, x, adj, truth)
-        losses.append(float(loss))
-        if k == 0:
-            g1, p1 = opt.grad.clone(), opt.flat.clone()
-    return dict(loss=losses, grad1=g1, flat1=p1, model=model, opt=opt, masks=masks, kinks=counts,
-                inputs=(x, adj, truth))
+        coords = model.get_model(x, adj)
+    cd = coords.detach().requires_grad_(True)
+    loss, _ = hicgat.ops.fused_dist_loss(cd, truth)
+    loss.backward()
+    return kink_bounds(model, out_pre, cd.grad, x, adj.rowptr32, adj.col32)
 
 
 def _loss_at(ref, flat):
@@ -95,10 +103,13 @@ def _assert_step_matches(ref, res, loss_tol=1e-5, grad_tol=1e-4, label=""):
     from kinks import compare_flat
     model, opt, masks = ref["model"], ref["opt"], ref["masks"]
     g_ref, g = ref["grad1"], res["grad1"].to(ref["grad1"].device)
-    per = compare_flat(model, zip(opt.params, opt.offsets), g_ref, g, masks)
+    per = compare_flat(model, zip(opt.params, opt.offsets), g_ref, g, masks, bounds=ref["bounds"])
     print(label, f"loss {ref['loss']} vs {res['loss']}; kinks {ref['kinks']};",
           {k: f"{d:.1e}/{m:.1e} ({c} masked)" for k, (d, m, c) in per.items()})
     assert abs(res["loss"][0] - ref["loss"][0]) <= loss_tol * abs(ref["loss"][0]), (res["loss"], ref["loss"])
+    if "coords1" in res:     # step()'s coordinates: [N, 3] in global row order, the step-1 forward's
+        c_ref, c = ref["coords1"], res["coords1"].to(ref["coords1"].device)
+        assert c.shape == c_ref.shape and float((c - c_ref).abs().max()) <= 1e-5 * float(c_ref.abs().max())
     assert abs(res["loss"][1] - ref["loss"][1]) <= 1e-4 * abs(ref["loss"][1]), (res["loss"], ref["loss"])
     for name, (d, m, _) in per.items():
         assert d <= grad_tol * m, (label, name, d, m)
@@ -162,7 +173,7 @@ def test_sharded_rccl_graph_replay_equals_eager(tmp_path, mode):
     assert torch.equal(r["pe"], r["pg"])
 
 
-def _worker(rank, world, port, backend, n, out, mode="slab"):
+def _worker(rank, world, port, backend, n, out, mode="slab", big_group=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -174,10 +185,13 @@ def _worker(rank, world, port, backend, n, out, mode="slab"):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         hicgat, adj, truth, x = _inputs(n, dev)
+        if big_group is not None:
+            hicgat.ops.BIG_GROUP = big_group
         torch.manual_seed(0)
         model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
         tr = hicgat.dist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode=mode)
-        loss, stats, _ = tr.step()
+        loss, stats, coords = tr.step()
+        coords1 = coords.clone().cpu()
         grad1 = tr.opt.grad.clone().cpu()
         flat1 = tr.opt.flat.clone().cpu()
         stats = stats.clone()           # the trainer's stats buffer is reused by the next step
@@ -185,15 +199,15 @@ def _worker(rank, world, port, backend, n, out, mode="slab"):
         loss2, _, _ = tr.step()
         torch.cuda.synchronize()
         if rank == 0:
-            torch.save({"loss": [l1, float(loss2)], "grad1": grad1, "flat1": flat1, "stats": stats.cpu(),
+            torch.save({"loss": [l1, float(loss2)], "grad1": grad1, "flat1": flat1, "stats": stats.cpu(), "coords1": coords1,
                         "mode": tr.mode, "rows": [int(v) for v in tr.plan.counts]}, out)
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, backend, n, tmp_path, mode="slab"):
+def _run(world, backend, n, tmp_path, mode="slab", big_group=None):
     out = str(tmp_path / f"{backend}{world}{mode}.pt")
-    mp.spawn(_worker, args=(world, _port(), backend, n, out, mode), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _port(), backend, n, out, mode, big_group), nprocs=world, join=True)
     return torch.load(out, weights_only=True)
 
 
@@ -204,15 +218,18 @@ def _need_gpu():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode,n", [("slab", 777), ("xagg", 777), ("xagg", 3000), ("xagg", 20000)])
-def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode, n):
+@pytest.mark.parametrize("mode,n,big", [("slab", 777, None), ("slab", 777, 1.0), ("allgather", 777, 1.0),
+                                        ("xagg", 777, None), ("xagg", 3000, None), ("xagg", 20000, None)])
+def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode, n, big):
     """World 1 over RCCL vs the single-GPU step (two steps), compared kink-aware (tests/kinks.py):
     the aggregate-first form ("xagg": out = W (sum alpha x) + b, gat_xagg.hip) rounds the GATConv
     differently, so a relu input at rounding level from 0 may flip; those entries are masked and
     everything else must hold loss to the north star's 1e-5 and gradients to 1e-4 of their max.
     n = 777 is the size whose block-2 LN output at |z| = 6e-8 flipped in round 3; n = 20000 is the
-    synth-20000 workload (BASELINE configs[2])."""
-    res = _run(1, "nccl", n, tmp_path, mode)
+    synth-20000 workload (BASELINE configs[2]).  ``big`` = 1: ops.BIG_GROUP lowered so that EVERY
+    parameter-gradient job of the MLP tail qualifies for holding -- the sharded step must not hold
+    them (it has no GATConv backward to issue them before its gradient all-reduce's tail bucket)."""
+    res = _run(1, "nccl", n, tmp_path, mode, big)
     ref = _single_gpu_steps(n)
     slab = mode == "slab"      # the h-first order of the single-GPU step: tighter
     _assert_step_matches(ref, res, loss_tol=1e-6 if slab else 1e-5, grad_tol=1e-5 if slab else 1e-4, label=f"{mode} n={n}")
@@ -255,7 +272,7 @@ def test_sharded_ranks_equal_one_rank(tmp_path, world, mode, n):
 @pytest.mark.parametrize("mode,n,world", [("slab", 777, 3), ("xagg", 777, 3), ("xagg", 3000, 2)])
 def test_simulated_ranks_run_their_shares(mode, n, world):
     """bench.py --simulate-world: each rank's share of a sharded step runs captured on one GPU with
-    the collectives left out; the shards partition the edges, slabs, tiles and support rows.  n = 3000
+    each collective emulated on its stream (hicgat_sim_collective); the shards partition the edges, slabs, tiles and support rows.  n = 3000
     over 2 ranks puts 1 500 rows on a rank: the one-kernel tail forward / backward (ops.fused_tail)
     inside the captured sharded step."""
     from hicgat import ops
@@ -314,14 +331,12 @@ def test_world1_step_matches_float64_standin(mode, n):
         dist.destroy_process_group()
     (lg, gg, opt, model), (lc, gc, _, _) = res["cuda"], res["cpu"]
     # the float64 stand-in decides every relu exactly; the fp32 run may flip one at rounding level
-    from kinks import compare_flat, kink_masks
+    from kinks import compare_flat
     torch.manual_seed(0)
     m0 = cls().to("cuda")
-    c = m0.conv
-    with torch.no_grad():
-        out_pre = hicgat.ops.gat_conv(x, c.lin_l.weight, c.att_l, c.att_r, c.bias, adj)
-    masks, counts = kink_masks(m0, out_pre)
-    per = compare_flat(model, zip(opt.params, opt.offsets), gc, gg, {k: v.cpu() for k, v in masks.items()})
+    masks, counts, bounds = _kink_info(hicgat, m0, x, adj, truth)
+    per = compare_flat(model, zip(opt.params, opt.offsets), gc, gg, {k: v.cpu() for k, v in masks.items()},
+                       bounds={k: v.cpu() for k, v in bounds.items()})
     print(mode, f"loss {lg:.8e} vs {lc:.8e}; kinks {counts}", {k: f"{d:.1e}/{m:.1e} ({c})" for k, (d, m, c) in per.items()})
     assert abs(lg - lc) <= 1e-5 * abs(lc)
     for k, (d, m, _) in per.items():
@@ -369,3 +384,36 @@ def test_xagg_head_fused_tail_matches_separate_launches(n, world):
     assert abs(l1[0] - l0[0]) <= 1e-6 * abs(l0[0]), (l0, l1)
     assert (g1[0] - g0[0]).abs().max().item() <= 1e-5 * g0[0].abs().max().item()
     assert abs(l1[1] - l0[1]) <= 1e-4 * abs(l0[1]), (l0, l1)
+
+
+def test_sim_collective_holds_for_the_modeled_time():
+    """The emulated collective of SimComm (hicgat_sim_collective): resident for the requested wall
+    time on its stream (bench.py --simulate-world puts the modeled collective times into the captured
+    rank step through it), overlappable with work on another stream, and argument-checked."""
+    from hicgat import _lib
+    lib = _lib.lib()
+    dev = torch.device("cuda", 0)
+    for us in (15.0, 120.0):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.check(lib.hicgat_sim_collective(us, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e3
+        assert us <= t <= us + 40, (us, t)
+    # two 100 us emulations on two streams overlap (16 workgroups each: the chip has room for both)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    s1.wait_event(e0)
+    s2.wait_event(e0)
+    for s in (s1, s2):
+        with torch.cuda.stream(s):
+            _lib.check(lib.hicgat_sim_collective(100.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
+    torch.cuda.current_stream().wait_stream(s1)
+    torch.cuda.current_stream().wait_stream(s2)
+    e1.record()
+    torch.cuda.synchronize()
+    assert e0.elapsed_time(e1) * 1e3 < 170
+    for bad in ((-1.0, 16, 256), (10.0, 0, 256), (10.0, 16, 100), (10.0, 16, 2048)):
+        assert lib.hicgat_sim_collective(*bad, None) == -1, bad
