@@ -23,15 +23,11 @@
 
 #include "common.hpp"
 
-#ifndef HICGAT_BWD_U
 // neighbours gathered per inner step of agg_bwd_dst (2 float4 loads per lane each).  Measured on
 // MI355X at N = 20000 (tools/kbench.py): U = 8 -> 0.95 ms (118 VGPRs, 4 waves per SIMD); U = 4 ->
 // 0.52; U = 2 -> 0.47.  With per-edge reductions in the loop the gather wants waves, not ILP.
-#define HICGAT_BWD_U 2
-#endif
-#ifndef HICGAT_SRC_U
-#define HICGAT_SRC_U 4   // neighbours per inner step of the (reduction-free) source pass
-#endif
+constexpr int kBwdDstU = 2;
+constexpr int kBwdSrcU = 4;   // neighbours per inner step of the (reduction-free) source pass
 
 namespace hicgat {
 
@@ -47,7 +43,7 @@ __global__ __launch_bounds__(256) void agg_bwd_dst_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ dout, float ns, float *__restrict__ row_stats) {
-  constexpr int U = HICGAT_BWD_U;
+  constexpr int U = kBwdDstU;
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (i >= row_end) return;
@@ -154,7 +150,7 @@ __device__ __forceinline__ void agg_bwd_src_row(
     float *__restrict__ dh, float *__restrict__ da_src) {
   // ldq: dout row stride in float4, ldr: row_stats row stride in floats (both multiples of 4, so
   // a multi-GPU caller can all-gather [dout | row stats] rows as one packed buffer)
-  constexpr int U = HICGAT_SRC_U;
+  constexpr int U = kBwdSrcU;
   const int lane = lane_id();
   const int beg = rowptr[r], end = rowptr[r + 1];
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
@@ -281,10 +277,8 @@ __global__ __launch_bounds__(256) void agg_bwd_rows_kernel(int row_begin, int ro
 // (bitwise the all-parts call).
 // stage 1: block b sums rows [b*R, (b+1)*R) into part[b][P][D] (the P asked-for parts in order);
 // stage 2: one thread per output column sums the partials in block order.
-#ifndef HICGAT_PG_BLOCKS
-#define HICGAT_PG_BLOCKS 512    // 1024 measured slower (stage 2 sums twice the partials)
-#endif
-constexpr int kParamBlocks = HICGAT_PG_BLOCKS;   // row blocks of stage 1 (128 left half the CUs idle)
+// row blocks of stage 1 (128 left half the CUs idle; 1024 measured slower: stage 2 sums twice the partials)
+constexpr int kParamBlocks = 512;
 
 template <int PARTS>
 __global__ __launch_bounds__(256) void param_grad_stage1(const float *__restrict__ h,

@@ -11,9 +11,7 @@
 // (a rank's destination shard); every per-row array is indexed by the global row id.
 #include "common.hpp"
 
-#ifndef HICGAT_FWD_U
-#define HICGAT_FWD_U 8   // neighbours gathered per inner step
-#endif
+constexpr int kFwdU = 8;   // neighbours gathered per inner step
 
 namespace hicgat {
 
@@ -61,22 +59,19 @@ __global__ __launch_bounds__(256) void att_logits_kernel(const float *__restrict
 //   da_dst_i = sum_j alpha_ij lrelu'(e_ij) (<dout_i, h_j> - delta_i) = <dout_i, out2_i> - delta_i S3_i
 // (agg_bwd_rows_kernel, gat_bwd.hip).  ACT = 1 applies the relu that follows the GATConv in
 // GATNetSelectiveResidualsUpdated (models.py:637) in the epilogue: out = relu(acc + bias).
-#ifndef HICGAT_FWD_OCC
-#define HICGAT_FWD_OCC 1   // __launch_bounds__ min blocks per CU of the training form (A/B builds)
-#endif
 //
 // SPLIT (the tiled form, gat_tiles.hip): the softmax statistics still come from the whole row
 // (rowptr/col), but only the edges of the sparse remainder (rowptr_s/col_s) are gathered, and the
 // raw sums (no bias, no activation) go to out/out2 with S3 of those edges; the matrix-core pass over
 // the row's dense 32x32 tiles adds the rest and applies the epilogue.
 template <bool TRAIN, int ACT, bool SPLIT = false>
-__global__ __launch_bounds__(256, TRAIN ? HICGAT_FWD_OCC : 1) void agg_fwd_h2c256_kernel(
+__global__ __launch_bounds__(256, 1) void agg_fwd_h2c256_kernel(
     const int *__restrict__ rowptr, const int *__restrict__ col, int row_begin, int row_end,
     const float *__restrict__ h, const float *__restrict__ a_src, const float *__restrict__ a_dst,
     const float *__restrict__ bias, float ns, float *__restrict__ out, float *__restrict__ out2,
     float *__restrict__ row_stats, const int *__restrict__ rowptr_s = nullptr,
     const int *__restrict__ col_s = nullptr) {
-  constexpr int U = HICGAT_FWD_U;  // neighbours in flight per lane
+  constexpr int U = kFwdU;  // neighbours in flight per lane
   const int lane = lane_id();
   const int i = row_begin + xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_in_block();
   if (i >= row_end) return;

@@ -20,10 +20,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int GBM = 64, GBN = 256, GBK = 16;
 constexpr int APAD = GBM + 4, BPAD = GBN + 4;
 
-#ifndef HICGAT_LIN_OCC
-#define HICGAT_LIN_OCC 1   // __launch_bounds__ min blocks per CU (A/B builds)
-#endif
-__global__ __launch_bounds__(256, HICGAT_LIN_OCC) void linear_att_kernel(const float *__restrict__ x,
+__global__ __launch_bounds__(256, 1) void linear_att_kernel(const float *__restrict__ x,
                                                          const float *__restrict__ W, int M, int K,
                                                          int Nc, int C, const float *__restrict__ att_s,
                                                          const float *__restrict__ att_d,

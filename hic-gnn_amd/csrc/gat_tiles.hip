@@ -44,25 +44,17 @@ __device__ __forceinline__ float f4_c(const float4 &v, int t) { return t == 0 ? 
 // row of accumulator element r (C/D layout of a 32x32 f32 tile: col = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int lk) { return (r & 3) + 8 * (r >> 2) + 4 * lk; }
 
-#ifndef HICGAT_BAND_KB
-#define HICGAT_BAND_KB 8    // k-pairs of neighbour rows loaded per batch (two batches per 32-column tile)
-#endif
-constexpr int KB = HICGAT_BAND_KB;
-#ifndef HICGAT_BAND_KBB
-#define HICGAT_BAND_KBB 4   // the same for the backward (four more per-column constants live)
-#endif
-constexpr int KBB = HICGAT_BAND_KBB;
+constexpr int KB = 8;    // k-pairs of neighbour rows loaded per batch (two batches per 32-column tile)
+constexpr int KBB = 4;   // the same for the backward (four more per-column constants live)
 static_assert(16 % KB == 0 && 16 % KBB == 0, "KB / KBB must divide 16");
 
-#ifndef HICGAT_BAND_OCC
-#define HICGAT_BAND_OCC 2   // min workgroups per CU (accumulators + one tile of B operands fit 2 waves/SIMD)
-#endif
+constexpr int kBandOcc = 2;   // min workgroups per CU (accumulators + one tile of B operands fit 2 waves/SIMD)
 
 // ---- forward: out_i += sum over the block's dense tiles of alpha_ij h_j (and out2 with alpha lrelu'),
 // then the epilogue (bias, relu) for every row of the block.  out/out2 hold the gather kernel's raw
 // sums on entry; row_stats holds (max, sum) over the whole row and S3 of the remainder.
 template <bool TRAIN, int ACT>
-__global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
+__global__ __launch_bounds__(256, kBandOcc) void band_fwd_kernel(
     const int *__restrict__ tptr, const int *__restrict__ tcol, const uint32_t *__restrict__ tmask, int row_begin,
     int row_end, int ncols, const float *__restrict__ h, const float *__restrict__ a_src,
     const float *__restrict__ a_dst, const float *__restrict__ bias, float ns, float *__restrict__ out,
@@ -183,7 +175,7 @@ __global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_fwd_kernel(
 //   dh_r     += da_src_r att_src + da_dst_r att_dst.
 // alpha_ir is the softmax weight of edge (i -> r) in destination row i's softmax, so the per-column
 // constants (a_dst_i, max_i, sum_i, delta_i) come from row_stats rows of the tile's columns.
-__global__ __launch_bounds__(256, HICGAT_BAND_OCC) void band_bwd_kernel(
+__global__ __launch_bounds__(256, kBandOcc) void band_bwd_kernel(
     const int *__restrict__ tptr, const int *__restrict__ tcol, const uint32_t *__restrict__ tmask, int row_begin,
     int row_end, int ncols, const float *__restrict__ h, const float *__restrict__ a_src,
     const float *__restrict__ a_dst, const float *__restrict__ row_stats, int64_t ldr, const float *__restrict__ dout,

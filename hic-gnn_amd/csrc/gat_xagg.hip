@@ -29,15 +29,8 @@
 //   xagg_param_finish   dW += att (x) g terms, datt_src / datt_dst = W_h g
 #include "common.hpp"
 
-#ifndef HICGAT_XAGG_U
-#define HICGAT_XAGG_U 4   // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
-#endif
-#ifndef HICGAT_XAGG_DXA_LDS
-#define HICGAT_XAGG_DXA_LDS 1   // edge pass: dxa operands read from LDS every pass (0: the compiler keeps them in VGPRs)
-#endif
-#ifndef HICGAT_XAGG_GL
-#define HICGAT_XAGG_GL 8   // edge pass: lanes per edge (16 float4 of x_j per lane in flight)
-#endif
+constexpr int kXaggU = 4;    // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
+constexpr int kXaggGL = 8;   // edge pass (slab form): lanes per edge (16 float4 of x_j per lane in flight)
 
 namespace hicgat {
 
@@ -105,7 +98,7 @@ __global__ __launch_bounds__(256) void xagg_fwd_kernel(const int *__restrict__ r
                                                        const float *__restrict__ a_src,
                                                        const float *__restrict__ a_dst, float ns,
                                                        float *__restrict__ X4, float *__restrict__ row_stats) {
-  constexpr int U = HICGAT_XAGG_U;
+  constexpr int U = kXaggU;
   __shared__ float4 part[3][8][64];      // waves 1..3: acc[hd][kd][half] per lane
   __shared__ float red[4][4];            // per wave: (m0, m1) then (s0, s1), then (t0, t1)
   const int lane = lane_id(), wv = wave_in_block();
@@ -309,12 +302,10 @@ __global__ __launch_bounds__(256) void xagg_edge_kernel(const int *__restrict__ 
   const float4 ms = reinterpret_cast<const float4 *>(row_stats)[2 * (size_t)i];       // max0 max1 sum0 sum1
   const float2 dl = *reinterpret_cast<const float2 *>(row_stats + 8 * (size_t)i + 4);  // delta0 delta1
   const float2 *as2 = reinterpret_cast<const float2 *>(a_src);
-  constexpr int GL = HICGAT_XAGG_GL, NG = 64 / GL, NC = 128 / GL;   // lanes per edge, edges per wave, float4s per lane
+  constexpr int GL = kXaggGL, NG = 64 / GL, NC = 128 / GL;   // lanes per edge, edges per wave, float4s per lane
   const int g = lane / GL, t = lane % GL;
   for (int e0 = beg + NG * wv; e0 < end; e0 += 4 * NG) {   // wave wv: edges e0 .. e0 + NG - 1 of every 4 NG
-#if HICGAT_XAGG_DXA_LDS
     asm volatile("" ::: "memory");   // re-read dxa from LDS each pass: no 64-128 VGPR copy, more waves
-#endif
     const int e = e0 + g;
     const bool live = e < end;
     const int j = live ? col[e] : i;
@@ -392,10 +383,7 @@ __device__ __forceinline__ float row_share_f(float v) {
 }
 // (j, q0, q1) of edges k .. k + U - 1 of the group's chunk (k a multiple of U, < 16; a slot past the
 // row's end has q = 0 and j = the row itself, so it adds nothing)
-#ifndef HICGAT_EDGE_U
-#define HICGAT_EDGE_U 2   // edges per group per step of the edge pass (neighbour rows in flight)
-#endif
-constexpr int EU = HICGAT_EDGE_U;
+constexpr int EU = 2;   // edges per group per step of the edge pass (neighbour rows in flight)
 template <int U>
 __device__ __forceinline__ void row_share_n(int k, int j, float q0, float q1, int (&jj)[U], float (&qq0)[U],
                                             float (&qq1)[U]) {
@@ -418,10 +406,8 @@ __device__ __forceinline__ void row_share_n(int k, int j, float q0, float q1, in
 #undef HICGAT_RS1
   }
 }
-#ifndef HICGAT_EDGE_RPB
-#define HICGAT_EDGE_RPB 2   // own rows per workgroup of the edge pass (= partial rows of g_src: rows / RPB)
-#endif
-__host__ __device__ inline int edge_acc_blocks(int rows) { return rows <= 0 ? 1 : (rows + HICGAT_EDGE_RPB - 1) / HICGAT_EDGE_RPB; }
+constexpr int kEdgeRPB = 2;   // own rows per workgroup of the edge pass (= partial rows of g_src: rows / RPB)
+__host__ __device__ inline int edge_acc_blocks(int rows) { return rows <= 0 ? 1 : (rows + kEdgeRPB - 1) / kEdgeRPB; }
 __global__ __launch_bounds__(256) void xagg_edge_acc_kernel(const int *__restrict__ rowptr,
                                                             const int *__restrict__ col, int row_begin,
                                                             int row_end, const float *__restrict__ x,

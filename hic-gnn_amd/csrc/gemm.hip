@@ -25,25 +25,18 @@ namespace hicgat {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-#ifndef HICGAT_GK
-#define HICGAT_GK 16
-#endif
-constexpr int GK = HICGAT_GK;  // K-step of the fp32 kernel
+constexpr int GK = 16;  // K-step of the fp32 kernel
+
+// min blocks per CU of the 64 x 128 fp32 kernel: 6 makes the compiler keep the accumulators in
+// VGPRs (74 in all, 6 waves per SIMD instead of 4): fwd 512x512 0.104 vs 0.115 ms, dX 0.057 vs
+// 0.060 (profiles/r01_kbench_gemm_tiles.txt).  The 128 x 128 kernel keeps 1: squeezed the same
+// way its split-K weight gradients ran 2x slower.
+constexpr int kOcc64 = 6, kOcc128 = 1;
 
 // CS (weight gradients, A_KM only): the workgroups of the first column tile also sum their A tile
 // over K, i.e. the bias gradient db[m] = sum_k dY[k][m] of the same Linear comes out of the dW
 // GEMM (its per-split partials go into the slab beside the dW partials, one slab sum for both).
 template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB, bool CS = false>
-#ifndef HICGAT_GEMM_OCC64
-// min blocks per CU of the 64 x 128 fp32 kernel: 6 makes the compiler keep the accumulators in
-// VGPRs (74 in all, 6 waves per SIMD instead of 4): fwd 512x512 0.104 vs 0.115 ms, dX 0.057 vs
-// 0.060 (profiles/r01_kbench_gemm_tiles.txt).  The 128 x 128 kernel keeps 1: squeezed the same
-// way its split-K weight gradients ran 2x slower.
-#define HICGAT_GEMM_OCC64 6
-#endif
-#ifndef HICGAT_GEMM_OCC128
-#define HICGAT_GEMM_OCC128 1   // the same for the 128 x 128 tile (A/B builds)
-#endif
 // One BM x BN output tile (block coordinates bx, by, split bz) of the kernel below; also the body of
 // the grouped weight-gradient kernel (several GEMMs in one launch).
 __device__ __forceinline__ void gemm_tile(const float *__restrict__ A, int64_t lda,
@@ -225,8 +218,8 @@ __device__ __forceinline__ void gemm_tile(const float *__restrict__ A, int64_t l
 }
 
 template <int BM, int BN, bool A_KM, bool B_KM, bool VEC, bool DB, bool CS = false>
-__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? HICGAT_GEMM_OCC64
-                                  : (BM == 128 && BN == 128 && VEC) ? HICGAT_GEMM_OCC128 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, (BM == 64 && BN == 128 && VEC) ? kOcc64
+                                  : (BM == 128 && BN == 128 && VEC) ? kOcc128 : 1) void gemm_kernel(const float *__restrict__ A, int64_t lda,
                                                    const float *__restrict__ B, int64_t ldb,
                                                    float *__restrict__ C, int64_t ldc, int M, int N,
                                                    int K, int kchunk, const float *__restrict__ bias,
@@ -241,9 +234,6 @@ __global__ void colsum_zero_kernel(float *out, int N, int accumulate) {
   if (n < N && !accumulate) out[n] = 0.f;
 }
 
-#ifndef HICGAT_GEMM_DB_ALL
-#define HICGAT_GEMM_DB_ALL 0   // 1: double-buffered LDS for every layout (A/B build; default: dX layout only)
-#endif
 // csum (weight gradients only): also db[m] (+)= sum_k A[k][m] (the CS kernels); the slab of split z
 // is then [M*N dW partials | M db partials].
 template <int BM, int BN, bool AK, bool BK_>
@@ -263,7 +253,7 @@ static int launch(const float *A, int64_t lda, const float *B, int64_t ldb, floa
   hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BK_, V, D, C_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, \
                      K, kchunk, bias, sl, stride, acc, cdst)
   if (a_ok && b_ok && al) {
-    constexpr bool db = HICGAT_GEMM_DB_ALL ? true : (!AK && BK_);
+    constexpr bool db = !AK && BK_;   // double-buffered LDS: the dX layout (every layout measured: no gain)
     if (cs) HICGAT_GEMM_GO(true, db, AK);
     else HICGAT_GEMM_GO(true, db, false);
   } else {
@@ -300,17 +290,8 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
   }
   // tall row-major problems (M = node rows): 64 x 128 tiles keep >= 2 blocks per CU in flight;
   // square-ish weight gradients (M, N = features, K = rows split): 128 x 128
-#ifndef HICGAT_GEMM_TALL128
-#define HICGAT_GEMM_TALL128 0   // 1: 128 x 128 tiles for the tall (M = node rows) problems too
-#endif
-#ifndef HICGAT_GEMM_TALL_TILE
-#define HICGAT_GEMM_TALL_TILE 0   // tall problems: 0 = 64 x 128, 2 = 128 x 256, 3 = 256 x 128 (A/B builds)
-#endif
-  if (HICGAT_GEMM_TALL_TILE == 2 && M > 1024 && N >= 256)
-    return launch<128, 256, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
-  if (HICGAT_GEMM_TALL_TILE == 3 && M > 1024 && N >= 128)
-    return launch<256, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
-  if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
+  // (128 x 128, 128 x 256 and 256 x 128 tiles for the tall problems measured slower, round 1)
+  if (M >= 128 && N >= 128 && M <= 1024)
     return launch<128, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   if (N >= 128) return launch<64, 128, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
   return launch<64, 64, AK, BK_>(A, lda, B, ldb, C, ldc, M, N, K, splits, bias, slab, acc, s);
@@ -323,13 +304,8 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // workgroup has the same MFMA work.  A job whose operands cannot be read as float4 (dense3: M = 3)
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
-#ifndef HICGAT_WEIGHTED_LG1_ROWS
-#define HICGAT_WEIGHTED_LG1_ROWS 1024   // weighted column-sum jobs taller than this: 2 lanes per row group
-#endif
-constexpr int64_t WEIGHTED_LG1_ROWS = HICGAT_WEIGHTED_LG1_ROWS;
-#ifndef HICGAT_WEIGHTED_LG
-#define HICGAT_WEIGHTED_LG 1   // log2 lanes per row group of those jobs (2: 0.425-0.427 ms, 1: 0.422-0.423 at P = 8)
-#endif
+constexpr int64_t WEIGHTED_LG1_ROWS = 1024;   // weighted column-sum jobs taller than this: 2 lanes per row group
+constexpr int kWeightedLg = 1;   // log2 lanes per row group of those jobs (2: 0.425-0.427 ms, 1: 0.422-0.423 at P = 8)
 // The job a block belongs to: the number of later job starts <= b, every start read at a constant
 // offset of the kernel argument block (one batch of scalar loads instead of one dependent load per
 // job scanned; measured even at P = 8, profiles/r04p_sim_ab.txt)
@@ -340,9 +316,6 @@ __device__ __forceinline__ int find_job(const int (&start)[KMAX], int n, int b) 
   for (int k = 1; k < KMAX; ++k) q += (k < n && b >= start[k]) ? 1 : 0;
   return q;
 }
-#ifndef HICGAT_GROUP_DB
-#define HICGAT_GROUP_DB 0   // 1: double-buffered LDS in the grouped weight-gradient tiles (A/B builds)
-#endif
 struct WJob {
   const float *dy;
   const float *x;
@@ -357,7 +330,7 @@ struct WJobs {
   WJob j[kMaxWJobs];
   int n;
 };
-__global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(const WJobs jobs) {
+__global__ __launch_bounds__(256, kOcc128) void wgrad_grouped_kernel(const WJobs jobs) {
   const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const WJob &J = jobs.j[q];
   const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
@@ -365,7 +338,7 @@ __global__ __launch_bounds__(256, HICGAT_GEMM_OCC128) void wgrad_grouped_kernel(
   const int64_t stride = (int64_t)J.M * J.N + J.M;
   float *cs = J.db ? (J.slab ? J.slab + (int64_t)J.M * J.N : J.db) : nullptr;
   if (J.vec)
-    gemm_tile<kGroupTile, kGroupTile, true, true, true, HICGAT_GROUP_DB, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
+    gemm_tile<kGroupTile, kGroupTile, true, true, true, false, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
                                                                      J.K, J.kchunk, nullptr, J.slab, stride,
                                                                      J.accumulate, cs, bx, by, bz);
   else
@@ -487,7 +460,7 @@ struct RJobs {
   int n, splits;
 };
 template <bool B_KM>
-__global__ __launch_bounds__(256, HICGAT_GEMM_OCC64) void gemm_rows_grouped_kernel(const RJobs jobs) {
+__global__ __launch_bounds__(256, kOcc64) void gemm_rows_grouped_kernel(const RJobs jobs) {
   const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const RJob &J = jobs.j[q];
   const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
@@ -631,7 +604,7 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
     // lanes per row group (one lane per group for the tallest jobs, uncoalesced, measured slower:
     // P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? HICGAT_WEIGHTED_LG : 2;
+    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? kWeightedLg : 2;
     J.blk0 = blk;
     cj.start[cj.n - 1] = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
@@ -742,7 +715,7 @@ extern "C" int hicgat_gemm_wgrad(int M, int N, int K, const float *dY, int64_t l
   hipStream_t s = (hipStream_t)stream;
   float *slab = static_cast<float *>(workspace);
   // the dispatch of hicgat_gemm_ex's fp32 path for the (K-major, K-major) layout
-  if (M >= 128 && N >= 128 && (M <= 1024 || HICGAT_GEMM_TALL128))
+  if (M >= 128 && N >= 128 && M <= 1024)
     return launch<128, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
   if (N >= 128) return launch<64, 128, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);
   return launch<64, 64, true, true>(dY, ldy, X, ldx, dW, lddw, M, N, K, splits, nullptr, slab, accumulate, s, db);

@@ -21,9 +21,6 @@
 namespace hicgat {
 
 constexpr int BT = 128;
-#ifndef HICGAT_PD_UNROLL
-#define HICGAT_PD_UNROLL 2   // rows per iteration of the packed interior loop (LDS reads of the next row in flight)
-#endif
 enum { MODE_SYM = 0, MODE_FULL = 1 };
 // loss kinds (include/hicgat.h): the KIND template parameter below
 enum { KIND_MSE = HICGAT_LOSS_MSE, KIND_COMBINED = HICGAT_LOSS_COMBINED, KIND_CONTRASTIVE = HICGAT_LOSS_CONTRASTIVE };
@@ -62,10 +59,6 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
-#ifndef HICGAT_PD_SUPPORT_RIDES
-#define HICGAT_PD_SUPPORT_RIDES 1   // sharded shares: the support blocks in the tile launch (A/B builds: 0)
-#endif
-constexpr bool SUPPORT_RIDES = HICGAT_PD_SUPPORT_RIDES;
 
 // v + the values of lanes l^16, l^32 and l^48 (ds_bpermute shuffles; a v_permlane16/32_swap form
 // measured slower: the loss chain 0.162 vs 0.157 ms, profiles/r04h_kbench_pairdist.txt)
@@ -87,9 +80,6 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // add the 16 per row in tx order at the end, while 0..127 add the column partials -- instead of
 // three 16-lane DPP sums per row inside the pair loop (~20 % of its VALU issue).
 constexpr int kRowPad = 17;
-#ifndef HICGAT_PD_ROWLDS
-#define HICGAT_PD_ROWLDS 1   // 0: the per-row DPP sums (A/B builds)
-#endif
 
 // Per-thread accumulators of one tile: the moments and the column partials of its 8 columns.
 struct TileAcc {
@@ -214,7 +204,7 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
   }
   const f2 z2 = f2{0.f, 0.f};
   f2 L2 = z2, sd2 = z2, sdd2 = z2, sdt2 = z2, st2 = z2, stt2 = z2;
-#pragma unroll HICGAT_PD_UNROLL
+#pragma unroll 2   // rows per iteration (the next row's LDS reads in flight)
   for (int k = K0; k < K1; ++k) {
     const int lr = ty * 4 + (k & 3) + (k >> 2) * 64;
     const f2 rx = f2{sc[0][lr][0], sc[0][lr][0]}, ry = f2{sc[0][lr][1], sc[0][lr][1]},
@@ -285,9 +275,6 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
   }
 }
 
-#ifndef HICGAT_PD_DBG
-#define HICGAT_PD_DBG 0   // A/B builds only: 1 = skip the T loads (math only), 2 = skip the math (loads only)
-#endif
 
 // MODE_SYM: T = symmetric truth, tiles I <= J, pairs i < j, w = (d - t)/d (scale 4/N^2 later).
 // MODE_FULL: T = upstream grad G of D, all tiles, pairs i != j, w = g/d.
@@ -295,9 +282,6 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
 // KIND_CONTRASTIVE: sum |d - t| and w = sgn(d - t) / d.
 // BG: the background form (T = bg at every pair; no T read, no diagonal term -- the support pass,
 // pairdist_support_kernel, adds the entries that differ and the diagonal).
-#ifndef HICGAT_PD_BG_OCC
-#define HICGAT_PD_BG_OCC 1   // workgroups per CU the background form's register budget is set for
-#endif
 template <int KIND>
 __device__ void support_block(const float *__restrict__ coords, float bg, int row_begin, int row_end,
                               const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col,
@@ -316,7 +300,7 @@ struct SupportArgs {
 };
 
 template <int MODE, bool VEC, int KIND, bool BG = false, bool SUP = false>
-__global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_kernel(const float *__restrict__ coords,
+__global__ __launch_bounds__(256, 1) void pairdist_tile_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ T, int N,
                                                             int64_t ldt, int64_t row0, int64_t col0,
                                                             int nb, int64_t t0,
@@ -336,7 +320,7 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   __shared__ float sc[2][BT][3];
   __shared__ float4 colred[4][BT];
   __shared__ double mred[4][7];
-  constexpr bool RL = BG && HICGAT_PD_ROWLDS;
+  constexpr bool RL = BG;
   __shared__ float4 rowpart_s[RL ? BT * kRowPad : 1];
   float4 *rowpart = RL ? rowpart_s : nullptr;
   const int64_t t = t0 + blockIdx.x;
@@ -374,7 +358,7 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
       const int r0 = (q < 8 ? 0 : 64) + wv * 16 + (q & 7) * 2;
       const int gi = min(I * BT + r0 + (lane >> 5), N - 1);
       const float *src = T + (size_t)(gi - row0) * ldt + (size_t)((int64_t)J * BT - col0) + (lane & 31) * 4;
-      if (HICGAT_PD_DBG != 1) __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, &tile[r0 * BT], 16, 0, 0);
     }
   }
   // sc[] (written above with ds_write) to all waves: LDS drain + raw barrier -- __syncthreads()
@@ -398,16 +382,14 @@ __global__ __launch_bounds__(256, BG ? HICGAT_PD_BG_OCC : 1) void pairdist_tile_
   const bool interior = I != J && (I + 1) * BT <= N && (J + 1) * BT <= N;   // block-uniform
   if (VEC) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // this wave's first 16 rows landed
   constexpr bool PK = (VEC || BG) && MODE == MODE_SYM;   // packed interior path (tile_rows_pk)
-  if (HICGAT_PD_DBG == 2) {
-  } else if (interior) {
+  if (interior) {
     if constexpr (PK) tile_rows_pk<KIND, 0, 4, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
     else tile_rows<MODE, VEC, KIND, false, 0, 4>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
     tile_rows<MODE, VEC, KIND, true, 0, 4, BG, RL>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   }
   if (VEC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // and the second 16
-  if (HICGAT_PD_DBG == 2) {
-  } else if (interior) {
+  if (interior) {
     if constexpr (PK) tile_rows_pk<KIND, 4, 8, BG, RL>(tile, bg, sc, tx, ty, cx, cy, cz, prow, A, rowpart);
     else tile_rows<MODE, VEC, KIND, false, 4, 8>(T, ldt, row0, col0, N, I, J, bg, tile, sc, tx, ty, cx, cy, cz, gj, prow, A, rowpart);
   } else {
@@ -905,27 +887,44 @@ extern "C" int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, flo
 }
 
 // finalize + a rank's rows of the all-reduced fp64 dcoords narrowed to fp32 (one launch after the
-// multi-GPU loss all-reduce instead of two)
+// multi-GPU loss all-reduce instead of two); with cbuf, also the coordinates in global row order,
+// cglob[i] = cbuf[gidx[i]] (the padded all-gather layout reordered: step()'s return value, no launch
+// of its own)
 __global__ __launch_bounds__(256) void finalize_rows_kernel(int N, int loss_kind, double *__restrict__ stats,
                                                             float *__restrict__ loss, const double *__restrict__ dc64,
-                                                            int64_t n3, float *__restrict__ dcoords) {
+                                                            int64_t n3, float *__restrict__ dcoords,
+                                                            const float *__restrict__ cbuf,
+                                                            const int32_t *__restrict__ gidx, float *__restrict__ cglob) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t == 0) finalize_stats(N, loss_kind, stats, loss);
   if (t < n3) dcoords[t] = (float)dc64[t];
+  if (cbuf && t < 3 * (int64_t)N) {
+    const int64_t i = t / 3;
+    cglob[t] = cbuf[3 * (int64_t)gidx[i] + (t - 3 * i)];
+  }
 }
 
-extern "C" int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64,
-                                             int row_begin, int row_end, float *dcoords, hicgat_stream_t stream) {
+extern "C" int hicgat_pairdist_finalize_rows_ex(int N, int loss_kind, double *stats, float *loss, const double *dc64,
+                                                int row_begin, int row_end, float *dcoords, const float *cbuf,
+                                                const int32_t *gidx, float *cglob, hicgat_stream_t stream) {
   if (N <= 0 || !stats || loss_kind < KIND_MSE || loss_kind > KIND_CONTRASTIVE) return HICGAT_EINVAL;
   if (row_begin < 0 || row_end > N || row_begin > row_end) return HICGAT_EINVAL;
   const int64_t n3 = 3 * (int64_t)(row_end - row_begin);
   if (n3 > 0 && (!dc64 || !dcoords)) return HICGAT_EINVAL;
+  if (cbuf && (!gidx || !cglob)) return HICGAT_EINVAL;
   const int64_t off = 3 * (int64_t)row_begin;
-  hipLaunchKernelGGL(finalize_rows_kernel, dim3((unsigned)((n3 + 255) / 256 + (n3 == 0))), dim3(256), 0,
-                     (hipStream_t)stream, N, loss_kind, stats, loss, n3 ? dc64 + off : nullptr, n3,
-                     n3 ? dcoords + off : nullptr);
+  const int64_t work = std::max<int64_t>(std::max<int64_t>(n3, cbuf ? 3 * (int64_t)N : 0), 1);
+  hipLaunchKernelGGL(finalize_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, N,
+                     loss_kind, stats, loss, n3 ? dc64 + off : nullptr, n3, n3 ? dcoords + off : nullptr, cbuf, gidx,
+                     cglob);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64,
+                                             int row_begin, int row_end, float *dcoords, hicgat_stream_t stream) {
+  return hicgat_pairdist_finalize_rows_ex(N, loss_kind, stats, loss, dc64, row_begin, row_end, dcoords, nullptr,
+                                          nullptr, nullptr, stream);
 }
 
 // ---- background form: T = bg except at a sorted symmetric CSR support + the diagonal -----------
@@ -973,7 +972,7 @@ extern "C" int hicgat_pairdist_mse_fused_support_range_ex(const float *coords, c
   // a rank's share (dcoords64: the sharded step): the support blocks ride in the tile launch (one
   // launch fewer on the critical path; at N = 20000 on one GPU the support pass needs the occupancy
   // of its own launch: 1.881 / 1.884 vs 1.875 / 1.877 ms per step, profiles/r04u_ab_single_gpu.txt)
-  const bool ride = dcoords64 && SUPPORT_RIDES && nt > 0 && sblocks > 0;
+  const bool ride = dcoords64 && nt > 0 && sblocks > 0;
   SupportArgs sa;
   if (ride) {
     sa.rowptr = rowptr;

@@ -31,28 +31,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // The compiler's scheduler sinks the ring's weight loads next to the MFMAs that use them (one group
 // in flight: every L2 latency exposed); a scheduling barrier after each group's loads keeps them R
-// groups ahead (HICGAT_TAIL_SCHED_PIN=0: the compiler's placement, A/B builds): P = 8 rank step
-// 0.426-0.427 vs 0.431-0.432 ms, synth-2000 0.597 vs 0.604 ms; R = 8: 0.442 (profiles/r04n_sim_ab.txt)
-#ifndef HICGAT_TAIL_SCHED_PIN
-#define HICGAT_TAIL_SCHED_PIN 1
-#endif
-#if HICGAT_TAIL_SCHED_PIN
+// groups ahead: P = 8 rank step 0.426-0.427 vs 0.431-0.432 ms, synth-2000 0.597 vs 0.604 ms without
+// the barriers; R = 8: 0.442 (profiles/r04n_sim_ab.txt)
 #define HICGAT_TAIL_SCHED() __builtin_amdgcn_sched_barrier(0)
-#else
-#define HICGAT_TAIL_SCHED() ((void)0)
-#endif
-
-#ifndef HICGAT_TAIL_RING
-#define HICGAT_TAIL_RING 4   // weight groups in flight per wave (the prefetch ring's depth)
-#endif
+constexpr int kTailRing = 4;   // weight groups in flight per wave (the prefetch ring's depth)
 
 // acc[h][t] (h < RB/16 row halves, t < NT) += A[RB x K] (LDS, row stride lda) x B^T, B = the weight
 // rows n0 + 16t + (l & 15) (K columns).  The weights of group g + R are loaded right after group g's
-// MFMAs, so R - 1 groups of MFMAs cover every load (a ring of R float4 sets, R = HICGAT_TAIL_RING).
+// MFMAs, so R - 1 groups of MFMAs cover every load (a ring of R float4 sets, R = kTailRing).
 template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
                                           f32x4 (&acc)[RB / 16][NT], int lane) {
-  constexpr int G = K / 16, H = RB / 16, R = G < HICGAT_TAIL_RING ? G : HICGAT_TAIL_RING;
+  constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
   static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
@@ -152,9 +142,7 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
 // MFMAs (with 4, one wave per SIMD, every latency of the chain is exposed; 8: 52 vs 62 us for the
 // P = 8 shard's forward; 16: rank step 0.438-0.440 vs 0.448 ms -- a rank's shard at P = 8 has 169
 // workgroups for 256 CUs, one each).  The LayerNorm parameter partials are one row per wave.
-#ifndef HICGAT_TAIL_WAVES
-#define HICGAT_TAIL_WAVES 16   // 16: 0.438 / 0.440 vs 0.448 ms per P = 8 rank step (profiles/r04k_sim_ab.txt)
-#endif
+constexpr int kTailWaves = 16;   // 16: 0.438 / 0.440 vs 0.448 ms per P = 8 rank step (profiles/r04k_sim_ab.txt)
 // HEADS (the sharded aggregate-first GATConv, gat_xagg.hip): the tail's input rows are formed here
 // from the two heads' aggregates, out^h = xa^h W_h^T + b^h (xa^h = x + h * xa_hs, row stride ldx; W_h
 // = rows 256h .. of lin_l's weight Wh [512][512]), written as Y0 (pre-activation) and O = relu(Y0)
@@ -163,15 +151,8 @@ __device__ __forceinline__ void ln_rows(const float *__restrict__ Ys, int lds, c
 // waves per SIMD pinned to one workgroup's (NW / 4): a shard's grid has at most one workgroup per
 // CU, and without the pin the compiler schedules for the occupancy the LDS would admit (two
 // workgroups, 64 VGPRs at NW = 16) and sinks every weight load next to its MFMAs -- the prefetch ring
-// collapses to one group in flight (HICGAT_TAIL_PIN=0 keeps that form for A/B)
-#ifndef HICGAT_TAIL_PIN
-#define HICGAT_TAIL_PIN 1
-#endif
-#if HICGAT_TAIL_PIN
-#define HICGAT_TAIL_WPE __attribute__((amdgpu_waves_per_eu(HICGAT_TAIL_WAVES / 4, HICGAT_TAIL_WAVES / 4)))
-#else
-#define HICGAT_TAIL_WPE
-#endif
+// collapses to one group in flight
+#define HICGAT_TAIL_WPE __attribute__((amdgpu_waves_per_eu(kTailWaves / 4, kTailWaves / 4)))
 template <int RB, int NW, bool HEADS = false>
 __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
@@ -287,7 +268,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
 template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int lda, const float *__restrict__ W, int ldw,
                                             int n0, f32x4 (&acc)[RB / 16][NT], int lane) {
-  constexpr int G = K / 16, H = RB / 16, R = G < HICGAT_TAIL_RING ? G : HICGAT_TAIL_RING;
+  constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
   static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wcol = W + (size_t)kq * ldw + n0 + li;
@@ -574,7 +555,7 @@ int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const 
   // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
   // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
   // with one workgroup per CU every phase's latency is exposed.
-  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
+  constexpr int RB = 16, NW = kTailWaves;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
@@ -607,7 +588,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
                                            const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2,
                                            float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
                                            hicgat_stream_t stream) {
-  if (HICGAT_TAIL_WAVES < 8) return HICGAT_EUNSUPPORTED;
+  if (kTailWaves < 8) return HICGAT_EUNSUPPORTED;
   TailHeads hh;
   hh.xa = xa;
   hh.xa_hs = xa_head_stride;
@@ -619,7 +600,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
                                st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh, (hipStream_t)stream);
 }
 
-extern "C" int hicgat_tail_bwd_waves(void) { return HICGAT_TAIL_WAVES; }
+extern "C" int hicgat_tail_bwd_waves(void) { return kTailWaves; }
 
 extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
   return M <= 0 ? 16 : (size_t)((M + 15) / 16) * 2 * W * sizeof(float);   // one [2W] row per workgroup
@@ -639,7 +620,7 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
                     const float *g3, const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
                     size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
                     const TailHeadsBwd &hh, hipStream_t stream) {
-  constexpr int RB = 16, NW = HICGAT_TAIL_WAVES;
+  constexpr int RB = 16, NW = kTailWaves;
   // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
   constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
   if (M < 0) return HICGAT_EINVAL;
@@ -691,7 +672,7 @@ extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const fl
                                            size_t ws3_bytes, int act, const float *Y0, const float *Wh,
                                            const float *bh, float *dout, float *row_stats, float *dxa,
                                            hicgat_stream_t stream) {
-  if (HICGAT_TAIL_WAVES < 8) return HICGAT_EUNSUPPORTED;
+  if (kTailWaves < 8) return HICGAT_EUNSUPPORTED;
   TailHeadsBwd hh;
   hh.act = act ? 1 : 0;
   hh.Y0 = Y0;

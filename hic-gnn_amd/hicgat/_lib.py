@@ -79,6 +79,7 @@ SIGNATURES = {
                                                c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_finalize": (c_int, [c_int, c_int, c_p, c_p, c_p]),
     "hicgat_pairdist_finalize_rows": (c_int, [c_int, c_int, c_p, c_p, c_p, c_int, c_int, c_p, c_p]),
+    "hicgat_pairdist_finalize_rows_ex": (c_int, [c_int, c_int, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_pairdist_num_tiles": (c_i64, [c_int, c_int]),
     "hicgat_pairdist_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_pairdist_mse_fused_support": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_p,

@@ -67,6 +67,16 @@ def resolve_mode(mode, P):
     if mode == "auto":
         return "xagg" if P >= AUTO_XAGG_MIN_P else "slab"
     return mode
+# workgroups of the xagg step's side-stream grouped weight-gradient launch (beside the edge pass,
+# which needs the CUs: the grouped launch's default 512 would crowd it)
+XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "128"))
+
+
+def _null():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 # side streams for the MLP tail's queued parameter-gradient launches in the sharded step
 # (ops.side_flush lanes; 1 = one chain as on a single GPU)
 SIDE_LANES = int(os.environ.get("HICGAT_DIST_SIDE_LANES", "3"))
@@ -305,6 +315,10 @@ class SimComm:
     def __init__(self, P, rank, emulate=True):
         self.P, self.rank, self.nccl, self.group = P, rank, True, None
         self.emulate = emulate
+        self.last = None
+
+    def begin_step(self):
+        self.last = None
 
     def _emulate(self, name, kind, t):
         if not self.emulate or not getattr(t, "is_cuda", False):
@@ -312,11 +326,19 @@ class SimComm:
             return
 
         def fn():
+            # collectives of one communicator run one after another in issue order whatever stream
+            # issued them (ProcessGroupNCCL queues them on the communicator's own stream): each
+            # emulation waits for the previous one (an event, so no extra stream joins a capture)
             from . import _lib
             lib = _lib.lib()
+            cur = torch.cuda.current_stream(t.device)
+            if self.last is not None:
+                cur.wait_event(self.last)
             _lib.check(lib.hicgat_sim_collective(float(coll_us(kind, t.numel() * t.element_size(), self.P)),
                                                  SIM_COMM_WGS, SIM_COMM_THREADS, _lib.stream(t.device)),
                        "hicgat_sim_collective")
+            self.last = torch.cuda.Event()
+            self.last.record(cur)
         _record(name, kind, t, self.P, fn)
 
     def all_gather_inplace(self, buf, own, name="all_gather"):
@@ -410,8 +432,9 @@ class ShardedTrainer:
             self.gpart = torch.zeros((kern.edge_acc_blocks(Rl), 2 * F), **f32)   # g_src partial rows
             self.a_src = torch.zeros((N, self.H), **f32)
             self.a_dst = torch.zeros((N, self.H), **f32)
-            self.g_src = torch.zeros(2 * F, **f32)
-            self.g_dst = torch.zeros(2 * F, **f32)
+            # [g_src | g_dst] (the edge pass's partial sums), one buffer: the step's second all-reduce
+            self.gsd = torch.zeros(2, 2 * F, **f32)
+            self.g_src, self.g_dst = self.gsd[0], self.gsd[1]
             rows = 0                                                       # no [N, D] node buffers
         self.h = torch.zeros((rows, D), **f32)
         self.out = torch.zeros((rows, D), **f32)
@@ -427,9 +450,8 @@ class ShardedTrainer:
         self.rs = torch.zeros((N if mode == "xagg" else rows, 4 * self.H), **f32)
         self.coords_buf = torch.zeros((P * R, 3), **f32)
         # step()'s coordinates in global row order (the loss reads the padded all-gather layout
-        # through gidx; the reorder runs on a side stream beside the loss, off the critical path)
+        # through gidx; the loss's finalize launch writes this reordered copy)
         self.coords_glob = torch.zeros((N, 3), **f32)
-        self._glob_ev = None
         if isinstance(self.comm, SimComm):
             # the other ranks' coordinates, which the all-gather would bring: any spread-out values
             g = torch.Generator().manual_seed(rank)
@@ -449,7 +471,7 @@ class ShardedTrainer:
         cut = (max(ends) + 3) // 4 * 4
         self.grad_split = cut if (firsts and min(firsts) >= cut) else None
         self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
-        self.coord_stream = torch.cuda.Stream(device=dev) if self.cuda else None
+        self.grad_stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
@@ -482,7 +504,8 @@ class ShardedTrainer:
         self.comm.all_reduce(self.red, name="loss_all_reduce")
         # finalize + this rank's rows of dcoords narrowed to fp32, one launch
         K.loss_finalize(N, self.kind, self.stats, self.loss, dc64=self.dc64, r0=self.r0, r1=self.r1,
-                        dcoords=self.dcoords)
+                        dcoords=self.dcoords,
+                        reorder=(self.coords_buf, self.gidx32, self.coords_glob) if self.direct_coords else None)
         return self.dcoords[self.r0:self.r1]
 
     def _tail(self, o=None, heads=None):
@@ -503,13 +526,8 @@ class ShardedTrainer:
         # direct: the loss reads the padded buffer through gidx (no reorder launch); the returned
         # coordinates are then in that layout (``global_coords`` reorders them)
         if self.direct_coords:
+            # the loss's finalize launch reorders them into coords_glob (step()'s output)
             coords = self.coords_buf
-            cur = torch.cuda.current_stream()
-            self.coord_stream.wait_stream(cur)
-            with torch.cuda.stream(self.coord_stream):
-                torch.index_select(self.coords_buf, 0, self.gidx, out=self.coords_glob)
-                self._glob_ev = torch.cuda.Event()
-                self._glob_ev.record()
         else:
             coords = self.coords_buf.index_select(0, self.gidx)
             self.coords_glob.copy_(coords)
@@ -523,22 +541,20 @@ class ShardedTrainer:
     def step(self):
         """One training step; returns (loss, stats, coords) with coords [N, 3] in global row order
         (the coordinates the step's loss was evaluated on)."""
+        if hasattr(self.comm, "begin_step"):
+            self.comm.begin_step()
         if self.mode == "xagg" and self.cuda:
             self.opt._reattach()     # the gradient buffer is zeroed by the step's first launch (xagg_logits)
         else:
             self.opt.zero_grad()
         self.model.train()
         if self.mode == "slab":
-            coords, tail_done = self._step_slab()
+            self._step_slab()
         elif self.mode == "xagg":
-            coords, tail_done = self._step_xagg()
+            self._step_xagg()       # its gradient all-reduces are part of the step's backward
         else:
-            coords, tail_done = self._step_allgather()
-        self._grad_allreduce(tail_done)
+            self._step_allgather()
         self.opt.step(counted=self._ctr() is not None)
-        if self._glob_ev is not None:
-            torch.cuda.current_stream().wait_event(self._glob_ev)
-            self._glob_ev = None
         return self.loss, self.stats, self.coords_glob
 
     def _ctr(self):
@@ -547,7 +563,7 @@ class ShardedTrainer:
         return self.opt.step_ctr if (self.mode == "xagg" and self.cuda and
                                      getattr(self.opt, "step_ctr", None) is not None) else None
 
-    def _grad_allreduce(self, tail_done):
+    def _grad_allreduce(self, tail_done):   # the slab / allgather forms
         """The flat gradient all-reduce in two buckets: the MLP tail's (on the comm stream, after
         ``tail_done`` -- an event on the side stream after the tail's dW GEMMs, so it runs beside
         lin_l's dW GEMM) and the GATConv's; the optimizer's stream waits for both."""
@@ -614,7 +630,7 @@ class ShardedTrainer:
                          accumulate=True)
             K.param_grad(self.h[r0:r1], dout[r0:r1].contiguous(), None, self.rs[r0:r1], H,
                          out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
-        return coords, tail_done
+        self._grad_allreduce(tail_done)
 
     def _step_xagg(self):
         """Aggregate-first GATConv (gat_xagg.hip): x replicated, every GEMM on own rows only."""
@@ -646,11 +662,15 @@ class ShardedTrainer:
                                 name="gemm_fwd")
             o, coords_loc, coords = self._tail(self.O if self.act else Y0)
         # ---- backward -----------------------------------------------------------------------
-        # every parameter gradient of the step -- the tail's dW / db / LayerNorm sums (collected from
-        # its backward), dW_h += dout^h^T xa^h with dbias^h (the heads' column sums of dout), g_src
-        # (the edge pass's partial rows) and g_dst -- in ONE grouped GEMM launch + ONE grouped
-        # column-sum launch after the edge pass, on this stream: at a P = 8 shard the ~15 separate
-        # launches over side lanes were the critical path (profiles/r03w_simprof_xagg_P8_rank0_timeline.txt)
+        # The tail's parameter gradients (dW / db / LayerNorm sums, collected from its backward) and
+        # the heads' dW_h += dout^h^T xa^h with dbias^h need only the tail's backward: ONE grouped
+        # weight-gradient launch + ONE grouped column-sum launch for all of them on a side stream, then
+        # the all-reduce of the whole flat gradient buffer -- both beside the edge pass.  The edge pass
+        # leaves only g_src / g_dst (the attention terms' partial sums, [2, 1024]): a small grouped
+        # launch, their all-reduce, and the finish that turns the SUMMED g into datt and W's att (x) g
+        # term on every rank (linear in g: the same as finishing per rank and summing).  Round 4 ran
+        # every gradient in one grouped launch after the edge pass and both buckets' all-reduces after
+        # it (profiles/r04z3_simprof_xagg_P8_rank0_timeline.txt).
         with ops.grouped_param_grads():
             coords_loc.backward(self.dcoords[r0:r1])
         with torch.no_grad():
@@ -661,17 +681,24 @@ class ShardedTrainer:
                                       None) for hd in (0, 1)], b_kmajor=1, name="gemm_dx")
             heads = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
                       None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
+            side = None
+            if self.cuda:
+                side = self.grad_stream
+                side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side) if side is not None else _null():
+                keep = ops.grouped_flush(K, heads, target_wgs=XAGG_SIDE_WGS)
+                # every gradient but the attention vectors' (0 until the finish) and W's att (x) g term
+                self.comm.all_reduce(self.opt.grad, name="grad_all_reduce")
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                             self.gpart, xa2=self.X4[:, 1])
-            # g_src (the edge pass's partial rows) and g_dst (its da_dst) need the edge pass; the heads'
-            # dW in the same launch pair (on a side stream beside the edge pass: 0.468 vs 0.459 ms per
-            # rank step at P = 8, profiles/r04h_sim_ab.txt)
-            ops.grouped_flush(K, heads + [("c", self.gpart, self.g_src, False),
-                                          ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None,
-                                           False)])
+            ops.grouped_flush(K, [("c", self.gpart, self.g_src, False),
+                                  ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)])
+            self.comm.all_reduce(self.gsd, name="g_all_reduce")
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
+            del keep
             K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
                                 self.att_r.grad.view(-1))
-        return coords, None
 
     def _step_allgather(self):
         K, D = self.K, self.D
@@ -712,5 +739,5 @@ class ShardedTrainer:
                         self.W.grad.addmm_(self.dh[q0:q1].t(), self.x_loc)
             K.param_grad(self.h[q0:q1], dout[q0:q1].contiguous(), self.da_src[q0:q1], self.rs[q0:q1], self.H,
                          out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)
-        return coords, tail_done
+        self._grad_allreduce(tail_done)
 

@@ -340,17 +340,22 @@ class HipKernels:
                 int(t1), int(s0), int(s1), int(kind), P(stats), P(loss), P(d32), P(d64), P(ws), ws.numel(),
                 _lib.stream(coords.device)), "hicgat_pairdist_mse_fused_support_range_ex")
 
-    def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None):
+    def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None, reorder=None):
         """mse / r / alpha / total from the (all-reduced) moments; with ``dc64`` also dcoords[r0:r1] =
-        fp32(dc64[r0:r1]) in the same launch."""
+        fp32(dc64[r0:r1]) in the same launch; ``reorder`` = (cbuf, gidx32, cglob): also cglob[i] =
+        cbuf[gidx[i]] (the all-gathered coordinates in global row order)."""
         if dc64 is None:
             _lib.check(self.lib.hicgat_pairdist_finalize(n, int(kind), P(stats), P(loss), _lib.stream(stats.device)),
                        "hicgat_pairdist_finalize")
             return
         assert dc64.is_contiguous() and dcoords.is_contiguous() and dc64.shape == dcoords.shape == (n, 3)
-        _lib.check(self.lib.hicgat_pairdist_finalize_rows(n, int(kind), P(stats), P(loss), P(dc64), int(r0), int(r1),
-                                                          P(dcoords), _lib.stream(stats.device)),
-                   "hicgat_pairdist_finalize_rows")
+        cbuf, gidx, cglob = reorder if reorder is not None else (None, None, None)
+        if reorder is not None:
+            assert cbuf.is_contiguous() and cglob.shape == (n, 3) and gidx.dtype == torch.int32 and gidx.numel() == n
+        _lib.check(self.lib.hicgat_pairdist_finalize_rows_ex(n, int(kind), P(stats), P(loss), P(dc64), int(r0), int(r1),
+                                                             P(dcoords), P(cbuf), P(gidx), P(cglob),
+                                                             _lib.stream(stats.device)),
+                   "hicgat_pairdist_finalize_rows_ex")
 
     def pairdist_fwd(self, coords):
         n = coords.shape[0]

@@ -293,6 +293,11 @@ int hicgat_pairdist_finalize(int N, int loss_kind, double *stats, float *loss, h
  * (all-reduced) fp64 coordinate gradient [N][3], in one launch (a rank's rows for its tail backward). */
 int hicgat_pairdist_finalize_rows(int N, int loss_kind, double *stats, float *loss, const double *dc64, int row_begin,
                                   int row_end, float *dcoords, hicgat_stream_t stream);
+/* The same; with cbuf (the padded all-gather coordinates [P*R][3]) also cglob[i] = cbuf[gidx[i]]
+ * (i < N: the coordinates in global row order, hicgat.dist's step() output) in the same launch. */
+int hicgat_pairdist_finalize_rows_ex(int N, int loss_kind, double *stats, float *loss, const double *dc64,
+                                     int row_begin, int row_end, float *dcoords, const float *cbuf,
+                                     const int32_t *gidx, float *cglob, hicgat_stream_t stream);
 /* Tile count and workspace of the two tilings, mode HICGAT_PD_TRI (the fused loss: upper-triangle
  * 128x128 tiles, nb(nb+1)/2) or HICGAT_PD_SQUARE (hicgat_pairdist_bwd: nb*nb), nb = ceil(N/128). */
 enum { HICGAT_PD_SQUARE = 0, HICGAT_PD_TRI = 1 };

@@ -396,9 +396,12 @@ class CpuKernels:
         dcoords.copy_(gf.to(dcoords.dtype).view_as(dcoords))
         self.loss_finalize(n, kind, stats, loss)
 
-    def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None):
+    def loss_finalize(self, n, kind, stats, loss, dc64=None, r0=0, r1=0, dcoords=None, reorder=None):
         if dc64 is not None:
             dcoords[r0:r1].copy_(dc64[r0:r1])
+        if reorder is not None:
+            cbuf, gidx, cglob = reorder
+            cglob.copy_(cbuf.index_select(0, gidx.long()))
         s = stats.double()
         M = n * (n - 1) / 2
         if kind == 2:        # contrastive: 0.1 * mean_{i<j} |t - d| (fp64)
