@@ -403,6 +403,10 @@ def test_sim_collective_holds_for_the_modeled_time():
         assert us <= t <= us + 40, (us, t)
     # two 100 us emulations on two streams overlap (16 workgroups each: the chip has room for both)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for s in (s1, s2):       # first use of a stream (its hardware queue) outside the timed region
+        with torch.cuda.stream(s):
+            _lib.check(lib.hicgat_sim_collective(1.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     s1.wait_event(e0)

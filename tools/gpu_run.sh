@@ -100,6 +100,14 @@ for S in "$@"; do
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json sim-P8-rank0 \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 3 --warmup 2" \
         "$COMMIT" || exit $? ;;
+    pmc_wait_sim)
+      # where the waves of rank 0's share of the simulated 8-rank xagg step spend their cycles (one pass:
+      # 8 SQ + 1 GRBM counters; WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES)
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+        -d gpurun_out/${T}_${S} -o run --output-format csv -- \
+        python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 3 --warmup 2 --no-bare > gpurun_out/${T}_${S}.log 2>&1 || exit $?
+      python tools/pmc_summary.py gpurun_out/${T}_${S}/run_counter_collection.csv > gpurun_out/${T}_${S}.txt || exit $?
+      echo "pmc_wait_sim ok" ;;
     simrank|simrank_ag|simrank_xa|simrank_au)
       M=slab; [ "$S" = simrank_ag ] && M=allgather; [ "$S" = simrank_xa ] && M=xagg; [ "$S" = simrank_au ] && M=auto
       for P in 2 4 8; do
