@@ -393,6 +393,8 @@ def test_sim_collective_holds_for_the_modeled_time():
     from hicgat import _lib
     lib = _lib.lib()
     dev = torch.device("cuda", 0)
+    _lib.check(lib.hicgat_sim_collective(1.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")   # code load
+    torch.cuda.synchronize()
     for us in (15.0, 120.0):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
