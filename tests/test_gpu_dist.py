@@ -395,8 +395,12 @@ def test_sim_collective_holds_for_the_modeled_time():
     dev = torch.device("cuda", 0)
     _lib.check(lib.hicgat_sim_collective(1.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")   # code load
     torch.cuda.synchronize()
+    def busy():   # keeps the GPU ahead of the host, so the events time the device, not the launch gap
+        _lib.check(lib.hicgat_sim_collective(500.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
+
     for us in (15.0, 120.0):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        busy()
         e0.record()
         _lib.check(lib.hicgat_sim_collective(us, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
         e1.record()
@@ -410,6 +414,7 @@ def test_sim_collective_holds_for_the_modeled_time():
             _lib.check(lib.hicgat_sim_collective(1.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    busy()
     e0.record()
     s1.wait_event(e0)
     s2.wait_event(e0)
