@@ -170,6 +170,11 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16, NT1 = 32 / NW, NT2 = 16 / NW;   // 16-column tiles per wave: block 1 / block 2
+  // the waves' column tiles rotated by the workgroup (consecutive workgroups of an XCD -- blockIdx
+  // 8 apart -- start on different tiles): the CUs stream different weight rows at any moment instead
+  // of all requesting the same L2 lines together.  Which wave computes a column does not change its
+  // arithmetic (same k order): bitwise the unrotated kernel
+  const int rot = (blockIdx.x >> 3) & (NW - 1), ws = (wv + rot) & (NW - 1);
   static_assert(NW == 4 || NW == 8 || NW == 16, "NW: 4, 8 or 16 waves");
   // x rows (HEADS: xa^0 rows -> As, xa^1 rows -> Bs) -> LDS (rows past M: zeros)
   for (int e = tid; e < (HEADS ? 2 : 1) * RB * 128; e += 64 * NW) {
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
   if constexpr (HEADS) {
     static_assert(NW == 8 || NW == 16, "the head GEMMs take NW / 2 waves per head");
     constexpr int HW = NW / 2, NTH = 16 / HW;   // waves per head, 16-column tiles per wave
-    const int hd = wv / HW, n0 = 16 * NTH * (wv % HW);
+    const int hd = wv / HW, n0 = 16 * NTH * ((wv + rot) % HW);
     f32x4 acc[H][NTH];
 #pragma unroll
     for (int h = 0; h < H; ++h)
@@ -217,8 +222,8 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, NT1, 512>(As, XS, W1c, 16 * NT1 * wv, acc, lane);
-    store_tiles<RB, NT1>(acc, 16 * NT1 * wv, b1c, Bs, XS, Y1, 512, m0, M, lane);
+    mfma_rows<RB, NT1, 512>(As, XS, W1c, 16 * NT1 * ws, acc, lane);
+    store_tiles<RB, NT1>(acc, 16 * NT1 * ws, b1c, Bs, XS, Y1, 512, m0, M, lane);
   }
   __syncthreads();
   ln_rows<RB, 256, true, NW>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
@@ -230,8 +235,8 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, NT2, 256>(As, XS, W2c, 16 * NT2 * wv, acc, lane);
-    store_tiles<RB, NT2>(acc, 16 * NT2 * wv, b2c, Bs, XS, Y2, 256, m0, M, lane);
+    mfma_rows<RB, NT2, 256>(As, XS, W2c, 16 * NT2 * ws, acc, lane);
+    store_tiles<RB, NT2>(acc, 16 * NT2 * ws, b2c, Bs, XS, Y2, 256, m0, M, lane);
   }
   __syncthreads();
   ln_rows<RB, 128, true, NW>(Bs, XS, g2, be2, eps, As, XS, z2, st2, m0, M, wv, lane);
@@ -241,8 +246,8 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     f32x4 acc[H][1];
 #pragma unroll
     for (int h = 0; h < H; ++h) acc[h][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, 1, 128>(As, XS, W3, 16 * wv, acc, lane);
-    store_tiles<RB, 1>(acc, 16 * wv, b3, Bs, XS, y3, 64, m0, M, lane);
+    mfma_rows<RB, 1, 128>(As, XS, W3, 16 * ((wv + rot) & 3), acc, lane);
+    store_tiles<RB, 1>(acc, 16 * ((wv + rot) & 3), b3, Bs, XS, y3, 64, m0, M, lane);
   }
   __syncthreads();
   ln_rows<RB, 64, false, NW>(Bs, XS, g3, be3, eps, As, XS, z3, st3, m0, M, wv, lane);
@@ -421,6 +426,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
   const int slot = blockIdx.x;
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16;
+  const int rot = (blockIdx.x >> 3) & (NW - 1), ws = (wv + rot) & (NW - 1);   // as in tail_fwd_kernel
   // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
   for (int e = tid; e < RB * 64; e += 64 * NW) {
     const int r = e >> 6, c = e & 63;
@@ -442,8 +448,9 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < ND; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, ND, 64>(Bs, XS, W3, 128, 16 * ND * wv, acc, lane);
-    put_tiles<RB, ND>(acc, 16 * ND * wv, As, XS, nullptr, 0, m0, M, lane);
+    const int wd = (wv + rot) % WD;
+    mfma_rows_t<RB, ND, 64>(Bs, XS, W3, 128, 16 * ND * wd, acc, lane);
+    put_tiles<RB, ND>(acc, 16 * ND * wd, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
   ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, Rs, m0, M, wv, lane);
@@ -455,8 +462,8 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, NT2, 256>(Bs, XS, W2c, 256, 16 * NT2 * wv, acc, lane);
-    put_tiles<RB, NT2>(acc, 16 * NT2 * wv, As, XS, nullptr, 0, m0, M, lane);
+    mfma_rows_t<RB, NT2, 256>(Bs, XS, W2c, 256, 16 * NT2 * ws, acc, lane);
+    put_tiles<RB, NT2>(acc, 16 * NT2 * ws, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
   ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, Rs, m0, M, wv, lane);
@@ -468,8 +475,8 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, NT1, 512>(Bs, XS, W1c, 512, 16 * NT1 * wv, acc, lane);
-    put_tiles<RB, NT1>(acc, 16 * NT1 * wv, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
+    mfma_rows_t<RB, NT1, 512>(Bs, XS, W1c, 512, 16 * NT1 * ws, acc, lane);
+    put_tiles<RB, NT1>(acc, 16 * NT1 * ws, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
   }
   if constexpr (HEADS) {
     static_assert(NW == 8 || NW == 16, "the dxa GEMMs take NW / 2 waves per head");
@@ -511,7 +518,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     }
     __syncthreads();
     constexpr int HW = NW / 2, NTX = 32 / HW;   // waves per head, 16-column tiles per wave
-    const int hd = wv / HW, n0 = 16 * NTX * (wv % HW);
+    const int hd = wv / HW, n0 = 16 * NTX * ((wv + rot) % HW);
     f32x4 acc[H][NTX];
 #pragma unroll
     for (int h = 0; h < H; ++h)
