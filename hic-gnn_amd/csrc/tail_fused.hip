@@ -44,6 +44,7 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
                                           f32x4 (&acc)[RB / 16][NT], int lane) {
   constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
   static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
+  static_assert(R % 2 == 0, "the activation slots alternate with the group's parity");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
   const float *arow = As + li * lda + kq;
@@ -52,22 +53,29 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
   for (int q = 0; q < R; ++q)
 #pragma unroll
     for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * q);
+  // the activations of group g + 1 are read from LDS before group g's MFMAs (two register slots):
+  // the waves of a SIMD leave a barrier together, and a read waited on right before its MFMAs parks
+  // all of them at once while the matrix pipe idles
+  float4 a[2][H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) a[0][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda);
   HICGAT_TAIL_SCHED();   // the ring's loads stay issued here, ahead of their MFMAs
   for (int g0 = 0; g0 < G; g0 += R) {
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      const int g = g0 + q;
-      float4 a[H];
+      const int g = g0 + q, cur = q & 1;   // R even: g and q have the same parity
+      if (g + 1 < G) {
 #pragma unroll
-      for (int h = 0; h < H; ++h) a[h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * g);
+        for (int h = 0; h < H; ++h) a[cur ^ 1][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * (g + 1));
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int h = 0; h < H; ++h) {
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].x, b[q][t].x, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].y, b[q][t].y, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t].z, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t].w, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].x, b[q][t].x, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].y, b[q][t].y, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].z, b[q][t].z, acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t].w, acc[h][t], 0, 0, 0);
         }
       if (g + R < G) {
 #pragma unroll
@@ -275,6 +283,7 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
                                             int n0, f32x4 (&acc)[RB / 16][NT], int lane) {
   constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
   static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
+  static_assert(R % 2 == 0, "the activation slots alternate with the group's parity");
   const int li = lane & 15, kq = 4 * (lane >> 4);
   const float *wcol = W + (size_t)kq * ldw + n0 + li;
   const float *arow = As + li * lda + kq;
@@ -285,22 +294,26 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * q + j) * ldw + 16 * t];
+  float4 a[2][H];   // group g + 1's activations read before group g's MFMAs (as in mfma_rows)
+#pragma unroll
+  for (int h = 0; h < H; ++h) a[0][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda);
   HICGAT_TAIL_SCHED();
   for (int g0 = 0; g0 < G; g0 += R) {
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      const int g = g0 + q;
-      float4 a[H];
+      const int g = g0 + q, cur = q & 1;
+      if (g + 1 < G) {
 #pragma unroll
-      for (int h = 0; h < H; ++h) a[h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * g);
+        for (int h = 0; h < H; ++h) a[cur ^ 1][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * (g + 1));
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int h = 0; h < H; ++h) {
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].x, b[q][t][0], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].y, b[q][t][1], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].z, b[q][t][2], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h].w, b[q][t][3], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].x, b[q][t][0], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].y, b[q][t][1], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].z, b[q][t][2], acc[h][t], 0, 0, 0);
+          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t][3], acc[h][t], 0, 0, 0);
         }
       if (g + R < G) {
 #pragma unroll
