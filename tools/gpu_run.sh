@@ -100,6 +100,11 @@ for S in "$@"; do
       python tools/pmc_mfma.py gpurun_out/${T}_${S}/run_counter_collection.csv x gpurun_out/${T}_${S}.json sim-P8-rank0 \
         "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -- python bench.py --simulate-world 8 --sim-rank 0 --dist-mode xagg --steps 3 --warmup 2" \
         "$COMMIT" || exit $? ;;
+    stamps)
+      # per-phase cycles of the one-kernel tail forward / backward (diagnostic build libhicgat_stamps.so,
+      # made on the CPU by `python tools/tail_stamps.py build`)
+      timeout -k 10 300 python tools/tail_stamps.py run 8 > gpurun_out/${T}_stamps.txt 2>&1 || exit $?
+      cat gpurun_out/${T}_stamps.txt | grep -v "^\[" ;;
     pmc_wait_sim)
       # where the waves of rank 0's share of the simulated 8-rank xagg step spend their cycles (one pass:
       # 8 SQ + 1 GRBM counters; WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES)
