@@ -37,28 +37,33 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kTailRing = 4;   // weight groups in flight per wave (the prefetch ring's depth)
 
 // acc[h][t] (h < RB/16 row halves, t < NT) += A[RB x K] (LDS, row stride lda) x B^T, B = the weight
-// rows n0 + 16t + (l & 15) (K columns).  The weights of group g + R are loaded right after group g's
-// MFMAs, so R - 1 groups of MFMAs cover every load (a ring of R float4 sets, R = kTailRing).
+// rows n0 + 16t + (l & 15) (K columns), in k super-groups of 32: lane l loads floats
+// 32G + 8(l >> 4) .. + 7 of its row as two float4, so one load pair covers whole 128-B lines of 16
+// rows (a 16-deep group per load read half lines, and the other half came back from L2 a group
+// later: the forward GEMMs ran at half the backward's MFMA rate, tools/tail_stamps.py).  The MFMA's
+// four k slots of step s of half e are 32G + 8(l >> 4) + 4e + s.  The weights of super-group G + R
+// are loaded right after G's MFMAs (a ring of R = 2 super-groups: 64 k ahead).
 template <int RB, int NT, int K>
 __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
                                           f32x4 (&acc)[RB / 16][NT], int lane) {
-  constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
-  static_assert(G % R == 0, "K: a multiple of 16 * ring depth");
-  static_assert(R % 2 == 0, "the activation slots alternate with the group's parity");
-  const int li = lane & 15, kq = 4 * (lane >> 4);
+  constexpr int G = K / 32, H = RB / 16, R = 2;
+  static_assert(K % 64 == 0 && G % R == 0, "K: a multiple of 64");
+  const int li = lane & 15, kq = 8 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
   const float *arow = As + li * lda + kq;
-  float4 b[R][NT];
+  float4 b[R][NT][2];
 #pragma unroll
   for (int q = 0; q < R; ++q)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * q);
-  // the activations of group g + 1 are read from LDS before group g's MFMAs (two register slots):
-  // the waves of a SIMD leave a barrier together, and a read waited on right before its MFMAs parks
-  // all of them at once while the matrix pipe idles
-  float4 a[2][H];
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-  for (int h = 0; h < H; ++h) a[0][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda);
+      for (int e = 0; e < 2; ++e) b[q][t][e] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 32 * q + 4 * e);
+  // the activations of super-group g + 1 are read from LDS before g's MFMAs (two register slots)
+  float4 a[2][H][2];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) a[0][h][e] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 4 * e);
   HICGAT_TAIL_SCHED();   // the ring's loads stay issued here, ahead of their MFMAs
   for (int g0 = 0; g0 < G; g0 += R) {
 #pragma unroll
@@ -66,20 +71,28 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
       const int g = g0 + q, cur = q & 1;   // R even: g and q have the same parity
       if (g + 1 < G) {
 #pragma unroll
-        for (int h = 0; h < H; ++h) a[cur ^ 1][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * (g + 1));
+        for (int h = 0; h < H; ++h)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            a[cur ^ 1][h][e] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 32 * (g + 1) + 4 * e);
       }
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+      for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int h = 0; h < H; ++h) {
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].x, b[q][t].x, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].y, b[q][t].y, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].z, b[q][t].z, acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t].w, acc[h][t], 0, 0, 0);
-        }
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h][e].x, b[q][t][e].x, acc[h][t], 0, 0, 0);
+            acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h][e].y, b[q][t][e].y, acc[h][t], 0, 0, 0);
+            acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h][e].z, b[q][t][e].z, acc[h][t], 0, 0, 0);
+            acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h][e].w, b[q][t][e].w, acc[h][t], 0, 0, 0);
+          }
       if (g + R < G) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) b[q][t] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 16 * (g + R));
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            b[q][t][e] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 32 * (g + R) + 4 * e);
       }
       HICGAT_TAIL_SCHED();
     }
@@ -306,15 +319,23 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
 #pragma unroll
         for (int h = 0; h < H; ++h) a[cur ^ 1][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda + 16 * (g + 1));
       }
+      // k-step outer, tiles inner (as in mfma_rows)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int h = 0; h < H; ++h) {
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].x, b[q][t][0], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].y, b[q][t][1], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].z, b[q][t][2], acc[h][t], 0, 0, 0);
-          acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t][3], acc[h][t], 0, 0, 0);
-        }
+        for (int h = 0; h < H; ++h) acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].x, b[q][t][0], acc[h][t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int h = 0; h < H; ++h) acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].y, b[q][t][1], acc[h][t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int h = 0; h < H; ++h) acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].z, b[q][t][2], acc[h][t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int h = 0; h < H; ++h) acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t][3], acc[h][t], 0, 0, 0);
       if (g + R < G) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
