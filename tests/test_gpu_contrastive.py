@@ -281,14 +281,23 @@ def test_contrastive_train_loop_tracks_oracle():
     # teacher forcing
     opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
     params = dict(model.named_parameters())
-    wl = wg = 0.0
+    # the L1 loss drives residuals d - t to 0 as it trains: a pair within rounding of its tie has its
+    # sign() decided by the last bits of d (the kernel's 1-2 ulp distance vs the oracle's), and its
+    # whole +-0.1/M term flips -- such states are held to 1e-3, the others to 2e-4
+    wl = wg = wg_tie = 0.0
+    ties = []
+    t64 = truth_h.to(DEV)
     for state, l_ref, g_ref in states:
         with torch.no_grad():
             for k, v in state.items():
                 params[k].copy_(v)
         opt.zero_grad()
-        val, st, _ = model.loss(data.x, data.edge_index, tr, "contrastive")
+        val, st, coords = model.loss(data.x, data.edge_index, tr, "contrastive")
         val.backward()
+        cd = coords.detach().double()
+        d = torch.cdist(cd, cd, compute_mode="donot_use_mm_for_euclid_dist")
+        near = ((d - t64).abs() <= 1e-6 * torch.maximum(d, t64)).triu(1)
+        ties.append(int(near.sum()))
         wl = max(wl, abs(float(st[10]) - l_ref) / l_ref)
         gscale = max(float(v.abs().max()) for v in g_ref.values())
         for k, gr in g_ref.items():
@@ -296,12 +305,16 @@ def test_contrastive_train_loop_tracks_oracle():
             if float(gr.abs().max()) < 1e-3 * gscale:
                 assert float(gd.abs().max()) < 1e-3 * gscale, k
                 continue
-            wg = max(wg, _rel(gd, gr))
+            if ties[-1]:
+                wg_tie = max(wg_tie, _rel(gd, gr))
+            else:
+                wg = max(wg, _rel(gd, gr))
     np.set_printoptions(precision=2, linewidth=200)
-    print(f"teacher-forced over {K} states: loss rel {wl:.2e}, grad rel {wg:.2e}")
+    print(f"teacher-forced over {K} states: loss rel {wl:.2e}, grad rel {wg:.2e} (states with near-tie pairs: "
+          f"{wg_tie:.2e}); near-tie pairs per state {ties}")
     print("free-running rel", rel)
     print("oracle spread   ", spread)
-    assert wl < 1e-5 and wg < 2e-4, (wl, wg)
+    assert wl < 1e-5 and wg < 2e-4 and wg_tie < 1e-3, (wl, wg, wg_tie)
     assert rel[0] < 1e-5 and rel[1] < 1e-5, rel[:3]
     run_rel, run_spread = np.maximum.accumulate(rel), np.maximum.accumulate(spread)
     ahead = run_spread[np.minimum(np.arange(len(spread)) + 2, len(spread) - 1)]
