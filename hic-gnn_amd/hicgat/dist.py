@@ -68,12 +68,12 @@ def resolve_mode(mode, P):
         return "xagg" if P >= AUTO_XAGG_MIN_P else "slab"
     return mode
 # workgroups of the xagg step's side-stream grouped weight-gradient launch (beside the edge pass,
-# which needs the CUs: the grouped launch's default 512 would crowd it)
-XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "128"))
-# what runs on that side stream: "all" (the tail's and the heads' weight gradients, then the whole
-# flat-gradient all-reduce; after the edge pass only g is reduced) or "tail" (the tail's gradients and
-# their bucket; the heads' dW, the finish and the GATConv bucket after the edge pass)
-XAGG_SIDE = os.environ.get("HICGAT_XAGG_SIDE", "all")
+# which needs the CUs: the grouped launch's default 512 would crowd it).  Rank 0 of the simulated
+# 8-rank step, emulated collectives, two sweeps (profiles/r05j_sim_ab.txt): 128: 0.477 / 0.475,
+# 192: 0.472 / 0.474, 256: 0.473 / 0.469, 384: 0.475 / 0.477, 512: 0.479 / 0.477, 1024: 0.487 /
+# 0.489 ms; the tail's gradients and bucket alone on the side stream (the heads' dW and the GATConv
+# bucket after the edge pass): 0.495 / 0.497 (removed)
+XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "256"))
 
 
 def _null():
@@ -691,26 +691,12 @@ class ShardedTrainer:
                 side.wait_stream(torch.cuda.current_stream())
             g_jobs = [("c", self.gpart, self.g_src, False),
                       ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)]
-            tail_only = XAGG_SIDE == "tail" and self.grad_split is not None
             with torch.cuda.stream(side) if side is not None else _null():
-                keep = ops.grouped_flush(K, [] if tail_only else heads, target_wgs=XAGG_SIDE_WGS)
-                if tail_only:
-                    self.comm.all_reduce(self.opt.grad[self.grad_split:], name="grad_all_reduce_tail_bucket")
-                else:
-                    # every gradient but the attention vectors' (0 until the finish) and W's att (x) g term
-                    self.comm.all_reduce(self.opt.grad, name="grad_all_reduce")
+                keep = ops.grouped_flush(K, heads, target_wgs=XAGG_SIDE_WGS)
+                # every gradient but the attention vectors' (0 until the finish) and W's att (x) g term
+                self.comm.all_reduce(self.opt.grad, name="grad_all_reduce")
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                             self.gpart, xa2=self.X4[:, 1])
-            if tail_only:
-                # the heads' dW with g after the edge pass, the finish per rank, the GATConv's bucket
-                ops.grouped_flush(K, heads + g_jobs)
-                K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
-                                    self.att_r.grad.view(-1))
-                self.comm.all_reduce(self.opt.grad[:self.grad_split], name="grad_all_reduce_gat_bucket")
-                if side is not None:
-                    torch.cuda.current_stream().wait_stream(side)
-                del keep
-                return
             ops.grouped_flush(K, g_jobs)
             self.comm.all_reduce(self.gsd, name="g_all_reduce")
             if side is not None:
