@@ -408,11 +408,18 @@ __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
   }
   red[threadIdx.x] = s;
   __syncthreads();
-  if (g != 0 || c >= J.cols) return;
-  for (int k = 1; k < ng; ++k) {     // the row groups in order
-    const float4 v = red[(k << J.lg) + lane];
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  // the row groups combined by a fixed pairwise tree (group g adds group g + h, h = ng/2 ... 1):
+  // log2(ng) LDS rounds instead of a chain of ng - 1 dependent LDS reads (128 for the tall weighted
+  // jobs); one fixed order, bitwise reproducible
+  for (int h = ng >> 1; h > 0; h >>= 1) {
+    if (g < h) {
+      const float4 v = red[((g + h) << J.lg) + lane];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      red[threadIdx.x] = s;
+    }
+    __syncthreads();
   }
+  if (g != 0 || c >= J.cols) return;
   float *d = J.dst + c;
   const float o[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
