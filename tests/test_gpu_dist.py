@@ -407,24 +407,34 @@ def test_sim_collective_holds_for_the_modeled_time():
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) * 1e3
         assert us <= t <= us + 40, (us, t)
-    # two 100 us emulations on two streams overlap (16 workgroups each: the chip has room for both)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    for s in (s1, s2):       # first use of a stream (its hardware queue) outside the timed region
-        with torch.cuda.stream(s):
-            _lib.check(lib.hicgat_sim_collective(1.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    busy()
-    e0.record()
-    s1.wait_event(e0)
-    s2.wait_event(e0)
-    for s in (s1, s2):
-        with torch.cuda.stream(s):
-            _lib.check(lib.hicgat_sim_collective(100.0, 16, 256, _lib.stream(dev)), "hicgat_sim_collective")
-    torch.cuda.current_stream().wait_stream(s1)
-    torch.cuda.current_stream().wait_stream(s2)
-    e1.record()
-    torch.cuda.synchronize()
-    assert e0.elapsed_time(e1) * 1e3 < 170
+    # two 100 us emulations on two streams overlap (16 workgroups each: the chip has room for both).
+    # In a fresh process: HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES = 4 on the
+    # box), and after the suite's earlier tests have made many streams, two new ones may share a
+    # queue and run in order (0.238 ms for the pair, r05m)
+    import subprocess
+    code = (
+        "import sys, torch\n"
+        f"sys.path[:0] = [{os.path.dirname(HERE)!r}, {os.path.join(os.path.dirname(HERE), 'hic-gnn_amd')!r}]\n"
+        "from hicgat import _lib\n"
+        "lib = _lib.lib(); dev = torch.device('cuda', 0)\n"
+        "def sim(us):\n"
+        "    _lib.check(lib.hicgat_sim_collective(us, 16, 256, _lib.stream(dev)), 'hicgat_sim_collective')\n"
+        "s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()\n"
+        "sim(1.0)\n"
+        "for s in (s1, s2):\n"
+        "    with torch.cuda.stream(s): sim(1.0)\n"
+        "torch.cuda.synchronize()\n"
+        "e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)\n"
+        "sim(500.0)\n"
+        "e0.record(); s1.wait_event(e0); s2.wait_event(e0)\n"
+        "for s in (s1, s2):\n"
+        "    with torch.cuda.stream(s): sim(100.0)\n"
+        "torch.cuda.current_stream().wait_stream(s1); torch.cuda.current_stream().wait_stream(s2)\n"
+        "e1.record(); torch.cuda.synchronize()\n"
+        "print(e0.elapsed_time(e1) * 1e3)\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    t = float(out.stdout.strip().splitlines()[-1])
+    assert t < 170, t
     for bad in ((-1.0, 16, 256), (10.0, 0, 256), (10.0, 16, 100), (10.0, 16, 2048)):
         assert lib.hicgat_sim_collective(*bad, None) == -1, bad
