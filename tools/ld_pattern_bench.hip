@@ -1,0 +1,74 @@
+// Per-CU load rate of the one-kernel tail's weight-stream address pattern against a contiguous one
+// (diagnostic, not part of the library).  A workgroup of 16 waves streams a [512 x 512] fp32 matrix
+// once per pass, 4 passes, each wave reading its 32 rows, in one of two lane -> address maps:
+//   rows : lane (li = lane & 15, j = lane >> 4) loads row n0 + li, k 8j + 4e .. +3  (the tail's map:
+//          16 rows per instruction, 64 B of each)
+//   flat : lane loads the 16 B at 16 * lane of a contiguous 1 KB block (a pre-permuted copy)
+// Build: hipcc -O3 --offload-arch=gfx950 tools/ld_pattern_bench.hip -o /tmp/ldb
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void ld_kernel(const float *__restrict__ W, float *__restrict__ sink, long long *cyc) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, j = lane >> 4;
+  constexpr int K = 512;
+  const int n0 = 32 * ((wv + blockIdx.x) & 15);   // wave's 32 rows (rotated by workgroup)
+  float acc = 0.f;
+  __syncthreads();
+  const long long t0 = clock64();
+  for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll 2
+    for (int g = 0; g < K / 32; ++g) {
+      float4 v[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float *p;
+          if (MODE == 0)
+            p = W + (size_t)(n0 + 16 * t + li) * K + 32 * g + 8 * j + 4 * e;
+          else   // the same 16 KB per (wave, g) as 4 contiguous 1 KB blocks
+            p = W + (((size_t)(n0 / 16 + t) * (K / 32) + g) * 2 + e) * 256 + 4 * lane;
+          v[t][e] = *reinterpret_cast<const float4 *>(p);
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc += (v[t][e].x + v[t][e].y) + (v[t][e].z + v[t][e].w);
+    }
+  }
+  __syncthreads();
+  const long long t1 = clock64();
+  if (acc == -1.5e-38f) sink[threadIdx.x] = acc;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+int main() {
+  const int K = 512, N = 512;
+  float *W, *sink;
+  long long *cyc;
+  hipMalloc(&W, (size_t)N * K * 4);
+  hipMemset(W, 0, (size_t)N * K * 4);
+  hipMalloc(&sink, 4096);
+  hipMalloc(&cyc, 4096 * 8);
+  for (int blocks : {1, 8, 169, 256}) {
+    for (int mode = 0; mode < 2; ++mode) {
+      for (int rep = 0; rep < 3; ++rep) {
+        if (mode == 0) hipLaunchKernelGGL(ld_kernel<0>, dim3(blocks), dim3(1024), 0, 0, W, sink, cyc);
+        else hipLaunchKernelGGL(ld_kernel<1>, dim3(blocks), dim3(1024), 0, 0, W, sink, cyc);
+      }
+      hipDeviceSynchronize();
+      std::vector<long long> c(blocks);
+      hipMemcpy(c.data(), cyc, blocks * 8, hipMemcpyDeviceToHost);
+      double s = 0;
+      for (auto x : c) s += (double)x;
+      s /= blocks;
+      const double bytes = 4.0 * N * K * 4;   // 4 passes of the matrix per workgroup
+      printf("blocks %3d  %-4s  %9.0f cycles per workgroup  %6.1f B/clk per CU\n", blocks, mode ? "flat" : "rows", s,
+             bytes / s);
+    }
+  }
+  return 0;
+}

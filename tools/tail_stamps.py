@@ -2,6 +2,7 @@
 
   python tools/tail_stamps.py build        # here (CPU): hic-gnn_amd/hicgat/libhicgat_stamps.so
   python tools/tail_stamps.py run [world]  # GPU box: rank 0 of the simulated world-rank xagg step
+  python tools/tail_stamps.py rows M ...   # GPU box: the plain fused tail (no head GEMMs) on M random rows
 
 ``build`` copies csrc/ to /tmp, inserts a stamp (``s_memtime`` by wave 0 of every workgroup, stored
 with a per-lane vector store into a debug buffer nothing else reads) at the entry of
@@ -137,7 +138,62 @@ def run(world):
             print(f"  phase {k:2d}: {v:9.0f} cycles  {v / med.sum():6.1%}")
 
 
+def rows(ms):
+    """The fused tail without the head GEMMs on M random rows, forward + backward, for each M: the
+    per-phase cycles at M / 16 workgroups -- few workgroups (no chip-wide contention for L2 / fabric)
+    against the 169 of a P = 8 rank tell a per-CU bound from a shared one."""
+    os.environ["HICGAT_LIB"] = LIB
+    os.environ["HICGAT_FUSED_TAIL_MIN_M"] = "1"
+    sys.path[:0] = [ROOT, PKG]
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import hicgat
+    from hicgat import _lib, ops
+    lib = _lib.load()
+    fn = lib.hicgat_debug_set_stamps
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(dev)
+    for M in ms:
+        x = torch.relu(torch.randn(M, 512, device=dev)).requires_grad_(True)
+        dc = torch.randn(M, 3, device=dev)
+        assert ops.fused_tail_ok(model, x), M
+
+        def step():
+            model.zero_grad(set_to_none=False)
+            ops.fused_tail(model, x).backward(dc)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        nwg = (M + 15) // 16
+        buf = torch.zeros(nwg * MAXS * 64, dtype=torch.int64, device=dev)
+        assert fn(ctypes.c_void_p(buf.data_ptr())) == 0
+        stamps = []
+        for _ in range(5):
+            buf.zero_()
+            step()
+            torch.cuda.synchronize()
+            stamps.append(buf.view(nwg, MAXS, 64)[:, :, 0].cpu().numpy().astype(np.float64))
+        assert fn(None) == 0
+        st = np.stack(stamps)
+        print(f"M = {M}: {nwg} workgroups of 16 rows")
+        for name, base in BASE.items():
+            blk = st[:, :, base:base + MAXS // 2]
+            n = int((blk[0, 0] > 0).sum())
+            d = np.diff(blk[:, :, :n], axis=2)
+            med = np.median(d.reshape(-1, n - 1), axis=0)
+            span = np.median(blk[:, :, n - 1] - blk[:, :, 0])
+            print(f"  {name}: median span {span:.0f} cycles; phases " + " ".join(f"{v:.0f}" for v in med))
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "rows":
+        rows([int(a) for a in sys.argv[2:]])
+        sys.exit(0)
     if sys.argv[1] == "build":
         build()
     else:
