@@ -43,7 +43,15 @@ constexpr int kTailRing = 4;   // weight groups in flight per wave (the prefetch
 // later: the forward GEMMs ran at half the backward's MFMA rate, tools/tail_stamps.py).  The MFMA's
 // four k slots of step s of half e are 32G + 8(l >> 4) + 4e + s.  The weights of super-group G + R
 // are loaded right after G's MFMAs (a ring of R = 2 super-groups: 64 k ahead).
-template <int RB, int NT, int K>
+//
+// PK: W is the PACKED copy of the weight (hicgat_tail_pack): the two float4 of lane l for rows
+// 16b .. 16b + 15 and super-group G sit at ((b * (K / 32) + G) * 2 + e) * 256 + 4l, so each load
+// instruction reads 1 KB contiguous.  The row-major rows put the 64 lanes of one load on 16 rows;
+// the vector memory path then serves 16 B per clock per CU where contiguous quads of lanes get
+// 64 B (tools/ld_pattern_bench.hip: 16.0 vs 63.5 B/clk), and the weight stream, not the MFMAs, set
+// every GEMM phase's pace (half the MFMA rate, profiles/r05rs_tail_bound.txt).  Same values in the
+// same registers: bitwise the row-major form.
+template <int RB, int NT, int K, bool PK = false>
 __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda, const float *__restrict__ W, int n0,
                                           f32x4 (&acc)[RB / 16][NT], int lane) {
   constexpr int G = K / 32, H = RB / 16, R = 2;
@@ -51,13 +59,20 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
   const int li = lane & 15, kq = 8 * (lane >> 4);
   const float *wrow = W + (size_t)(n0 + li) * K + kq;
   const float *arow = As + li * lda + kq;
+  // weight float4 e of super-group g for tile t (row-major or packed)
+  auto wld = [&](int t, int g, int e) -> float4 {
+    if constexpr (PK)
+      return *reinterpret_cast<const float4 *>(W + (((size_t)(n0 / 16 + t) * G + g) * 2 + e) * 256 + 4 * lane);
+    else
+      return *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 32 * g + 4 * e);
+  };
   float4 b[R][NT][2];
 #pragma unroll
   for (int q = 0; q < R; ++q)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) b[q][t][e] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 32 * q + 4 * e);
+      for (int e = 0; e < 2; ++e) b[q][t][e] = wld(t, q, e);
   // the activations of super-group g + 1 are read from LDS before g's MFMAs (two register slots)
   float4 a[2][H][2];
 #pragma unroll
@@ -91,8 +106,7 @@ __device__ __forceinline__ void mfma_rows(const float *__restrict__ As, int lda,
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int e = 0; e < 2; ++e)
-            b[q][t][e] = *reinterpret_cast<const float4 *>(wrow + (size_t)16 * t * K + 32 * (g + R) + 4 * e);
+          for (int e = 0; e < 2; ++e) b[q][t][e] = wld(t, g + R, e);
       }
       HICGAT_TAIL_SCHED();
     }
@@ -174,7 +188,7 @@ constexpr int kTailWaves = 16;   // 16: 0.438 / 0.440 vs 0.448 ms per P = 8 rank
 // workgroups, 64 VGPRs at NW = 16) and sinks every weight load next to its MFMAs -- the prefetch ring
 // collapses to one group in flight
 #define HICGAT_TAIL_WPE __attribute__((amdgpu_waves_per_eu(kTailWaves / 4, kTailWaves / 4)))
-template <int RB, int NW, bool HEADS = false>
+template <int RB, int NW, bool HEADS = false, bool PK = false>
 __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NTH; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, NTH, 512>(hd ? Bs : As, XS, Wh + (size_t)hd * 256 * 512, n0, acc, lane);
+    mfma_rows<RB, NTH, 512, PK>(hd ? Bs : As, XS, Wh + (size_t)hd * 256 * 512, n0, acc, lane);
     __syncthreads();   // every wave is done with xa^0 / xa^1 before As takes relu(out)
     const int li = lane & 15, r0 = 4 * (lane >> 4);
 #pragma unroll
@@ -243,7 +257,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, NT1, 512>(As, XS, W1c, 16 * NT1 * ws, acc, lane);
+    mfma_rows<RB, NT1, 512, PK>(As, XS, W1c, 16 * NT1 * ws, acc, lane);
     store_tiles<RB, NT1>(acc, 16 * NT1 * ws, b1c, Bs, XS, Y1, 512, m0, M, lane);
   }
   __syncthreads();
@@ -256,7 +270,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<RB, NT2, 256>(As, XS, W2c, 16 * NT2 * ws, acc, lane);
+    mfma_rows<RB, NT2, 256, PK>(As, XS, W2c, 16 * NT2 * ws, acc, lane);
     store_tiles<RB, NT2>(acc, 16 * NT2 * ws, b2c, Bs, XS, Y2, 256, m0, M, lane);
   }
   __syncthreads();
@@ -291,7 +305,10 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
 // acc[h][t] += A[RB x K] (LDS) x B, B[k][n] = W[k][n] (W [K][ldw] row-major: dx = dy W): lane l reads
 // W[16g + 4(l >> 4) + s][n0 + 16t + (l & 15)] -- 16 consecutive floats per k across the lanes -- with
 // the weights of group g + 4 loaded after group g's MFMAs (ring of 4).
-template <int RB, int NT, int K>
+// PK: W is the packed copy (hicgat_tail_pack): lane l's four values of 16-row group g and column
+// tile c (16 columns) are one float4 at ((g * (ldw / 16) + c) * 64 + l) * 4 -- 1 KB contiguous per
+// load instead of four 4-B loads per lane over 4 rows; same values, bitwise the row-major form.
+template <int RB, int NT, int K, bool PK = false>
 __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int lda, const float *__restrict__ W, int ldw,
                                             int n0, f32x4 (&acc)[RB / 16][NT], int lane) {
   constexpr int G = K / 16, H = RB / 16, R = G < kTailRing ? G : kTailRing;
@@ -301,12 +318,20 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
   const float *wcol = W + (size_t)kq * ldw + n0 + li;
   const float *arow = As + li * lda + kq;
   float b[R][NT][4];
+  // the four weights of lane l for 16-row group g and tile t (row-major or packed)
+  auto wld = [&](float (&d)[4], int t, int g) {
+    if constexpr (PK) {
+      const float4 v = *reinterpret_cast<const float4 *>(W + (((size_t)g * (ldw / 16) + n0 / 16 + t) * 64 + lane) * 4);
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = wcol[(size_t)(16 * g + j) * ldw + 16 * t];
+    }
+  };
 #pragma unroll
   for (int q = 0; q < R; ++q)
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * q + j) * ldw + 16 * t];
+    for (int t = 0; t < NT; ++t) wld(b[q][t], t, q);
   float4 a[2][H];   // group g + 1's activations read before group g's MFMAs (as in mfma_rows)
 #pragma unroll
   for (int h = 0; h < H; ++h) a[0][h] = *reinterpret_cast<const float4 *>(arow + h * 16 * lda);
@@ -338,9 +363,7 @@ __device__ __forceinline__ void mfma_rows_t(const float *__restrict__ As, int ld
         for (int h = 0; h < H; ++h) acc[h][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][h].w, b[q][t][3], acc[h][t], 0, 0, 0);
       if (g + R < G) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) b[q][t][j] = wcol[(size_t)(16 * (g + R) + j) * ldw + 16 * t];
+        for (int t = 0; t < NT; ++t) wld(b[q][t], t, g + R);
       }
       HICGAT_TAIL_SCHED();
     }
@@ -440,7 +463,7 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
 // with delta^h = <dout^h, Y0^h - b^h> into row_stats[8r + 4 + h] (S3 moved to [6:8], as
 // xagg_rows_bwd does), then dxa^h = dout^h W_h ([RB x 256] [256 x 512], waves 0-3 head 0, 4-7 head 1)
 // into dxa [M][1024].
-template <int RB, int NW, bool HEADS = false>
+template <int RB, int NW, bool HEADS = false, bool PK = false>
 __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
     const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
@@ -496,7 +519,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT2; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, NT2, 256>(Bs, XS, W2c, 256, 16 * NT2 * ws, acc, lane);
+    mfma_rows_t<RB, NT2, 256, PK>(Bs, XS, W2c, 256, 16 * NT2 * ws, acc, lane);
     put_tiles<RB, NT2>(acc, 16 * NT2 * ws, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
@@ -509,7 +532,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, NT1, 512>(Bs, XS, W1c, 512, 16 * NT1 * ws, acc, lane);
+    mfma_rows_t<RB, NT1, 512, PK>(Bs, XS, W1c, 512, 16 * NT1 * ws, acc, lane);
     put_tiles<RB, NT1>(acc, 16 * NT1 * ws, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
   }
   if constexpr (HEADS) {
@@ -558,14 +581,85 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int t = 0; t < NTX; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows_t<RB, NTX, 256>(As + 256 * hd, XS, Wh + (size_t)hd * 256 * 512, 512, n0, acc, lane);
+    mfma_rows_t<RB, NTX, 256, PK>(As + 256 * hd, XS, Wh + (size_t)hd * 256 * 512, 512, n0, acc, lane);
     put_tiles<RB, NTX>(acc, n0, nullptr, 0, dxa + 512 * hd, 1024, m0, M, lane);
   }
+}
+
+// ---- packed weight copies (hicgat_tail_pack) ------------------------------------------------------
+// Float offsets in the pack buffer: the forward (mfma_rows) layouts of W1c [512][512], W2c [256][256]
+// and Wh [512][512], then their backward (mfma_rows_t) layouts.
+constexpr int64_t kPackF1 = 0, kPackF2 = kPackF1 + 512 * 512, kPackFH = kPackF2 + 256 * 256,
+                  kPackB1 = kPackFH + 512 * 512, kPackB2 = kPackB1 + 512 * 512, kPackBH = kPackB2 + 256 * 256,
+                  kPackTotal = kPackBH + 512 * 512;
+struct PackJob {
+  const float *src;   // [R][C] row-major
+  float *dst;
+  int R, C, bwd, blk0;
+};
+struct PackJobs {
+  PackJob j[6];
+  int n;
+};
+// one thread per float4 of the packed copy (coalesced writes; the reads gather 4 floats)
+__global__ __launch_bounds__(256) void tail_pack_kernel(const PackJobs jobs) {
+  int q = 0;
+#pragma unroll
+  for (int k = 1; k < 6; ++k) q += (k < jobs.n && (int)blockIdx.x >= jobs.j[k].blk0) ? 1 : 0;
+  const PackJob &J = jobs.j[q];
+  const int64_t o4 = (int64_t)(blockIdx.x - J.blk0) * 256 + threadIdx.x;
+  if (o4 >= (int64_t)J.R * J.C / 4) return;
+  const int L = (int)(o4 & 63);
+  float4 v;
+  if (!J.bwd) {   // mfma_rows: ((b * G + g) * 2 + e) * 256 + 4L  <-  row 16b + (L & 15), cols 32g + 8(L >> 4) + 4e ..
+    const int G = J.C / 32;
+    const int64_t chunk = o4 >> 6;
+    const int e = (int)(chunk & 1), g = (int)((chunk >> 1) % G), b = (int)((chunk >> 1) / G);
+    v = *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * b + (L & 15)) * J.C + 32 * g + 8 * (L >> 4) + 4 * e);
+  } else {        // mfma_rows_t: ((g * (C / 16) + c) * 64 + L) * 4 + s  <-  row 16g + 4(L >> 4) + s, col 16c + (L & 15)
+    const int64_t blk = o4 >> 6;
+    const int g = (int)(blk / (J.C / 16)), c = (int)(blk % (J.C / 16));
+    const float *p = J.src + (size_t)(16 * g + 4 * (L >> 4)) * J.C + 16 * c + (L & 15);
+    v = make_float4(p[0], p[J.C], p[2 * (size_t)J.C], p[3 * (size_t)J.C]);
+  }
+  reinterpret_cast<float4 *>(J.dst)[o4] = v;
 }
 
 }  // namespace hicgat
 
 using namespace hicgat;
+
+extern "C" size_t hicgat_tail_pack_bytes(void) { return (size_t)kPackTotal * sizeof(float); }
+
+extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
+                                hicgat_stream_t stream) {
+  if (!W1c || !W2c || !pack) return HICGAT_EINVAL;
+  if (pack_bytes < hicgat_tail_pack_bytes()) return HICGAT_EINVAL;
+  if (((uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)Wh | (uintptr_t)pack) & 15) return HICGAT_EUNSUPPORTED;
+  float *pk = static_cast<float *>(pack);
+  PackJobs pj;
+  pj.n = 0;
+  int blk = 0;
+  auto add = [&](const float *src, int64_t off, int R, int C, int bwd) {
+    PackJob &J = pj.j[pj.n++];
+    J.src = src;
+    J.dst = pk + off;
+    J.R = R;
+    J.C = C;
+    J.bwd = bwd;
+    J.blk0 = blk;
+    blk += (R * C / 4 + 255) / 256;
+  };
+  add(W1c, kPackF1, 512, 512, 0);
+  add(W2c, kPackF2, 256, 256, 0);
+  if (Wh) add(Wh, kPackFH, 512, 512, 0);
+  add(W1c, kPackB1, 512, 512, 1);
+  add(W2c, kPackB2, 256, 256, 1);
+  if (Wh) add(Wh, kPackBH, 512, 512, 1);
+  hipLaunchKernelGGL(tail_pack_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, pj);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
 
 namespace {
 struct TailHeads {   // the HEADS operands of the head-fused forms (all null: the plain tail)
@@ -575,12 +669,37 @@ struct TailHeads {   // the HEADS operands of the head-fused forms (all null: th
   float *Y0 = nullptr, *O = nullptr;
 };
 
+template <bool HEADS, bool PK>
+int tail_fwd_go(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c, const float *g1,
+                const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2, const float *W3,
+                const float *b3, const float *g3, const float *be3, const float *W4, const float *b4, float eps,
+                float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2, float *y3, float *st3, float *z3,
+                float *coords, const float *Wh, const TailHeads &hh, hipStream_t stream) {
+  // 16 rows per workgroup (66 KiB of dynamic LDS: two workgroups per CU).  A 32-row form (132 KiB,
+  // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
+  // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
+  // with one workgroup per CU every phase's latency is exposed.
+  constexpr int RB = 16, NW = kTailWaves;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS, PK>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
+  if (!attr) return HICGAT_ELAUNCH;
+  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, HEADS, PK>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+                     (size_t)2 * RB * XS * sizeof(float), stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3,
+                     b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1, Y2,
+                     reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords, hh.xa_hs,
+                     Wh, hh.bh, hh.Y0, hh.O);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 template <bool HEADS>
 int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c, const float *g1,
                     const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2,
                     const float *W3, const float *b3, const float *g3, const float *be3, const float *W4,
                     const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2,
-                    float *y3, float *st3, float *z3, float *coords, const TailHeads &hh, hipStream_t stream) {
+                    float *y3, float *st3, float *z3, float *coords, const TailHeads &hh, const void *pack,
+                    hipStream_t stream) {
   if (M < 0 || ldx < 512 || (ldx & 3)) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
   const void *ps[] = {x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4,
@@ -590,24 +709,16 @@ int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const 
   if (HEADS && (!hh.Wh || !hh.bh || !hh.Y0 || !hh.O || (hh.xa_hs & 3))) return HICGAT_EINVAL;
   // float4 rows: x, the weight rows and the LDS images need 16-B alignment
   if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3 | (uintptr_t)hh.Wh | (uintptr_t)hh.Y0 |
-       (uintptr_t)hh.O) & 15)
+       (uintptr_t)hh.O | (uintptr_t)pack) & 15)
     return HICGAT_EUNSUPPORTED;
-  // 16 rows per workgroup (66 KiB of dynamic LDS: two workgroups per CU).  A 32-row form (132 KiB,
-  // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
-  // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
-  // with one workgroup per CU every phase's latency is exposed.
-  constexpr int RB = 16, NW = kTailWaves;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               2 * RB * XS * (int)sizeof(float)) == hipSuccess;
-  if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, HEADS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
-                     (size_t)2 * RB * XS * sizeof(float), stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3,
-                     b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1, Y2,
-                     reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords, hh.xa_hs,
-                     hh.Wh, hh.bh, hh.Y0, hh.O);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  if (pack) {
+    const float *pk = static_cast<const float *>(pack);
+    return tail_fwd_go<HEADS, true>(x, ldx, M, pk + kPackF1, b1c, g1, be1, pk + kPackF2, b2c, g2, be2, W3, b3, g3,
+                                    be3, W4, b4, eps, Y1, st1, z1, Y2, st2, z2, y3, st3, z3, coords,
+                                    HEADS ? pk + kPackFH : nullptr, hh, stream);
+  }
+  return tail_fwd_go<HEADS, false>(x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
+                                   st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh.Wh, hh, stream);
 }
 }  // namespace
 
@@ -616,9 +727,9 @@ extern "C" int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const f
                                      const float *g2, const float *be2, const float *W3, const float *b3,
                                      const float *g3, const float *be3, const float *W4, const float *b4, float eps,
                                      float *Y1, float *st1, float *z1, float *Y2, float *st2, float *z2, float *y3,
-                                     float *st3, float *z3, float *coords, hicgat_stream_t stream) {
+                                     float *st3, float *z3, float *coords, const void *pack, hicgat_stream_t stream) {
   return tail_fwd_launch<false>(x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
-                                st1, z1, Y2, st2, z2, y3, st3, z3, coords, TailHeads{}, (hipStream_t)stream);
+                                st1, z1, Y2, st2, z2, y3, st3, z3, coords, TailHeads{}, pack, (hipStream_t)stream);
 }
 
 extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64_t xa_head_stride, const float *Wh,
@@ -628,7 +739,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
                                            const float *b3, const float *g3, const float *be3, const float *W4,
                                            const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2,
                                            float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
-                                           hicgat_stream_t stream) {
+                                           const void *pack, hicgat_stream_t stream) {
   if (kTailWaves < 8) return HICGAT_EUNSUPPORTED;
   TailHeads hh;
   hh.xa = xa;
@@ -638,7 +749,7 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
   hh.Y0 = Y0;
   hh.O = O;
   return tail_fwd_launch<true>(xa, ld_xa, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
-                               st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh, (hipStream_t)stream);
+                               st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh, pack, (hipStream_t)stream);
 }
 
 extern "C" int hicgat_tail_bwd_waves(void) { return kTailWaves; }
@@ -654,16 +765,36 @@ struct TailHeadsBwd {   // the HEADS operands of the backward (all null: the pla
   float *dout = nullptr, *row_stats = nullptr, *dxa = nullptr;
 };
 
+template <bool HEADS, bool PK>
+int tail_bwd_go(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
+                const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c, const float *W1c,
+                const float *g1, const float *be1, const float *g2, const float *be2, const float *g3,
+                const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1, void *ws2, void *ws3,
+                const float *Wh, const TailHeadsBwd &hh, hipStream_t stream) {
+  constexpr int RB = 16, NW = kTailWaves;
+  // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
+  constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS, PK>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kBwdLds) == hipSuccess;
+  if (!attr) return HICGAT_ELAUNCH;
+  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS, PK>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+                     (size_t)kBwdLds, stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
+                     Y2, reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c,
+                     W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1),
+                     static_cast<float *>(ws2), static_cast<float *>(ws3), hh.act, hh.Y0, Wh, hh.bh, hh.dout,
+                     hh.row_stats, hh.dxa);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
 template <bool HEADS>
 int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
                     const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c,
                     const float *W1c, const float *g1, const float *be1, const float *g2, const float *be2,
                     const float *g3, const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
                     size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
-                    const TailHeadsBwd &hh, hipStream_t stream) {
-  constexpr int RB = 16, NW = kTailWaves;
-  // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
-  constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
+                    const TailHeadsBwd &hh, const void *pack, hipStream_t stream) {
   if (M < 0) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
   const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
@@ -673,22 +804,19 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
   if (HEADS && (!hh.Y0 || !hh.Wh || !hh.bh || !hh.row_stats || !hh.dxa)) return HICGAT_EINVAL;
   if (HEADS && (((uintptr_t)hh.Y0 | (uintptr_t)hh.bh | (uintptr_t)hh.dout | (uintptr_t)hh.row_stats) & 15))
     return HICGAT_EUNSUPPORTED;
+  if ((uintptr_t)pack & 15) return HICGAT_EUNSUPPORTED;
   // every workgroup owns NW partial rows of each LN workspace (one per wave)
   if (ws1_bytes < hicgat_tail_bwd_workspace_bytes(M, 256) || ws2_bytes < hicgat_tail_bwd_workspace_bytes(M, 128) ||
       ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
     return HICGAT_EINVAL;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               kBwdLds) == hipSuccess;
-  if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
-                     (size_t)kBwdLds, stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
-                     Y2, reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c,
-                     W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1),
-                     static_cast<float *>(ws2), static_cast<float *>(ws3), hh.act, hh.Y0, hh.Wh, hh.bh, hh.dout,
-                     hh.row_stats, hh.dxa);
-  HICGAT_CHECK_LAUNCH();
-  return HICGAT_OK;
+  if (pack) {
+    const float *pk = static_cast<const float *>(pack);
+    return tail_bwd_go<HEADS, true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1, g1, be1,
+                                    g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1, ws2, ws3,
+                                    HEADS ? pk + kPackBH : nullptr, hh, stream);
+  }
+  return tail_bwd_go<HEADS, false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                                   dx, dY1, dY2, dy3, ws1, ws2, ws3, hh.Wh, hh, stream);
 }
 }  // namespace
 
@@ -698,9 +826,9 @@ extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y
                                      const float *be1, const float *g2, const float *be2, const float *g3,
                                      const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1,
                                      size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3, size_t ws3_bytes,
-                                     hicgat_stream_t stream) {
+                                     const void *pack, hicgat_stream_t stream) {
   return tail_bwd_launch<false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
-                                dx, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, TailHeadsBwd{},
+                                dx, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, TailHeadsBwd{}, pack,
                                 (hipStream_t)stream);
 }
 
@@ -712,7 +840,7 @@ extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const fl
                                            void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
                                            size_t ws3_bytes, int act, const float *Y0, const float *Wh,
                                            const float *bh, float *dout, float *row_stats, float *dxa,
-                                           hicgat_stream_t stream) {
+                                           const void *pack, hicgat_stream_t stream) {
   if (kTailWaves < 8) return HICGAT_EUNSUPPORTED;
   TailHeadsBwd hh;
   hh.act = act ? 1 : 0;
@@ -723,6 +851,6 @@ extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const fl
   hh.row_stats = row_stats;
   hh.dxa = dxa;
   return tail_bwd_launch<true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
-                               nullptr, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, hh,
+                               nullptr, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, hh, pack,
                                (hipStream_t)stream);
 }

@@ -125,14 +125,16 @@ SIGNATURES = {
                                        c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_ln_relu_res_workspace_bytes": (c_sz, [c_int]),
     "hicgat_ln_relu_res_bwd_params": (c_int, [c_int, c_p, c_p, c_int, c_p, c_sz, c_p]),
-    "hicgat_tail_fwd_fused": (c_int, [c_p, c_i64, c_int] + [c_p] * 14 + [c_f] + [c_p] * 10 + [c_p]),
+    "hicgat_tail_pack_bytes": (c_sz, []),
+    "hicgat_tail_pack": (c_int, [c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "hicgat_tail_fwd_fused": (c_int, [c_p, c_i64, c_int] + [c_p] * 14 + [c_f] + [c_p] * 10 + [c_p, c_p]),
     "hicgat_tail_bwd_waves": (c_int, []),
     "hicgat_tail_bwd_workspace_bytes": (c_sz, [c_int, c_int]),
-    "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p]),
+    "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p, c_p]),
     "hicgat_tail_fwd_fused_heads": (c_int, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_int] + [c_p] * 14 + [c_f]
-                                    + [c_p] * 10 + [c_p]),
+                                    + [c_p] * 10 + [c_p, c_p]),
     "hicgat_tail_bwd_fused_heads": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 3 + [c_p, c_sz] * 3
-                                    + [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                    + [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_weights": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_agg": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_int, c_int, c_p, c_i64,
                                 c_p]),

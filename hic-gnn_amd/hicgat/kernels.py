@@ -500,13 +500,27 @@ class HipKernels:
                                                    P(dgamma), P(dbeta), int(accumulate), P(ws), ws.numel(),
                                                    _lib.stream(dz.device)), "hicgat_ln_relu_res_bwd")
 
+    def tail_pack(self, W1c, W2c, Wh=None):
+        """The packed copies of W1c [512, 512], W2c [256, 256] and (head forms) Wh [512, 512] that the
+        tail kernels read instead of the row-major weights (hicgat_tail_pack): a new device buffer, so
+        a forward's copy stays valid for its own backward."""
+        for t in (W1c, W2c) + ((Wh,) if Wh is not None else ()):
+            assert t.is_contiguous() and t.dtype == torch.float32
+        assert W1c.shape == (512, 512) and W2c.shape == (256, 256) and (Wh is None or Wh.shape == (512, 512))
+        n = int(self.lib.hicgat_tail_pack_bytes())
+        pack = torch.empty(n // 4, dtype=torch.float32, device=W1c.device)
+        _lib.check(self.lib.hicgat_tail_pack(P(W1c), P(W2c), P(Wh), P(pack), n, _lib.stream(W1c.device)),
+                   "hicgat_tail_pack")
+        return pack
+
     def tail_fwd_fused(self, x, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, coords=None,
-                       heads=None):
+                       heads=None, pack=None):
         """The flagship's MLP tail forward in one launch (tail_fused.hip): returns (coords, saved)
         with saved = (Y1, st1, z1, Y2, st2, z2, y3, st3, z3); ``coords`` (contiguous [M, 3]): write
         the output there (e.g. the rank's rows of the sharded step's all-gather buffer).
         ``heads`` (``ops.TailHeads``): the head-fused form -- the input rows x (written) are
-        relu(xa^h W_h^T + b^h) of the xagg GATConv (hicgat_tail_fwd_fused_heads)."""
+        relu(xa^h W_h^T + b^h) of the xagg GATConv (hicgat_tail_fwd_fused_heads).  ``pack``: the
+        ``tail_pack`` copies of these W1c / W2c (/ the heads' W), or None (row-major reads)."""
         M = x.shape[0]
         dev = x.device
         f = dict(dtype=torch.float32, device=dev)
@@ -519,7 +533,8 @@ class HipKernels:
         assert coords.shape == (M, 3) and coords.is_contiguous()
         ws = [W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4]
         assert all(t.is_contiguous() for t in ws) and x.stride(1) == 1
-        tail = [float(eps), P(Y1), P(st1), P(z1), P(Y2), P(st2), P(z2), P(y3), P(st3), P(z3), P(coords), _lib.stream(dev)]
+        tail = [float(eps), P(Y1), P(st1), P(z1), P(Y2), P(st2), P(z2), P(y3), P(st3), P(z3), P(coords), P(pack),
+                _lib.stream(dev)]
         with _timed("tail_fwd_fused"):
             if heads is None:
                 _lib.check(self.lib.hicgat_tail_fwd_fused(P(x), x.stride(0), M, *[P(t) for t in ws], *tail),
@@ -533,7 +548,7 @@ class HipKernels:
                     *tail), "hicgat_tail_fwd_fused_heads")
         return coords, (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)
 
-    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=None):
+    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=None, pack=None):
         """The tail's input-gradient chain in one launch (tail_fused.hip): returns (dx, dY1, dY2, dy3,
         (ws1, ws2, ws3)) -- the LayerNorm dgamma/dbeta partials stay in the workspaces
         (``ln_relu_res_bwd_params``).  ``heads``: the head-fused form (dx None; the xagg GATConv's
@@ -551,7 +566,7 @@ class HipKernels:
             if heads is None:
                 _lib.check(self.lib.hicgat_tail_bwd_fused(
                     P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dx), P(dY1),
-                    P(dY2), P(dy3), *wsa, _lib.stream(dev)), "hicgat_tail_bwd_fused")
+                    P(dY2), P(dy3), *wsa, P(pack), _lib.stream(dev)), "hicgat_tail_bwd_fused")
             else:
                 h = heads
                 assert h.dout.shape == (M, 512) and h.dout.is_contiguous() and h.dxa.shape == (M, 1024)
@@ -559,7 +574,7 @@ class HipKernels:
                 dx = None
                 _lib.check(self.lib.hicgat_tail_bwd_fused_heads(
                     P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dY1), P(dY2),
-                    P(dy3), *wsa, int(h.act), P(h.Y0), P(h.W), P(h.bias), P(h.dout), P(h.rs), P(h.dxa),
+                    P(dy3), *wsa, int(h.act), P(h.Y0), P(h.W), P(h.bias), P(h.dout), P(h.rs), P(h.dxa), P(pack),
                     _lib.stream(dev)), "hicgat_tail_bwd_fused_heads")
         return dx, dY1, dY2, dy3, ws
 

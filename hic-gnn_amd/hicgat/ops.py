@@ -678,6 +678,9 @@ FUSED_TAIL_MAX_M = int(os.environ.get("HICGAT_FUSED_TAIL_MAX_M", "12288"))
 # functions' backward steps on the fused forward's tensors): P = 8 rank step 0.583 vs 0.622 ms, P = 4
 # 0.856 vs 0.889, synth-2000 0.628 vs 0.652 ms per step (profiles/r03t_ab_fused_tail_bwd.txt)
 FUSED_TAIL_BWD = os.environ.get("HICGAT_FUSED_TAIL_BWD", "1") != "0"
+# ... both reading W1c / W2c / the heads' W as packed copies (hicgat_tail_pack, one launch per
+# forward; 0: the row-major weights)
+TAIL_PACK = os.environ.get("HICGAT_TAIL_PACK", "1") != "0"
 
 
 class _FusedTailFn(torch.autograd.Function):
@@ -695,11 +698,14 @@ class _FusedTailFn(torch.autograd.Function):
         W1c, b1c = _joined(Wa, Wal).contiguous(), _joined(ba, bal).contiguous()
         W2c, b2c = _joined(W1, W1al).contiguous(), _joined(b1, b1al).contiguous()
         # heads: x's rows are formed (written) by the kernel from the xagg GATConv's aggregates
+        # the weights as packed copies for both kernels (made once per forward; the backward reuses them)
+        pack = K.tail_pack(W1c, W2c, heads.W if heads is not None else None) if TAIL_PACK else None
         coords, saved = K.tail_fwd_fused(x, W1c, b1c, ga.contiguous(), bea.contiguous(), W2c, b2c, g1.contiguous(),
                                          be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
                                          be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out,
-                                         heads=heads)
+                                         heads=heads, pack=pack)
         ctx.heads = heads
+        ctx.pack = pack
         if coords_out is not None:
             # the kernel wrote into the caller's buffer (e.g. the all-gather rows); the output is a
             # fresh tensor object over the same memory, so autograd sees a new output (no view or
@@ -724,7 +730,7 @@ class _FusedTailFn(torch.autograd.Function):
             dx, dY1, dY2, dy3, (ws1, ws2, ws3) = K.tail_bwd_fused(
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
-                g2.contiguous(), be2.contiguous(), heads=ctx.heads)
+                g2.contiguous(), be2.contiguous(), heads=ctx.heads, pack=ctx.pack)
             rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per workgroup
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)

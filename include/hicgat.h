@@ -472,7 +472,17 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
                           const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2,
                           const float *W3, const float *b3, const float *g3, const float *be3, const float *W4,
                           const float *b4, float eps, float *Y1, float *st1, float *z1, float *Y2, float *st2,
-                          float *z2, float *y3, float *st3, float *z3, float *coords, hicgat_stream_t stream);
+                          float *z2, float *y3, float *st3, float *z3, float *coords, const void *pack,
+                          hicgat_stream_t stream);
+/* pack: NULL, or the packed weight copies hicgat_tail_pack made from THESE W1c / W2c (and, for the head
+ * forms, Wh): the kernels then read W1c, W2c and Wh from it (1 KB contiguous per wave load instead of
+ * 16 rows x 64 B: the vector memory path serves the row-major rows at 16 B per clock per CU, a quarter
+ * of the contiguous rate, and that set the pace of the kernels' GEMM phases); results bitwise the
+ * row-major form.  W3 / W4 are always read row-major.  hicgat_tail_pack_bytes(): the buffer's size.
+ * Not a reference interface: the copies are a layout of the same parameters. */
+size_t hicgat_tail_pack_bytes(void);
+int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
+                     hicgat_stream_t stream);
 /* The same tail's backward input-gradient chain in one launch: from dcoords [M][3] and the forward's
  * Y1, st1, Y2, st2, y3, st3 (hicgat_tail_fwd_fused), with W4 = dense3.weight [3][64], W3 = dense2.weight
  * [64][128], W2c = [W_dense1; W_align_dense1] [256][256], W1c = [W_densea; W_align_densea] [512][512],
@@ -491,7 +501,7 @@ int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const fl
                           const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
                           const float *be2, const float *g3, const float *be3, float *dx, float *dY1, float *dY2,
                           float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
-                          size_t ws3_bytes, hicgat_stream_t stream);
+                          size_t ws3_bytes, const void *pack, hicgat_stream_t stream);
 /* The head-fused forms for the sharded aggregate-first GATConv (hicgat.dist "xagg"; the GATConv of
  * models.py:619 by linearity per head, then the tail): the forward forms the tail's input rows
  * itself, Y0[:, 256h:256h+256] = xa^h W_h^T + b^h (xa^h = xa + h * xa_head_stride, [M][ld_xa]; W_h =
@@ -508,14 +518,14 @@ int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64_t xa_head_
                                 const float *be2, const float *W3, const float *b3, const float *g3, const float *be3,
                                 const float *W4, const float *b4, float eps, float *Y1, float *st1, float *z1,
                                 float *Y2, float *st2, float *z2, float *y3, float *st3, float *z3, float *coords,
-                                hicgat_stream_t stream);
+                                const void *pack, hicgat_stream_t stream);
 int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
                                 const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
                                 const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
                                 const float *be2, const float *g3, const float *be3, float *dY1, float *dY2,
                                 float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
                                 size_t ws3_bytes, int act, const float *Y0, const float *Wh, const float *bh,
-                                float *dout, float *row_stats, float *dxa, hicgat_stream_t stream);
+                                float *dout, float *row_stats, float *dxa, const void *pack, hicgat_stream_t stream);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --

@@ -1451,6 +1451,78 @@ def test_gatconv_tiny_graphs_match_oracle(n):
         assert _rel(pm.grad.cpu(), pr.grad) < 1e-4 or pr.grad.abs().max() < 1e-30, name
 
 
+# ---------------------------------------------------------------- a6: the tail's packed weight copies
+def test_tail_pack_layout_and_bitwise_kernels():
+    """hicgat_tail_pack: the forward (mfma_rows) and backward (mfma_rows_t) layouts of W1c / W2c / Wh
+    against their index formulas, and the four one-kernel tail launches (plain and head-fused,
+    forward and backward) reading the packed copies bitwise equal to the same launches reading the
+    row-major weights (every lane holds the same values in the same registers).  M = 1030: a partial
+    last workgroup."""
+    from hicgat import kernels, ops
+    K = kernels.default()
+    torch.manual_seed(11)
+    W1c, W2c, Wh = (torch.randn(n, n, device=DEV) * 0.05 for n in (512, 256, 512))
+    pack = K.tail_pack(W1c, W2c, Wh).cpu()
+
+    def fwd_layout(W):
+        R, C = W.shape
+        G = C // 32
+        o = torch.arange(R * C // 4)
+        L, chunk = o % 64, o // 64
+        e, g, b = chunk % 2, (chunk // 2) % G, (chunk // 2) // G
+        rows = 16 * b + L % 16
+        cols = 32 * g + 8 * (L // 16) + 4 * e
+        return torch.stack([W[rows, cols + c] for c in range(4)], 1).reshape(-1)
+
+    def bwd_layout(W):
+        R, C = W.shape
+        o = torch.arange(R * C // 4)
+        L, blk = o % 64, o // 64
+        g, cb = blk // (C // 16), blk % (C // 16)
+        rows = 16 * g + 4 * (L // 16)
+        cols = 16 * cb + L % 16
+        return torch.stack([W[rows + c, cols] for c in range(4)], 1).reshape(-1)
+
+    Wc = [w.cpu() for w in (W1c, W2c, Wh)]
+    want = torch.cat([fwd_layout(Wc[0]), fwd_layout(Wc[1]), fwd_layout(Wc[2]),
+                      bwd_layout(Wc[0]), bwd_layout(Wc[1]), bwd_layout(Wc[2])])
+    assert pack.shape == want.shape and torch.equal(pack, want)
+
+    M = 1030
+    f = dict(device=DEV)
+    x = torch.relu(torch.randn(M, 512, **f))
+    small = [torch.randn(n, **f) * 0.1 for n in (512, 256, 256, 256, 128, 128, 64, 64, 64)]
+    b1c, g1, be1, b2c, g2, be2, b3, g3, be3 = small
+    g1, g2, g3 = 1 + g1, 1 + g2, 1 + g3
+    W3, W4, b4 = torch.randn(64, 128, **f) * 0.1, torch.randn(3, 64, **f) * 0.1, torch.randn(3, **f) * 0.1
+    dc = torch.randn(M, 3, **f)
+    X4 = torch.randn(2, 2, M, 512, **f)
+    bias = torch.randn(512, **f) * 0.1
+    rs_init = torch.randn(M, 8, **f)
+    for heads in (False, True):
+        outs = []
+        for pk in (None, K.tail_pack(W1c, W2c, Wh if heads else None)):
+            h = None
+            xin = x.clone()
+            if heads:
+                h = ops.TailHeads(X4, Wh, bias, torch.empty(M, 512, **f), torch.empty(M, 512, **f),
+                                  rs_init.clone(), torch.empty(M, 1024, **f), act=1)
+            coords, saved = K.tail_fwd_fused(xin, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, 1e-5,
+                                             heads=h, pack=pk)
+            rs0 = h.rs.clone() if heads else None
+            dx, dY1, dY2, dy3, ws = K.tail_bwd_fused(dc, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=h,
+                                                     pack=pk)
+            torch.cuda.synchronize()
+            o = [coords, *saved, dY1, dY2, dy3, *ws]
+            if heads:
+                o += [xin, h.Y0, h.dout, h.dxa, h.rs, rs0]
+            else:
+                o += [dx]
+            outs.append([t.detach().cpu().clone() for t in o])
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (heads, a.shape)
+
+
 # ---------------------------------------------------------------- a6: the fused MLP-tail forward
 @pytest.mark.parametrize("m,sinks,bwd", [(2701, False, True), (2701, True, True), (2701, True, False),
                                          (16000, True, True), (1030, False, True)])
