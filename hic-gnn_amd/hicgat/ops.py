@@ -665,15 +665,14 @@ def dual_ln_relu_res(x, lin1, lin2, norm):
 # (HICGAT_FUSED_TAIL=0: off).  Measured (profiles/r03r_ab_fused_tail.txt, 4-deep weight prefetch):
 # a rank's shard at P = 8 (2 700 rows) 0.613 vs 0.650 ms per rank step, P = 4 (5 000) 0.877 vs
 # 0.896, synth-2000 0.641 vs 0.664 ms per step; with the fused backward too (r03za) the P = 2 shard
-# (10 000 rows) 1.302 / 1.307 vs 1.313 / 1.315 ms; slower on the whole graph: the single-GPU
-# N = 20000 step 1.977 vs 1.913 ms with the fused forward -- 16-row workgroups stream the 1.3 MB of
-# tail weights from L2 once per 16 rows (1.6 GB at N = 20000) where the tiled GEMMs reuse each weight
-# tile over 160 rows, and a 32-row form (one workgroup per CU) exposed every phase's latency -- and
-# the fused backward's LN partials are one row per wave (workspaces sized by M).
+# (10 000 rows) 1.302 / 1.307 vs 1.313 / 1.315 ms.  On the whole 20000-row graph it was slower
+# (1.936 vs 1.913 ms per step) while its 16-row workgroups read the weights row-major -- a quarter
+# of the load rate -- and is faster since they read packed copies (TAIL_PACK): 1.815 / 1.819 vs
+# 1.871 / 1.876 ms per step (profiles/r05aa_fused_tail_20000_ab.txt), so MAX_M now covers it.
 # Graphs below MIN_M (chr19: 58 / 114 loci) keep the per-layer kernels.
 FUSED_TAIL = os.environ.get("HICGAT_FUSED_TAIL", "1") != "0"
 FUSED_TAIL_MIN_M = int(os.environ.get("HICGAT_FUSED_TAIL_MIN_M", "1024"))
-FUSED_TAIL_MAX_M = int(os.environ.get("HICGAT_FUSED_TAIL_MAX_M", "12288"))
+FUSED_TAIL_MAX_M = int(os.environ.get("HICGAT_FUSED_TAIL_MAX_M", "32768"))
 # ... and its backward input-gradient chain in one launch too (tail_fused.hip; 0: the per-layer
 # functions' backward steps on the fused forward's tensors): P = 8 rank step 0.583 vs 0.622 ms, P = 4
 # 0.856 vs 0.889, synth-2000 0.628 vs 0.652 ms per step (profiles/r03t_ab_fused_tail_bwd.txt)
