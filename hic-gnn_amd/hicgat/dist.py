@@ -9,7 +9,7 @@ rowptr is the prefix sum), every rank keeping at least one row; the upper-triang
 contiguous ranges; the loss's support rows (the contact set of cont2dist's target) in P blocks
 balanced by support nnz.
 
-Three step forms (``mode``; "auto" picks slab at P = 2 and xagg from P = 4, ``resolve_mode``):
+Three step forms (``mode``; "auto" picks xagg from P = 2, ``resolve_mode``):
 
 ``"slab"`` (default) -- no per-step collective larger than the 2.4 MB gradient buffer.  The 512-d
   node embeddings x are constant, so they are all-gathered ONCE (every rank holds all of x, 41 MB)
@@ -57,10 +57,12 @@ from .optim import FlatAdam
 TILE = 128
 MODES = ("slab", "xagg", "allgather")
 # "auto" (bench.py's default): the form measured faster per world size on the N = 20000 graph
-# (bench.py --simulate-world, profiles/r03*_simrank_*): at P = 2 the slab form (1.37 vs 1.48 ms
-# modeled: 10000-row shards keep its replicated lin_l GEMMs cheap next to the xagg edge pass), from
-# P = 4 on the aggregate-first form (P = 8: 0.71 vs 0.84 ms: no replicated O(N d^2) work at all)
-AUTO_XAGG_MIN_P = int(os.environ.get("HICGAT_AUTO_XAGG_MIN_P", "4"))
+# (bench.py --simulate-world).  Round 3 (profiles/r03*_simrank_*): slab at P = 2 (1.37 vs 1.48 ms
+# modeled: 10000-row shards kept its replicated lin_l GEMMs cheap next to the xagg edge pass), xagg
+# from P = 4 (P = 8: 0.71 vs 0.84 ms).  Round 5, with the packed one-kernel tail and the emulated
+# collectives: xagg at P = 2 too (1.234 vs 1.279 ms, profiles/r05af_simrank_xagg_P2.json,
+# r05y_simrank_auto_P2.json)
+AUTO_XAGG_MIN_P = int(os.environ.get("HICGAT_AUTO_XAGG_MIN_P", "2"))
 
 
 def resolve_mode(mode, P):

@@ -34,7 +34,9 @@ def test_bench_gpus2_self_launches_two_ranks():
     col = res["collectives"]
     assert col["world_size"] == 2 and col["process_group_size"] == 2 and col["ranks_counted_by_all_reduce"] == 2
     assert col["backend"] == "gloo"
-    names = {"coords_all_gather", "loss_all_reduce", "grad_all_reduce_gat_bucket", "grad_all_reduce_tail_bucket"}
+    # the "auto" form at 2 ranks is xagg: the flat gradient beside the edge pass, then g (slab form:
+    # the gradient in two buckets)
+    names = {"coords_all_gather", "loss_all_reduce", "grad_all_reduce", "g_all_reduce"}
     assert names <= set(col["measured_us"]), col["measured_us"].keys()
     for k, v in col["measured_us"].items():
         assert v["calls"] == 2 and v["avg_us"] > 0 and v["min_us"] <= v["avg_us"], (k, v)

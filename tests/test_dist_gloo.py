@@ -149,11 +149,12 @@ def test_three_uneven_ranks_equal_single_rank(tmp_path, mode):
 
 @pytest.mark.parametrize("world", [4, 8])
 def test_auto_form_at_four_and_eight_ranks_equals_single_rank(tmp_path, world):
-    """bench.py's default form at the driver's larger world sizes ("auto" = xagg from 4 ranks,
+    """bench.py's default form at the driver's larger world sizes ("auto" = xagg from 2 ranks,
     hicgat.dist.resolve_mode): 4 and 8 gloo ranks on a 301-node graph equal world 1 of the same
     form, and the shards still partition the rows, edges, tiles and support rows."""
     from hicgat import dist as hdist
-    assert hdist.resolve_mode("auto", world) == "xagg" and hdist.resolve_mode("auto", 2) == "slab"
+    assert hdist.resolve_mode("auto", world) == "xagg" and hdist.resolve_mode("auto", 2) == "xagg"
+    assert hdist.resolve_mode("auto", 1) == "slab"
     one = _run(1, 301, "combined", tmp_path, mode="xagg")
     many = _run(world, 301, "combined", tmp_path, mode="auto")
     _close(one, many)

@@ -236,17 +236,17 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode, n, big):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world,mode", [(2, "auto"), (8, "auto")])
+@pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "auto"), (8, "auto")])
 def test_configs3_synth20000_sharded_matches_single_gpu(tmp_path, world, mode):
     """BASELINE configs[3]: the synth-20000 graph (bench.py's workload, N = 20000, 4.02 M edges)
-    destination-row sharded over ``world`` ranks in the form bench.py --gpus runs ("auto": slab at
-    P = 2 -- 10 000-row shards, the one-kernel tail; xagg at P = 8 -- 2 500-row shards, K-split row
-    GEMMs, the xagg edge / slab passes), gloo ranks sharing the one GPU, two training steps against
+    destination-row sharded over ``world`` ranks in the form bench.py --gpus runs ("auto": xagg --
+    10 000-row shards at P = 2, 2 500-row shards at P = 8, the head-fused one-kernel tail, the edge
+    pass) and the slab form at P = 2, gloo ranks sharing the one GPU, two training steps against
     the single-GPU step from the same seed (HiC-GNN_main.py:123-132): loss 1e-5 relative at both
     steps, every step-1 gradient to 1e-4 of its max with the kink-decided entries masked, the
     step-1 Adam update."""
     res = _run(world, "gloo", 20000, tmp_path, mode)
-    assert res["mode"] == ("slab" if world == 2 else "xagg") and len(res["rows"]) == world
+    assert res["mode"] == ("slab" if mode == "slab" else "xagg") and len(res["rows"]) == world
     ref = _single_gpu_steps(20000)
     _assert_step_matches(ref, res, label=f"P={world} {res['mode']} rows {res['rows']}")
 
