@@ -601,28 +601,52 @@ struct PackJobs {
   PackJob j[6];
   int n;
 };
-// one thread per float4 of the packed copy (coalesced writes; the reads gather 4 floats)
+// One wave per unit: the forward layout's unit is a 16-row x 32-column block of W (the two 1 KB
+// chunks e = 0, 1 of super-group g), the backward layout's a 16 x 16 block (one 1 KB chunk).  The
+// wave reads the block as whole 128-B / 64-B row pieces (contiguous quads of lanes), turns it
+// through LDS and writes its chunks as 1 KB contiguous -- a lane-per-row read or write runs the
+// vector memory path at a quarter of the rate (tools/ld_pattern_bench.hip).
+// the wave's LDS writes visible to its other lanes' reads
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __global__ __launch_bounds__(256) void tail_pack_kernel(const PackJobs jobs) {
+  __shared__ float tile[4][16][36];
   int q = 0;
 #pragma unroll
   for (int k = 1; k < 6; ++k) q += (k < jobs.n && (int)blockIdx.x >= jobs.j[k].blk0) ? 1 : 0;
   const PackJob &J = jobs.j[q];
-  const int64_t o4 = (int64_t)(blockIdx.x - J.blk0) * 256 + threadIdx.x;
-  if (o4 >= (int64_t)J.R * J.C / 4) return;
-  const int L = (int)(o4 & 63);
-  float4 v;
-  if (!J.bwd) {   // mfma_rows: ((b * G + g) * 2 + e) * 256 + 4L  <-  row 16b + (L & 15), cols 32g + 8(L >> 4) + 4e ..
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int u = (blockIdx.x - J.blk0) * 4 + wv;                       // this wave's unit
+  float (*T)[36] = tile[wv];
+  float4 *out = reinterpret_cast<float4 *>(J.dst);
+  if (!J.bwd) {   // P[((b * G + g) * 2 + e) * 256 + 4L + c] = W[16b + (L & 15)][32g + 8(L >> 4) + 4e + c]
     const int G = J.C / 32;
-    const int64_t chunk = o4 >> 6;
-    const int e = (int)(chunk & 1), g = (int)((chunk >> 1) % G), b = (int)((chunk >> 1) / G);
-    v = *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * b + (L & 15)) * J.C + 32 * g + 8 * (L >> 4) + 4 * e);
-  } else {        // mfma_rows_t: ((g * (C / 16) + c) * 64 + L) * 4 + s  <-  row 16g + 4(L >> 4) + s, col 16c + (L & 15)
-    const int64_t blk = o4 >> 6;
-    const int g = (int)(blk / (J.C / 16)), c = (int)(blk % (J.C / 16));
-    const float *p = J.src + (size_t)(16 * g + 4 * (L >> 4)) * J.C + 16 * c + (L & 15);
-    v = make_float4(p[0], p[J.C], p[2 * (size_t)J.C], p[3 * (size_t)J.C]);
+    if (u >= (J.R / 16) * G) return;                                   // wave-uniform
+    const int b = u / G, g = u % G;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = lane + 64 * h, r = t >> 3, c4 = t & 7;
+      *reinterpret_cast<float4 *>(&T[r][4 * c4]) =
+          *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * b + r) * J.C + 32 * g + 4 * c4);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      out[((size_t)u * 2 + e) * 64 + lane] = *reinterpret_cast<const float4 *>(&T[lane & 15][8 * (lane >> 4) + 4 * e]);
+  } else {        // P[((g * (C / 16) + c) * 64 + L) * 4 + s] = W[16g + 4(L >> 4) + s][16c + (L & 15)]
+    const int CB = J.C / 16;
+    if (u >= (J.R / 16) * CB) return;
+    const int g = u / CB, cb = u % CB;
+    const int r = lane >> 2, c4 = lane & 3;
+    *reinterpret_cast<float4 *>(&T[r][4 * c4]) =
+        *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * g + r) * J.C + 16 * cb + 4 * c4);
+    wave_lds_sync();
+    const int r0 = 4 * (lane >> 4), cc = lane & 15;
+    out[(size_t)u * 64 + lane] = make_float4(T[r0][cc], T[r0 + 1][cc], T[r0 + 2][cc], T[r0 + 3][cc]);
   }
-  reinterpret_cast<float4 *>(J.dst)[o4] = v;
 }
 
 }  // namespace hicgat
@@ -648,7 +672,8 @@ extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float 
     J.C = C;
     J.bwd = bwd;
     J.blk0 = blk;
-    blk += (R * C / 4 + 255) / 256;
+    const int units = bwd ? (R / 16) * (C / 16) : (R / 16) * (C / 32);   // one wave each, 4 per block
+    blk += (units + 3) / 4;
   };
   add(W1c, kPackF1, 512, 512, 0);
   add(W2c, kPackF2, 256, 256, 0);

@@ -12,9 +12,13 @@ import torch  # noqa: E402
 
 
 def timeit(fn, reps=20):
+    """Device time per call: a 3 ms emulated-collective kernel first keeps the GPU busy while the host
+    enqueues the calls, so host launch overhead (ctypes job tables) stays out of the events."""
+    from hicgat import _lib
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _lib.check(_lib.lib().hicgat_sim_collective(3000.0, 16, 256, _lib.stream(torch.device("cuda", 0))), "busy")
     e0.record()
     for _ in range(reps):
         fn()
@@ -78,22 +82,24 @@ def main():
                                                                    tr.rs, dz, tr.ns, tr.gpart))
     res["dxa grouped GEMM"] = timeit(lambda: K.gemm_rows_grouped(
         [(tr.dout_l[:, hc[hd]], W[hc[hd]], tr.dxa[:, hd * F:(hd + 1) * F], None, None) for hd in (0, 1)], b_kmajor=1))
-    if rec:
-        w, c, tg = rec[-1]
-        Kp = tr.K
-        res["grads: both launches"] = timeit(lambda: Kp.param_grads_grouped(w, c, tg))
-        res["grads: weight-gradient jobs only (+ their slab sums)"] = timeit(lambda: Kp.param_grads_grouped(w, [], tg))
+    Kp = tr.K
+    for li, (w, c, tg) in enumerate(rec):   # every grouped launch pair of the step (side, then g's)
+        pre = f"grads[{li}] target {tg}:"
+        res[f"{pre} both launches"] = timeit(lambda: Kp.param_grads_grouped(w, c, tg))
+        res[f"{pre} weight-gradient jobs only (+ their slab sums)"] = timeit(lambda: Kp.param_grads_grouped(w, [], tg))
+        if c:
+            res[f"{pre} column-sum jobs only"] = timeit(lambda: Kp.param_grads_grouped([], c, tg))
         for k, job in enumerate(c):
-            res[f"grads: colsum job {k} {tuple(job[0].shape)}{' weighted' if len(job) > 3 else ''}"] = \
+            res[f"{pre} colsum job {k} {tuple(job[0].shape)}{' weighted' if len(job) > 3 else ''}"] = \
                 timeit(lambda job=job: Kp.param_grads_grouped([], [job], tg))
         for k, job in enumerate(w):
-            res[f"grads: wgrad job {k} dy {tuple(job[0].shape)} x {tuple(job[1].shape)}"] = \
+            res[f"{pre} wgrad job {k} dy {tuple(job[0].shape)} x {tuple(job[1].shape)}"] = \
                 timeit(lambda job=job: Kp.param_grads_grouped([job], [], tg))
     print(f"rank {a.rank} of {a.world}: rows {tr.local_rows}, nnz {tr.local_nnz}, dxa finite "
           f"{bool(torch.isfinite(tr.dxa).all())}, |dxa| max {float(tr.dxa.abs().max()):.3e}, "
           f"denormal frac {float(((tr.dxa.abs() < 1.2e-38) & (tr.dxa != 0)).float().mean()):.3e}")
     for k, v in res.items():
-        print(f"{k:48s} {v:9.1f} us")
+        print(f"{k:72s} {v:9.1f} us")
 
 
 if __name__ == "__main__":
