@@ -4,7 +4,10 @@
 //   rows : lane (li = lane & 15, j = lane >> 4) loads row n0 + li, k 8j + 4e .. +3  (the tail's map:
 //          16 rows per instruction, 64 B of each)
 //   flat : lane loads the 16 B at 16 * lane of a contiguous 1 KB block (a pre-permuted copy)
-// Build: hipcc -O3 --offload-arch=gfx950 tools/ld_pattern_bench.hip -o /tmp/ldb
+// Also the store side (st_kernel): a wave writing 1 KB per instruction as dwordx4 (contiguous), as
+// dwords of 16 consecutive columns in 4 rows (the tail's MFMA C-tile stores: lane & 15 = column,
+// 4 (lane >> 4) + r = row), and as dwords of 64 consecutive floats (a LayerNorm row).
+// Build: hipcc -O3 --offload-arch=gfx950 tools/ld_pattern_bench.hip -o tools/ld_pattern_bench
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -45,6 +48,36 @@ __global__ __launch_bounds__(1024) void ld_kernel(const float *__restrict__ W, f
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+template <int MODE>
+__global__ __launch_bounds__(1024) void st_kernel(float *__restrict__ O, long long *cyc) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // each wave writes 64 KB per pass into its own region: 16 rows x 1024 floats (row stride 1024)
+  float *base = O + ((size_t)blockIdx.x * 16 + wv) * 16 * 1024;
+  float4 *b4 = reinterpret_cast<float4 *>(O) + ((size_t)blockIdx.x * 16 + wv) * 4096;
+  __syncthreads();
+  const long long t0 = clock64();
+  for (int pass = 0; pass < 4; ++pass) {
+    const float v = (float)(pass + lane);
+    if (MODE == 0) {          // dwordx4, 1 KB contiguous per instruction
+#pragma unroll 4
+      for (int i = 0; i < 64; ++i)
+        b4[(size_t)i * 64 + lane] = make_float4(v, v + 1.f, v + 2.f, v + 3.f);
+    } else if (MODE == 1) {   // dword, C-tile map: row 4 (lane >> 4) + r, 16 columns per row
+#pragma unroll 4
+      for (int i = 0; i < 256; ++i) {
+        const int t = i & 63, r = i >> 6;   // 64 column tiles x 4 rows
+        base[(size_t)(4 * (lane >> 4) + r) * 1024 + 16 * t + (lane & 15)] = v;
+      }
+    } else {                  // dword, 64 consecutive floats per instruction
+#pragma unroll 4
+      for (int i = 0; i < 256; ++i) base[(size_t)i * 64 + lane] = v;
+    }
+  }
+  __syncthreads();
+  const long long t1 = clock64();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 int main() {
   const int K = 512, N = 512;
   float *W, *sink;
@@ -68,6 +101,26 @@ int main() {
       const double bytes = 4.0 * N * K * 4;   // 4 passes of the matrix per workgroup
       printf("blocks %3d  %-4s  %9.0f cycles per workgroup  %6.1f B/clk per CU\n", blocks, mode ? "flat" : "rows", s,
              bytes / s);
+    }
+  }
+  float *O;
+  hipMalloc(&O, (size_t)256 * 16 * 16 * 1024 * 4);
+  const char *names[3] = {"st-x4", "st-tile", "st-row"};
+  for (int blocks : {1, 169}) {
+    for (int mode = 0; mode < 3; ++mode) {
+      for (int rep = 0; rep < 3; ++rep) {
+        if (mode == 0) hipLaunchKernelGGL(st_kernel<0>, dim3(blocks), dim3(1024), 0, 0, O, cyc);
+        else if (mode == 1) hipLaunchKernelGGL(st_kernel<1>, dim3(blocks), dim3(1024), 0, 0, O, cyc);
+        else hipLaunchKernelGGL(st_kernel<2>, dim3(blocks), dim3(1024), 0, 0, O, cyc);
+      }
+      hipDeviceSynchronize();
+      std::vector<long long> c(blocks);
+      hipMemcpy(c.data(), cyc, blocks * 8, hipMemcpyDeviceToHost);
+      double sum = 0;
+      for (auto x : c) sum += (double)x;
+      sum /= blocks;
+      const double bytes = 4.0 * 16 * 64 * 1024;   // 4 passes x 16 waves x 64 KB
+      printf("blocks %3d  %-7s %9.0f cycles per workgroup  %6.1f B/clk per CU\n", blocks, names[mode], sum, bytes / sum);
     }
   }
   return 0;
