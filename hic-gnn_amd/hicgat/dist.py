@@ -11,7 +11,7 @@ balanced by support nnz.
 
 Three step forms (``mode``; "auto" picks xagg from P = 2, ``resolve_mode``):
 
-``"slab"`` (default) -- no per-step collective larger than the 2.4 MB gradient buffer.  The 512-d
+``"slab"`` -- no per-step collective larger than the 2.4 MB gradient buffer.  The 512-d
   node embeddings x are constant, so they are all-gathered ONCE (every rank holds all of x, 41 MB)
   and each rank recomputes h = x W^T for every row (10.5 GFLOP, ~0.1 ms) instead of all-gathering
   h every step.  The backward's source side is split by DESTINATION owner instead of by source
@@ -24,6 +24,13 @@ Three step forms (``mode``; "auto" picks xagg from P = 2, ``resolve_mode``):
   [loss moments | dcoords], the gradient all-reduce in two buckets -- the MLP tail's (ready when
   the side stream's dW GEMMs finish, reduced on a comm stream beside lin_l's dW GEMM) and the
   GATConv's -- and identical Adam on every rank.
+``"xagg"`` (what "auto" runs) -- the aggregate-first GATConv (gat_xagg.hip): by linearity per head,
+  out_i^h = W_h (sum_j alpha_ij x_j) + b^h, with a_src = x (W_h^T att^h); x is replicated (gathered
+  once), every GEMM runs on the rank's own rows, the backward's edge pass folds the source side in
+  (g = sum ds x, reduced as an 8 KB all-reduce; W's att (x) g term and datt applied to the summed g
+  on every rank).  The tail's and the heads' dW and the flat-gradient all-reduce run on a side stream
+  beside the edge pass.  Per step: coords all-gather, the fp64 [moments | dcoords] all-reduce, the
+  flat-gradient all-reduce, g's all-reduce.
 ``"allgather"`` -- the north star's literal form: each rank computes h for its rows, RCCL
   all-gather of h [N, 512] before the layer; after the backward's row pass one all-gather of packed
   rows [dout | row stats] so each rank's source pass covers its own rows r completely (its dW is
@@ -355,7 +362,7 @@ class SimComm:
 
 
 class ShardedTrainer:
-    def __init__(self, model, x, adj, truth, lr=1e-3, kind="mse", group=None, kern=None, mode="slab", comm=None):
+    def __init__(self, model, x, adj, truth, lr=1e-3, kind="mse", group=None, kern=None, mode="auto", comm=None):
         if kern is None:
             from .kernels import default
             kern = default()
