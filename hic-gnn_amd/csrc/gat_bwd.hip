@@ -354,6 +354,13 @@ __global__ __launch_bounds__(256) void param_grad_stage2(const float *__restrict
   }
 }
 
+// Unused dynamic LDS per workgroup of the whole-graph source pass (hicgat_gat_agg_bwd_src): 5
+// workgroups per CU (the 160 KiB / 32 KiB) instead of the 7 its 68 VGPRs allow -- fewer rows in
+// flight per CU (L2 misses), and the side stream's dW kernels wait for the pass instead of sharing
+// its CUs: single-GPU step -8 us alone, -20 us with the forward gather's cap (gat_fwd.hip; 3 per CU:
+// even, 6 per CU: even), profiles/r05at_gather_occupancy_ab.txt
+constexpr size_t kSrcOccLds = 32768;
+
 // Grid of the source pass: one workgroup per 4 rows.  (A persistent grid of 2-3 workgroups per CU,
 // leaving slots to the side stream's GEMMs, measured the same step or slower)
 #define HICGAT_SRC_LAUNCH(SPLIT_, rows_, ...)                                                              \
@@ -406,7 +413,7 @@ extern "C" int hicgat_gat_agg_bwd_src_ld(const int32_t *rowptr, const int32_t *c
       !dh || !da_src)
     return HICGAT_EINVAL;
   const int rows = row_end - row_begin;
-  HICGAT_SRC_LAUNCH(false, rows,
+  hipLaunchKernelGGL((agg_bwd_src_h2c256_kernel<false>), dim3((rows + 3) / 4), dim3(256), kSrcOccLds,
                      (hipStream_t)stream, rowptr, col, row_begin, row_end, h, a_src, a_dst,
                      row_stats, ld_stats, dout, ld_dout / 4, att_src, att_dst, neg_slope, dh, da_src);
   HICGAT_CHECK_LAUNCH();

@@ -194,6 +194,12 @@ extern "C" int hicgat_gat_att_logits(const float *h, const float *att_src, const
   return HICGAT_OK;
 }
 
+// Unused dynamic LDS per workgroup of the gather launch below: 3 workgroups per CU (160 KiB / 52 KiB)
+// instead of the 4 its 98 VGPRs allow -- fewer rows in flight per CU, fewer L2 misses: the
+// single-GPU step 1.798-1.803 vs 1.820-1.821 ms together with the source pass's cap (gat_bwd.hip;
+// 2 per CU: +30 us), profiles/r05at_gather_occupancy_ab.txt
+constexpr size_t kAggFwdOccLds = 53248;
+
 extern "C" int hicgat_gat_agg_fwd_act(const int32_t *rowptr, const int32_t *col, int N, int nnz,
                                       int H, int C, int row_begin, int row_end, const float *h,
                                       const float *a_src, const float *a_dst, const float *bias,
@@ -208,7 +214,7 @@ extern "C" int hicgat_gat_agg_fwd_act(const int32_t *rowptr, const int32_t *col,
   const dim3 grid((rows + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define HICGAT_FWD_LAUNCH(TR, AC)                                                                  \
-  hipLaunchKernelGGL((agg_fwd_h2c256_kernel<TR, AC>), grid, block, 0, s, rowptr, col, row_begin,   \
+  hipLaunchKernelGGL((agg_fwd_h2c256_kernel<TR, AC>), grid, block, kAggFwdOccLds, s, rowptr, col, row_begin, \
                      row_end, h, a_src, a_dst, bias, neg_slope, out, out2, row_stats)
   if (out2) {
     if (act) HICGAT_FWD_LAUNCH(true, 1);
