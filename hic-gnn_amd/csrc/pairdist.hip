@@ -236,10 +236,12 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       else L2 = __builtin_elementwise_fma(r, r, L2);
       if (PEARSON) {
         sd2 += d;
-        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
-        sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
-        st2 += tv[h];
-        stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
+        if constexpr (!BG) {   // background form: t = bg at every pair, these four follow below
+          sdd2 = __builtin_elementwise_fma(d, d, sdd2);
+          sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
+          st2 += tv[h];
+          stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
+        }
       }
       const f2 w = ABSL ? f2{sgn_inv(r.x, inv.x), sgn_inv(r.y, inv.y)} : r * inv;
       px = __builtin_elementwise_fma(w, dx, px);
@@ -265,13 +267,25 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
     A.az[2 * h] = az2[h].x;
     A.az[2 * h + 1] = az2[h].y;
   }
-  A.L += L2.x + L2.y;
+  const float L = L2.x + L2.y;
+  A.L += L;
   if (PEARSON) {
-    A.sd += sd2.x + sd2.y;
-    A.sdd += sdd2.x + sdd2.y;
-    A.sdt += sdt2.x + sdt2.y;
-    A.st += st2.x + st2.y;
-    A.stt += stt2.x + stt2.y;
+    const float sd = sd2.x + sd2.y;
+    A.sd += sd;
+    if constexpr (BG) {
+      // t = bg at all 8 (K1 - K0) pairs: sum d^2 = sum (d - bg)^2 + bg (2 sum d - n bg), sum d t =
+      // bg sum d, sum t and sum t^2 by count (four packed ops per two pairs out of the loop)
+      constexpr float npair = 8.f * (K1 - K0);
+      A.sdd += L + bg * fmaf(-npair, bg, 2.f * sd);
+      A.sdt = fmaf(bg, sd, A.sdt);
+      A.st = fmaf(npair, bg, A.st);
+      A.stt = fmaf(npair * bg, bg, A.stt);
+    } else {
+      A.sdd += sdd2.x + sdd2.y;
+      A.sdt += sdt2.x + sdt2.y;
+      A.st += st2.x + st2.y;
+      A.stt += stt2.x + stt2.y;
+    }
   }
 }
 

@@ -90,6 +90,7 @@ def main():
         "pairdist_mse_fused": lambda K: K.fused_loss(coords, truth.buf, n, 0, 0, -1, stats, loss, dc),
         "pairdist_combined": lambda K: K.fused_loss(coords, truth.buf, n, 1, 0, -1, stats, loss, dc),
         "pairdist_support": lambda K: K.fused_loss_support(coords, truth.support, n, 0, stats, loss, dc),
+        "pairdist_support_combined": lambda K: K.fused_loss_support(coords, truth.support, n, 1, stats, loss, dc),
         "gat_agg_fwd_tiled": lambda K: K.agg_fwd_tiled(adj.rowptr32, adj.col32, tiles(), h, a_s, a_d, b, 0.2, 1, out,
                                                        out2, rs),
         "gat_agg_bwd_src_tiled": lambda K: K.agg_bwd_src_tiled(tiles(), h, a_s, a_d, rs, dout, al, ar, 0.2, dh, da),
