@@ -246,22 +246,59 @@ def cpu_baseline(wl, seed, steps=5, warmup=2):
     x = torch.tensor(synth.features(n, seed=seed))
     torch.manual_seed(0)
     model = og.GATNetSelectiveResidualsUpdated()
+    # parity (outside the timed CPU steps): the step-1 forward of the same seed-0 weights -- the
+    # coordinates (get_model; the flagship has no dropout, so the training forward's are the same)
+    # and the MSE with exact-formula distances, as the device computes them
+    t_par = time.perf_counter()
+    with torch.no_grad():
+        c1 = model.get_model(x, adj)
+        mode, og.CDIST_MODE = og.CDIST_MODE, "donot_use_mm_for_euclid_dist"
+        try:
+            l1_exact = float(torch.nn.functional.mse_loss(
+                torch.cdist(c1, c1, p=2, compute_mode=og.CDIST_MODE).float(), truth.float()))
+        finally:
+            og.CDIST_MODE = mode
+    log(f"[cpu] step-1 forward for parity: loss (exact cdist) {l1_exact:.9g} ({time.perf_counter() - t_par:.1f} s)")
     marks = [time.perf_counter()]
 
     def on_step(k, lv):
         marks.append(time.perf_counter())
         log(f"[cpu] step {k} loss {lv:.6g} ({marks[-1] - marks[-2]:.2f} s)")
 
-    ol.train(model, x, adj, truth, steps=warmup + steps, on_step=on_step)
+    hist = ol.train(model, x, adj, truth, steps=warmup + steps, on_step=on_step)
     per = np.diff(marks)[warmup:]
     med = float(np.median(per))
     return dict(value=1.0 / med, unit="steps/s", cores=threads, kind="port",
+                step1={"coords": c1.detach(), "loss_exact_cdist": l1_exact, "loss_reference_cdist": hist[0]},
                 median_s_per_step=med, step_s=[float(v) for v in per], cpu_model=_cpu_model(),
                 host_cpus_visible=os.cpu_count(),
                 sample=f"median of {steps} timed steps (after {warmup} warm-up) of the full {n}-node step "
                        f"(oracle GATNetSelectiveResidualsUpdated, fwd+MSE+bwd+Adam, torch CPU, "
                        f"{threads} threads = the box's CPU share (OMP_NUM_THREADS), {os.cpu_count()} host CPUs "
                        f"visible, {_cpu_model()})")
+
+
+PARITY_TOL = 1e-5   # BASELINE.json north star: "predicted coordinates and loss within 1e-5 relative fp32"
+
+
+def parity_block(dev, cpu):
+    """The device's training step 1 against the CPU oracle's step 1 on the same workload and seed-0
+    weights (HiC-GNN_main.py:126-130): the loss relative to the oracle's (exact-formula distances,
+    as the device computes them; the reference's mm-formula cdist value beside it)
+    and the coordinates as max |difference| / max |oracle coordinate|."""
+    c_dev = dev["coords"].double().cpu()
+    c_cpu = cpu["coords"].double()
+    coords_rel = float((c_dev - c_cpu).abs().max() / c_cpu.abs().max())
+    l_ref = cpu["loss_exact_cdist"]
+    loss_rel = abs(dev["loss"] - l_ref) / abs(l_ref)
+    l_mm = cpu["loss_reference_cdist"]
+    return {"step": 1, "loss_device": dev["loss"], "loss_oracle": l_ref, "loss_rel": loss_rel,
+            "coords_rel": coords_rel, "tol": PARITY_TOL, "pass": bool(loss_rel <= PARITY_TOL and coords_rel <= PARITY_TOL),
+            "loss_oracle_reference_cdist": l_mm, "loss_rel_reference_cdist": abs(dev["loss"] - l_mm) / abs(l_mm),
+            "note": "device step 1 (the first eager warm-up step, seed-0 weights) vs the CPU oracle's step 1 on "
+                    "the same workload: loss vs the oracle's MSE with exact-formula distances (the device's "
+                    "distances); loss_oracle_reference_cdist is the oracle's own training-loop value with torch's "
+                    "mm-formula cdist (the reference's arithmetic, SURVEY fact 8)"}
 
 
 def _free_port():
@@ -475,6 +512,12 @@ def main():
     # first replay (its upload to the device), so the timed region replays a resident graph
     n_eager = max(1, args.warmup - 1) if args.warmup >= 2 else max(1, args.warmup)
     replay_warm = args.warmup >= 2
+    # the first eager warm-up step is training step 1 from the seed-0 weights: its loss and forward
+    # coordinates are kept for the parity block (the CPU oracle's step 1 on the same workload)
+    first = step()
+    step1 = {"loss": float(first[0].item()), "coords": first[2].detach().clone()}
+    n_eager -= 1
+    done_warm = 1
     if args.graph and world > 1:
         try:
             step = runner.captured(warmup=n_eager)   # kernels + RCCL collectives in one graph
@@ -483,7 +526,7 @@ def main():
             log(f"[bench] rank {rank}: GRAPH CAPTURE OF THE SHARDED STEP FAILED ({exc}); timing eager steps")
             sync()
             args.graph = False
-            for w in range(args.warmup):
+            for w in range(done_warm, args.warmup):
                 step()
         if args.graph and replay_warm:
             step()
@@ -493,7 +536,7 @@ def main():
         if replay_warm:
             step()
     else:
-        for w in range(args.warmup):
+        for w in range(done_warm, args.warmup):
             step()
     sync()
     if world > 1 or args.selftest_cpu:
@@ -671,7 +714,9 @@ def main():
     if rank == 0 and world == 1 and not args.selftest_cpu and not args.no_cpu_baseline \
             and args.model == "GATNetSelectiveResidualsUpdated":
         log("[bench] cpu baseline (oracle) ...")
-        result["cpu_baseline"] = cpu_baseline(wl, args.seed, steps=args.cpu_steps, warmup=args.cpu_warmup)
+        cb = cpu_baseline(wl, args.seed, steps=args.cpu_steps, warmup=args.cpu_warmup)
+        result["parity"] = parity_block(step1, cb.pop("step1"))
+        result["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1 or args.selftest_cpu:

@@ -42,3 +42,25 @@ extern "C" int hicgat_sim_collective(float us, int workgroups, int threads, hicg
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
+
+// ---- streams and stamps -------------------------------------------------------------------------
+extern "C" int hicgat_stream_create(int priority, hicgat_stream_t *out) {
+  if (!out) return HICGAT_EINVAL;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority) != hipSuccess) return HICGAT_ELAUNCH;
+  *out = (hicgat_stream_t)s;
+  return HICGAT_OK;
+}
+
+// one wave; lane 0 writes (a per-lane vector store, like every other store of the library)
+__global__ __launch_bounds__(64) void wall_stamp_kernel(unsigned long long *out, int slot) {
+  const unsigned long long t = wall_clock64();
+  if (threadIdx.x == 0) out[slot] = t;
+}
+
+extern "C" int hicgat_wall_stamp(unsigned long long *out, int slot, hicgat_stream_t stream) {
+  if (!out || slot < 0 || (reinterpret_cast<uintptr_t>(out) & 7)) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(wall_stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out, slot);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}

@@ -236,8 +236,8 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
       else L2 = __builtin_elementwise_fma(r, r, L2);
       if (PEARSON) {
         sd2 += d;
-        if constexpr (!BG) {   // background form: t = bg at every pair, these four follow below
-          sdd2 = __builtin_elementwise_fma(d, d, sdd2);
+        sdd2 = __builtin_elementwise_fma(d, d, sdd2);
+        if constexpr (!BG) {   // background form: t = bg at every pair, these three follow below
           sdt2 = __builtin_elementwise_fma(d, tv[h], sdt2);
           st2 += tv[h];
           stt2 = __builtin_elementwise_fma(tv[h], tv[h], stt2);
@@ -272,16 +272,16 @@ __device__ __forceinline__ void tile_rows_pk(const float *tile, float bg, const 
   if (PEARSON) {
     const float sd = sd2.x + sd2.y;
     A.sd += sd;
+    A.sdd += sdd2.x + sdd2.y;   // summed directly in every form: sum (d - bg)^2 + bg (2 sum d - n bg)
+                                // cancels when d << bg (collapsed coordinates early in training)
     if constexpr (BG) {
-      // t = bg at all 8 (K1 - K0) pairs: sum d^2 = sum (d - bg)^2 + bg (2 sum d - n bg), sum d t =
-      // bg sum d, sum t and sum t^2 by count (four packed ops per two pairs out of the loop)
+      // t = bg at all 8 (K1 - K0) pairs: sum d t = bg sum d, sum t and sum t^2 by count (three packed
+      // ops per two pairs out of the loop)
       constexpr float npair = 8.f * (K1 - K0);
-      A.sdd += L + bg * fmaf(-npair, bg, 2.f * sd);
       A.sdt = fmaf(bg, sd, A.sdt);
       A.st = fmaf(npair, bg, A.st);
       A.stt = fmaf(npair * bg, bg, A.stt);
     } else {
-      A.sdd += sdd2.x + sdd2.y;
       A.sdt += sdt2.x + sdt2.y;
       A.st += st2.x + st2.y;
       A.stt += stt2.x + stt2.y;

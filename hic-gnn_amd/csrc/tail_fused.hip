@@ -22,6 +22,9 @@
 // held in LDS (torch.nn.LayerNorm: biased variance, eps 1e-5 inside the square root).
 #include "common.hpp"
 
+#include <mutex>
+#include <unordered_map>
+
 extern "C" size_t hicgat_ln_relu_res_workspace_bytes(int W);   // layernorm.hip
 
 namespace hicgat {
@@ -655,6 +658,23 @@ using namespace hicgat;
 
 extern "C" size_t hicgat_tail_pack_bytes(void) { return (size_t)kPackTotal * sizeof(float); }
 
+// What the last hicgat_tail_pack into each pack buffer wrote (host-side record): the head-fused
+// forms read the Wh regions, which a pack made with Wh = NULL leaves unwritten -- they refuse such
+// a pack (HICGAT_EINVAL) instead of reading uninitialised memory.
+namespace {
+std::mutex g_pack_mu;
+std::unordered_map<const void *, bool> g_pack_heads;
+void pack_note(const void *pack, bool heads) {
+  std::lock_guard<std::mutex> lk(g_pack_mu);
+  g_pack_heads[pack] = heads;
+}
+bool pack_has_heads(const void *pack) {
+  std::lock_guard<std::mutex> lk(g_pack_mu);
+  auto it = g_pack_heads.find(pack);
+  return it != g_pack_heads.end() && it->second;
+}
+}  // namespace
+
 extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
                                 hicgat_stream_t stream) {
   if (!W1c || !W2c || !pack) return HICGAT_EINVAL;
@@ -683,6 +703,7 @@ extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float 
   if (Wh) add(Wh, kPackBH, 512, 512, 1);
   hipLaunchKernelGGL(tail_pack_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, pj);
   HICGAT_CHECK_LAUNCH();
+  pack_note(pack, Wh != nullptr);
   return HICGAT_OK;
 }
 
@@ -737,6 +758,7 @@ int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const 
        (uintptr_t)hh.O | (uintptr_t)pack) & 15)
     return HICGAT_EUNSUPPORTED;
   if (pack) {
+    if (HEADS && !pack_has_heads(pack)) return HICGAT_EINVAL;   // packed without Wh
     const float *pk = static_cast<const float *>(pack);
     return tail_fwd_go<HEADS, true>(x, ldx, M, pk + kPackF1, b1c, g1, be1, pk + kPackF2, b2c, g2, be2, W3, b3, g3,
                                     be3, W4, b4, eps, Y1, st1, z1, Y2, st2, z2, y3, st3, z3, coords,
@@ -835,6 +857,7 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
       ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
     return HICGAT_EINVAL;
   if (pack) {
+    if (HEADS && !pack_has_heads(pack)) return HICGAT_EINVAL;   // packed without Wh
     const float *pk = static_cast<const float *>(pack);
     return tail_bwd_go<HEADS, true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1, g1, be1,
                                     g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1, ws2, ws3,

@@ -8,6 +8,8 @@ import os
 
 import torch
 
+from . import streams as _streams
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HICGAT_LIB lets tools/kbench.py A/B an alternative build of the same ABI in one process
 LIB_PATH = os.environ.get("HICGAT_LIB", os.path.join(_HERE, "libhicgat.so"))
@@ -148,6 +150,8 @@ SIGNATURES = {
     "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_int, c_p]),
     "hicgat_step_begin": (c_int, [c_p, c_i64, c_p, c_p]),
     "hicgat_sim_collective": (c_int, [c_f, c_int, c_int, c_p]),
+    "hicgat_stream_create": (c_int, [c_int, ctypes.POINTER(c_p)]),
+    "hicgat_wall_stamp": (c_int, [c_p, c_int, c_p]),
 }
 
 
@@ -197,7 +201,12 @@ def ptr(t):
 
 
 def stream(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current stream's handle for a launch; inside a graph capture it must be the capture's
+    origin or a stream forked into it (``streams.check_launch``)."""
+    h = torch.cuda.current_stream(device).cuda_stream
+    if _streams.LEDGER.active:
+        _streams.check_launch(h)
+    return ctypes.c_void_p(h)
 
 
 def workspace(nbytes, device):

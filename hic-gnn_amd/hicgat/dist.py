@@ -57,7 +57,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import ops, streams
 from .ops import _ACTS, weight_grad
 from .optim import FlatAdam
 
@@ -83,6 +83,10 @@ def resolve_mode(mode, P):
 # 0.489 ms; the tail's gradients and bucket alone on the side stream (the heads' dW and the GATConv
 # bucket after the edge pass): 0.495 / 0.497 (removed)
 XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "256"))
+# the xagg step's side branch (grouped dW + the flat-gradient all-reduce) on the "grad" stream beside
+# the edge pass; False: the same launches in the same order on the step's own stream (the serial
+# order tests/test_gpu_xagg.py compares the overlapped step against)
+XAGG_SIDE_BRANCH = True
 
 
 def _null():
@@ -346,12 +350,11 @@ class SimComm:
             lib = _lib.lib()
             cur = torch.cuda.current_stream(t.device)
             if self.last is not None:
-                cur.wait_event(self.last)
+                streams.wait(cur, self.last)
             _lib.check(lib.hicgat_sim_collective(float(coll_us(kind, t.numel() * t.element_size(), self.P)),
                                                  SIM_COMM_WGS, SIM_COMM_THREADS, _lib.stream(t.device)),
                        "hicgat_sim_collective")
-            self.last = torch.cuda.Event()
-            self.last.record(cur)
+            self.last = streams.record(cur)
         _record(name, kind, t, self.P, fn)
 
     def all_gather_inplace(self, buf, own, name="all_gather"):
@@ -483,8 +486,9 @@ class ShardedTrainer:
         firsts = [o for p, o in zip(self.opt.params, self.opt.offsets) if id(p) not in conv_ids]
         cut = (max(ends) + 3) // 4 * 4
         self.grad_split = cut if (firsts and min(firsts) >= cut) else None
-        self.comm_stream = torch.cuda.Stream(device=dev) if self.cuda else None
-        self.grad_stream = torch.cuda.Stream(device=dev) if self.cuda else None
+        # the device's persistent streams (hicgat.streams): every trainer of a process uses the same two
+        self.comm_stream = streams.get("comm", dev) if self.cuda else None
+        self.grad_stream = streams.get("grad", dev) if self.cuda else None
 
     def captured(self, warmup=2):
         """The step as one hipGraph (kernels + RCCL collectives, "nccl" backend only): one replay
@@ -553,7 +557,10 @@ class ShardedTrainer:
 
     def step(self):
         """One training step; returns (loss, stats, coords) with coords [N, 3] in global row order
-        (the coordinates the step's loss was evaluated on)."""
+        (the coordinates the step's loss was evaluated on).  All three are the trainer's persistent
+        buffers (a captured step refreshes them in place on every replay), so the next step
+        overwrites them: a caller that keeps a step's values across steps (best-dSCC tracking, a
+        history) must ``clone()`` them, as ``hicgat.train.train``'s callers of ``train_step`` do."""
         if hasattr(self.comm, "begin_step"):
             self.comm.begin_step()
         if self.mode == "xagg" and self.cuda:
@@ -576,28 +583,37 @@ class ShardedTrainer:
         return self.opt.step_ctr if (self.mode == "xagg" and self.cuda and
                                      getattr(self.opt, "step_ctr", None) is not None) else None
 
-    def _grad_allreduce(self, tail_done):   # the slab / allgather forms
-        """The flat gradient all-reduce in two buckets: the MLP tail's (on the comm stream, after
-        ``tail_done`` -- an event on the side stream after the tail's dW GEMMs, so it runs beside
-        lin_l's dW GEMM) and the GATConv's; the optimizer's stream waits for both."""
+    def _tail_bucket(self, tail_done):   # the slab / allgather forms
+        """The MLP tail's gradient bucket, all-reduced on the comm stream as soon as the side lanes'
+        tail dW launches are done (``tail_done``: events recorded on those lanes), beside lin_l's dW
+        GEMM.  Called INSIDE the overlapped-gradients block, before ``ops.side_join`` joins the lanes
+        back: a wait on a lane's event after that join is what aborted the round-5 captures
+        (``hicgat.streams`` rule 2)."""
         g, cut = self.opt.grad, self.grad_split
         if cut is None:
-            self.comm.all_reduce(g, name="grad_all_reduce")
             return
         if self.cuda:
             cs = self.comm_stream
             if tail_done:
                 for ev in tail_done:
-                    cs.wait_event(ev)
+                    streams.wait(cs, ev)
             else:                       # no side stream in use: the tail's gradients are on this one
-                cs.wait_stream(torch.cuda.current_stream())
+                streams.fork(cs, torch.cuda.current_stream())
             with torch.cuda.stream(cs):
                 self.comm.all_reduce(g[cut:], name="grad_all_reduce_tail_bucket")
-            self.comm.all_reduce(g[:cut], name="grad_all_reduce_gat_bucket")
-            torch.cuda.current_stream().wait_stream(cs)
         else:
             self.comm.all_reduce(g[cut:], name="grad_all_reduce_tail_bucket")
-            self.comm.all_reduce(g[:cut], name="grad_all_reduce_gat_bucket")
+
+    def _gat_bucket(self):
+        """The GATConv's gradient bucket (or the whole buffer when there is no split), then the
+        optimizer's stream joins the comm stream."""
+        g, cut = self.opt.grad, self.grad_split
+        if cut is None:
+            self.comm.all_reduce(g, name="grad_all_reduce")
+            return
+        self.comm.all_reduce(g[:cut], name="grad_all_reduce_gat_bucket")
+        if self.cuda:
+            streams.join(torch.cuda.current_stream(), self.comm_stream)
 
     def _side_event(self):
         """Events after the side streams' queued work (the tail's dW GEMMs), or None (CPU)."""
@@ -614,7 +630,6 @@ class ShardedTrainer:
                       self.out, self.out2, self.rs)
         o, coords_loc, coords = self._tail()
         # ---- backward -----------------------------------------------------------------------
-        tail_done = None
         dout = self.pack[:, :D]
         with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT, hold_big=False):
             coords_loc.backward(self.dcoords[r0:r1])
@@ -628,7 +643,7 @@ class ShardedTrainer:
             K.agg_bwd_src(self.rowptr_s, self.col_s, 0, N, self.h, a_src, a_dst, self.rs, dout, al, ar, self.ns,
                           self.dh, self.da_src, round_robin=True)
             ops.side_flush(after=fork, lanes=SIDE_LANES)
-            tail_done = self._side_event()
+            self._tail_bucket(self._side_event())
             with torch.no_grad():
                 # lin_l's partial dW over all rows (x replicated) on a side stream of its own (lane 2:
                 # beside the tail's dW GEMMs on lane 0, not queued behind them), the GAT parameter
@@ -643,7 +658,7 @@ class ShardedTrainer:
                          accumulate=True)
             K.param_grad(self.h[r0:r1], dout[r0:r1].contiguous(), None, self.rs[r0:r1], H,
                          out=(None, self.att_r.grad.view(-1), dbias), accumulate=True)
-        self._grad_allreduce(tail_done)
+        self._gat_bucket()
 
     def _step_xagg(self):
         """Aggregate-first GATConv (gat_xagg.hip): x replicated, every GEMM on own rows only."""
@@ -695,23 +710,34 @@ class ShardedTrainer:
             heads = [("w", self.dout_l[:, hd * C:(hd + 1) * C], self.X4[hd, 0], self.W.grad[hd * C:(hd + 1) * C],
                       None if self.bias is None else self.bias.grad[hd * C:(hd + 1) * C]) for hd in (0, 1)]
             side = None
-            if self.cuda:
+            if self.cuda and XAGG_SIDE_BRANCH:
                 side = self.grad_stream
-                side.wait_stream(torch.cuda.current_stream())
+                streams.fork(side, torch.cuda.current_stream())
             g_jobs = [("c", self.gpart, self.g_src, False),
                       ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)]
             # (the side work captured after the edge pass instead -- the edge pass first in the graph's
             # order -- measured slower: 0.485 / 0.491 vs 0.468 / 0.470 ms, profiles/r05l_sim_ab.txt)
+            # Buffers on the two branches until the join below.  The side branch reads dout_l, X4[:, 0],
+            # rs_own's columns, the tail's saved tensors, and reads + writes the flat gradient opt.grad
+            # (every gradient but the attention vectors', which stay 0 until the finish, and W's
+            # att (x) g term) through its all-reduce.  This branch (the edge pass, g's column sums and
+            # all-reduce) reads x, a_src, a_dst, rs, dxa, X4[:, 1] and writes ONLY gpart and gsd --
+            # nothing on it may touch opt.grad before the join (tests/test_gpu_xagg.py checks the
+            # numbers with a communicator whose all-reduce really changes the buffer).
             with torch.cuda.stream(side) if side is not None else _null():
+                streams.stamp("grad_begin")
                 keep = ops.grouped_flush(K, heads, target_wgs=XAGG_SIDE_WGS)
                 # every gradient but the attention vectors' (0 until the finish) and W's att (x) g term
                 self.comm.all_reduce(self.opt.grad, name="grad_all_reduce")
+                streams.stamp("grad_end")
+            streams.stamp("edge_begin")
             K.xagg_edge_acc(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.rs, self.dxa, self.ns,
                             self.gpart, xa2=self.X4[:, 1])
+            streams.stamp("edge_end")
             ops.grouped_flush(K, g_jobs)
             self.comm.all_reduce(self.gsd, name="g_all_reduce")
             if side is not None:
-                torch.cuda.current_stream().wait_stream(side)
+                streams.join(torch.cuda.current_stream(), side)
             del keep
             K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
                                 self.att_r.grad.view(-1))
@@ -728,7 +754,6 @@ class ShardedTrainer:
                       self.out, self.out2, self.rs)
         o, coords_loc, coords = self._tail()
         # ---- backward -----------------------------------------------------------------------
-        tail_done = None
         with ops.overlapped_param_grads(self.cuda and ops.OVERLAP_DEFAULT, hold_big=False):
             coords_loc.backward(self.dcoords[self.r0:self.r1])
             dout, rs_all = self.pack[:, :D], self.pack[:, D:]
@@ -743,7 +768,7 @@ class ShardedTrainer:
             K.agg_bwd_src(self.rowptr, self.col, q0, q1, self.h, a_src, a_dst, rs_all, dout, al, ar, self.ns,
                           self.dh, self.da_src)
             ops.side_flush(after=fork, lanes=SIDE_LANES)
-            tail_done = self._side_event()
+            self._tail_bucket(self._side_event())
             dbias = self.bias.grad if self.bias is not None else torch.empty(D, device=self.h.device)
             with torch.no_grad():
                 # lin_l's dW on the side stream (joined before the gradient all-reduce), param_grad
@@ -755,5 +780,5 @@ class ShardedTrainer:
                         self.W.grad.addmm_(self.dh[q0:q1].t(), self.x_loc)
             K.param_grad(self.h[q0:q1], dout[q0:q1].contiguous(), self.da_src[q0:q1], self.rs[q0:q1], self.H,
                          out=(self.att_l.grad.view(-1), self.att_r.grad.view(-1), dbias), accumulate=True)
-        self._grad_allreduce(tail_done)
+        self._gat_bucket()
 

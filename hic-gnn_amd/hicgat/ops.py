@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-from . import _lib, kernels
+from . import _lib, kernels, streams
 
 
 def _sink(p):
@@ -62,9 +62,7 @@ def side_mark():
     """An event on the current stream marking where queued side work may start (``side_flush``)."""
     if not _SIDE["on"] or not _SIDE["queue"]:
         return None
-    ev = torch.cuda.Event()
-    ev.record()
-    return ev
+    return streams.record()
 
 
 _FLUSH_LANES = (0, 4, 5, 6)
@@ -102,8 +100,10 @@ def side_flush(after=None, lanes=1):
             items = [q for q in items if q[2] < SMALL_WORK] + [q for q in items if q[2] >= SMALL_WORK]
         if items:
             with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
+                streams.stamp("side_begin")
                 for fn, _, _ in items:
                     fn()
+                streams.stamp("side_end")
 
 
 def side_record():
@@ -112,13 +112,8 @@ def side_record():
     if not _SIDE["on"]:
         return []
     with _SIDE_LOCK:
-        streams = [_SIDE["streams"][key] for key in _SIDE["mains"]]
-    evs = []
-    for st in streams:
-        ev = torch.cuda.Event()
-        ev.record(st)
-        evs.append(ev)
-    return evs
+        sides = [_SIDE["streams"][key] for key in _SIDE["mains"]]
+    return [streams.record(st) for st in sides]
 
 
 @contextlib.contextmanager
@@ -173,7 +168,7 @@ def side_join():
         with _SIDE_LOCK:
             _SIDE["on"] = max(0, _SIDE["on"] - 1)
             for key, main in _SIDE["mains"].items():
-                main.wait_stream(_SIDE["streams"][key])
+                streams.join(main, _SIDE["streams"][key])
             _SIDE["mains"].clear()
             _SIDE["hold"].clear()
 
@@ -237,13 +232,13 @@ def _side(*keep, after=None, lane=0):
     with _SIDE_LOCK:
         side = _SIDE["streams"].get(key)
         if side is None:
-            side = _SIDE["streams"][key] = torch.cuda.Stream(device=dev)
+            side = _SIDE["streams"][key] = streams.get(f"side{lane}", dev)
         _SIDE["mains"].setdefault(key, cur)
         _SIDE["hold"].extend(keep)
     if after is not None:
-        side.wait_event(after)
+        streams.wait(side, after)
     else:
-        side.wait_stream(cur)
+        streams.fork(side, cur)
     return torch.cuda.stream(side)
 
 
@@ -313,7 +308,9 @@ class _GATConvFn(torch.autograd.Function):
         if ctx.tiles is not None:
             K.agg_bwd_src_tiled(ctx.tiles, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
         else:
+            streams.stamp("src_begin")
             K.agg_bwd_src(rowptr, col, 0, N, h, a_src, a_dst, row_stats, dout, al, ar, ctx.ns, dh, da_src)
+            streams.stamp("src_end")
         side_flush(after=fork)
         # after the gathers: the GAT column sums, then lin_l's dW on this stream (with the held
         # first-block dW: BIG_GROUP).  The column sums on a side stream beside the grouped dW launch:

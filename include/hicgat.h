@@ -479,7 +479,9 @@ int hicgat_tail_fwd_fused(const float *x, int64_t ldx, int M, const float *W1c, 
  * 16 rows x 64 B: the vector memory path serves the row-major rows at 16 B per clock per CU, a quarter
  * of the contiguous rate, and that set the pace of the kernels' GEMM phases); results bitwise the
  * row-major form.  W3 / W4 are always read row-major.  hicgat_tail_pack_bytes(): the buffer's size.
- * Not a reference interface: the copies are a layout of the same parameters. */
+ * Not a reference interface: the copies are a layout of the same parameters.  The library records,
+ * per pack buffer, whether its last hicgat_tail_pack included Wh: the head-fused forms
+ * (hicgat_tail_{fwd,bwd}_fused_heads) return HICGAT_EINVAL for a pack made with Wh = NULL. */
 size_t hicgat_tail_pack_bytes(void);
 int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
                      hicgat_stream_t stream);
@@ -601,6 +603,17 @@ int hicgat_step_begin(float *grad, int64_t n, int64_t *step_counter, hicgat_stre
  * shows the modeled collective's duration, its overlap with the kernels on other streams and the
  * CU slots it holds.  Not used by the training path. */
 int hicgat_sim_collective(float us, int workgroups, int threads, hicgat_stream_t stream);
+
+/* ---- streams and stamps (host plumbing; no reference counterpart) ----------------------------
+ * A non-blocking HIP stream at `priority` (hipStreamCreateWithPriority), made ONCE per device and
+ * name by hicgat.streams and kept for the process: every side / comm / warm-up stream of the step
+ * is one of these, never a stream from torch's round-robin pool (which aliases after 32 requests),
+ * so two lanes of one step are always two streams.  *out receives the stream. */
+int hicgat_stream_create(int priority, hicgat_stream_t *out);
+/* out[slot] = the device's steady wall clock (100 MHz counter) when this one-wave launch runs on
+ * `stream`: enqueued at fork / join points of a captured step it records, per replay, when each
+ * branch started and ended (tests/test_gpu_overlap.py).  out 8-B aligned, slot >= 0. */
+int hicgat_wall_stamp(unsigned long long *out, int slot, hicgat_stream_t stream);
 #ifdef __cplusplus
 }
 #endif

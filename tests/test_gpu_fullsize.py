@@ -264,3 +264,95 @@ def test_synth20000_support_form_loss_matches_dense():
     assert _rel(res[0, "support"][1][rows], g_ref) < 1e-5
     print(f"support nnz {sf.nnz} ({sf.nnz / n / n:.2%}); mse {res[0, 'support'][0][7]:.9g} vs dense "
           f"{res[0, 'dense'][0][7]:.9g}")
+
+
+@pytest.mark.timeout(900)
+def test_synth20000_training_step_matches_oracle():
+    """BASELINE configs[2] -- bench.py's headline workload exactly (N = 20000, 1 % power-law contacts,
+    seed 0, 4.02 M edges): one whole training step of the flagship (forward, MSE, backward, Adam;
+    HiC-GNN_main.py:126-130) on the device against the CPU oracle from the same seed-0 weights
+    (exact-formula distances, as the device computes them): loss and coordinates to
+    1e-5 relative (the north star's bar), every gradient to 2e-4 of its tensor's max with the entries
+    a relu at rounding distance from its kink decides bounded by their flipped term
+    (tests/kinks.py::kink_bounds), and the Adam update wherever it does not hinge on the gradient's
+    rounding."""
+    import hicgat
+    from hicgat import synth
+    from kinks import compare_flat, kink_bounds
+    from oracle import gat as og
+    from oracle import graph as ogr
+    n = 20000
+    i, j, c = synth.contact_pairs(n, density=0.01, seed=0)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    xh = synth.features(n, seed=0)
+    x = torch.tensor(xh, device=DEV)
+    torch.manual_seed(0)
+    model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+    opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+    # kink masks / flipped-term bounds at the step-1 weights (the device's fp32 relu inputs)
+    cv = model.conv
+    with torch.no_grad():
+        out_pre = hicgat.ops.gat_conv(x, cv.lin_l.weight, cv.att_l, cv.att_r, cv.bias, adj)
+        c0 = model.get_model(x, adj)
+    cd = c0.detach().requires_grad_(True)
+    l0, _ = hicgat.ops.fused_dist_loss(cd, tr)
+    l0.backward()
+    masks, counts, bounds = kink_bounds(model, out_pre, cd.grad, x, adj.rowptr32, adj.col32)
+    del out_pre, cd, l0
+    loss, _, coords = hicgat.train.train_step(model, opt, x, adj, tr)
+    torch.cuda.synchronize()
+    loss_d = float(loss.item())
+    coords_d = coords.detach().cpu().clone()
+    g_dev = opt.grad.detach().clone()
+    params = {k: p.detach().cpu().clone() for k, p in model.named_parameters()}
+
+    # the oracle on the host: the CSR of the same pairs (utils.load_input's symmetric, sorted form),
+    # cont2dist of the same contacts, the same features and seed
+    rows = np.concatenate([i, j])
+    cols = np.concatenate([j, i])
+    order = np.lexsort((cols, rows))
+    rows, cols = rows[order], cols[order]
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(rp, rows + 1, 1)
+    radj = (torch.tensor(np.cumsum(rp)), torch.tensor(cols.astype(np.int64)))
+    y = torch.zeros((n, n), dtype=torch.float64)
+    y[torch.tensor(i), torch.tensor(j)] = torch.tensor(c)
+    y[torch.tensor(j), torch.tensor(i)] = torch.tensor(c)
+    t_ref = ogr.cont2dist(y, 0.5).float()
+    del y
+    torch.manual_seed(0)
+    ref = og.GATNetSelectiveResidualsUpdated()
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+    try:
+        c_ref = ref.get_model(torch.tensor(xh), radj)
+        l_ref = torch.nn.functional.mse_loss(torch.cdist(c_ref, c_ref, compute_mode=og.CDIST_MODE).float(), t_ref)
+        l_ref.backward()
+    finally:
+        og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+    rel_l = abs(loss_d - l_ref.item()) / l_ref.item()
+    rel_c = _rel(coords_d, c_ref.detach())
+    print(f"synth-20000 step 1: loss {loss_d:.9g} vs oracle {l_ref.item():.9g} (rel {rel_l:.2e}); coords rel {rel_c:.2e}; "
+          f"kinks {counts}")
+    assert rel_l < 1e-5 and rel_c < 1e-5
+    # the oracle's gradients in the device's flat layout
+    rg = dict(ref.named_parameters())
+    names = {id(p): k for k, p in model.named_parameters()}
+    g_ref = torch.zeros_like(g_dev)
+    for p, o in zip(opt.params, opt.offsets):
+        g_ref[o:o + p.numel()] = rg[names[id(p)]].grad.reshape(-1).to(g_ref.device)
+    per = compare_flat(model, zip(opt.params, opt.offsets), g_ref, g_dev, masks, bounds=bounds)
+    print("grad max excess / max |ref| (masked):", {k: f"{d / m:.1e} ({c_})" for k, (d, m, c_) in per.items()})
+    for k, (d, m, _) in per.items():
+        assert d <= 2e-4 * m, (k, d, m)
+    gscale = max(float(g_ref.abs().max()), 1e-30)
+    assert float(rg["dense3.bias"].grad.abs().max()) < 1e-3 * gscale        # 0 in exact arithmetic
+    ropt.step()
+    for k, pr in ref.named_parameters():
+        gr = pr.grad
+        sig = (gr.abs() > 1e-3 * gr.abs().max()) & (gr.abs() > 1e-6) & ~masks[k].cpu()
+        if sig.any():
+            assert float((params[k] - pr.detach()).abs()[sig].max()) < 1e-6, k

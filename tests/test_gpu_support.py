@@ -131,3 +131,32 @@ def test_dense_truth_keeps_the_dense_path():
     form: the loss streams the dense truth."""
     _, tr = _contacts_truth(600, None, 1)
     assert tr.support is None
+
+
+@pytest.mark.parametrize("n", [700, 2000])
+@pytest.mark.parametrize("scale", [1e-2, 1e-3])
+def test_support_pearson_with_collapsed_coordinates(n, scale):
+    """The combined loss's Pearson r (stats[8]) when the predicted distances are far below the
+    background distance 1 (coordinates at 0.01 / 0.001 of unit scale: early training or a collapsed
+    model).  The background form sums d^2 directly (the round-5 form rebuilt it as
+    sum (d - 1)^2 + (2 sum d - n), a difference of two ~n-sized terms in fp32 that would lose the
+    variance here): r, the moments and the total against an fp64 evaluation of the same pairs, and
+    against the dense-truth kernel."""
+    from scipy.stats import pearsonr
+    A, tr = _contacts_truth(n, 0.05, n + 1)
+    assert tr.support is not None
+    rng = np.random.default_rng(n)
+    c = torch.tensor((scale * rng.standard_normal((n, 3))).astype(np.float32), device=DEV)
+    r = _both(tr, c, 1)
+    (sd, _, _), (ss, _, _) = r["dense"], r["support"]
+    cd = c.double().cpu()
+    D = torch.cdist(cd, cd, compute_mode="donot_use_mm_for_euclid_dist")
+    iu = np.triu_indices(n, 1)
+    d = D.numpy()[iu]
+    t = tr.dense().double().cpu().numpy()[iu]
+    r64 = float(pearsonr(t, d)[0])
+    sdd64 = float(np.sum(d * d))
+    print(f"n={n} scale={scale}: r support {ss[8]:.9g} dense {sd[8]:.9g} fp64 {r64:.9g}; "
+          f"sum d^2 support {ss[2]:.9g} fp64 {sdd64:.9g}")
+    assert abs(ss[2] - sdd64) <= 1e-5 * sdd64
+    assert abs(ss[8] - r64) <= 1e-5 and abs(sd[8] - r64) <= 1e-5

@@ -205,3 +205,55 @@ def test_param_grads_grouped_matches_float64(target):
     print(target, {k: f"{v:.1e}" for k, v in errs.items()})
     assert all(v < 1e-5 for v in errs.values()), errs
     assert all(torch.equal(res[0][k], res[1][k]) for k in outs)
+
+
+@pytest.mark.parametrize("n,world", [(3000, 2), (20000, 8)])
+def test_xagg_side_branch_equals_serial_order_with_a_real_reduce(n, world):
+    """The xagg step runs its side branch (grouped dW, then the all-reduce of the WHOLE flat
+    gradient) on the "grad" stream while the edge pass, g's column sums and g's all-reduce run on the
+    step's stream.  That is correct only if nothing on the step's stream touches opt.grad between the
+    fork and the join.  A communicator whose all-reduce really changes its buffer in place on the
+    issuing stream (t *= P, as a sum over P equal ranks would) makes any such race visible: the
+    captured overlapped step must replay bit-equal to the same launches in serial order
+    (dist.XAGG_SIDE_BRANCH = False), gradients and parameters, over three replays."""
+    for p in (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import hicgat
+    from hicgat import dist as hdist
+    from hicgat import synth
+
+    class ScaleComm(hdist.SimComm):
+        def __init__(self, P, rank):
+            super().__init__(P, rank, emulate=False)
+
+        def all_reduce(self, t, name="all_reduce"):
+            t.mul_(float(self.P))
+
+    density, seed = (0.01, 0) if n == 20000 else (0.05, 3)
+    i, j, c = synth.contact_pairs(n, density=density, seed=seed)
+    A = synth.dense_contacts(n, i, j, c, device="cuda")
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    truth = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    x = torch.tensor(synth.features(n, seed=seed), device="cuda")
+    res = {}
+    saved = hdist.XAGG_SIDE_BRANCH
+    try:
+        for side in (False, True):
+            hdist.XAGG_SIDE_BRANCH = side
+            torch.manual_seed(0)
+            model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+            tr = hdist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode="xagg", comm=ScaleComm(world, 0))
+            step = tr.captured(warmup=1)
+            out = []
+            for _ in range(3):
+                loss = float(step()[0])
+                out.append((loss, tr.opt.grad.clone(), tr.opt.flat.clone()))
+            torch.cuda.synchronize()
+            res[side] = out
+            del step, tr, model
+    finally:
+        hdist.XAGG_SIDE_BRANCH = saved
+    for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
+        assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)

@@ -5,6 +5,8 @@
 #
 # steps (each under its own time limit; the script stops at the first failure):
 #   tests        pytest -m gpu (whole GPU suite)
+#   testsall     the same, test failures do not stop the later steps
+#   probe_capture tools/capture_probe.py (legal order, then the round-5 slab order; put it LAST)
 #   tests:<k>    pytest -m gpu -k <k>   (testsoft:<k>: test failures do not stop the later steps)
 #   testenv:<env>:<k> pytest -m gpu -k <k> under an environment assignment
 #   smoke        __graft_entry__.smoke()
@@ -41,6 +43,17 @@ for S in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread \
         > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_gpu.log; [ $rc -eq 0 ] || exit $rc ;;
+    testsall)
+      # the whole suite; test failures (rc 1) do not stop the later steps, a crash / timeout does
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread \
+        > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest_gpu.log; [ $rc -le 1 ] || exit $rc ;;
+    probe_capture)
+      # tools/capture_probe.py: the legal fork / join order, then the round-5 slab order (streams rule 2)
+      # -- LAST in a call: the second may crash its process
+      timeout -k 10 120 python tools/capture_probe.py ok > gpurun_out/${T}_capture_probe.txt 2>&1 || exit $?
+      timeout -k 10 120 python tools/capture_probe.py rule2 >> gpurun_out/${T}_capture_probe.txt 2>&1; rc=$?
+      echo "rule2 probe exit status $rc" >> gpurun_out/${T}_capture_probe.txt
+      grep -v amdgpu.ids gpurun_out/${T}_capture_probe.txt ;;
     tests:*|testsoft:*)
       K=${S#tests:}; K=${K#testsoft:}
       timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf -s --timeout 300 --timeout-method thread -k "$K" \
