@@ -148,11 +148,13 @@ for S in "$@"; do
       E=${S#probe}; E=${E#:}; G=""; [ "$S" = probegrads ] && { E=""; G="--grads"; }
       env $E timeout -k 10 300 python tools/xagg_probe.py $G > gpurun_out/${T}_probe.txt 2>&1 || exit $?
       grep " us$" gpurun_out/${T}_probe.txt ;;
-    simprof|simprof_ag|simprof_xa)
-      M=slab; [ "$S" = simprof_ag ] && M=allgather; [ "$S" = simprof_xa ] && M=xagg
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${S} -o run --output-format csv -- \
-        python bench.py --simulate-world 8 --sim-rank 0 --dist-mode $M --steps 20 --warmup 3 > gpurun_out/${T}_${S}.log 2>&1 || exit $?
-      python tools/step_timeline.py gpurun_out/${T}_${S}/run_kernel_trace.csv 10 > gpurun_out/${T}_${S}_timeline.txt || exit $?
+    simprof|simprof_ag|simprof_xa|simprof:*|simprof_ag:*|simprof_xa:*)
+      # optional :<P> (default 8): rank 0 of the simulated P-rank step
+      B=${S%%:*}; PP=8; [ "$B" != "$S" ] && PP=${S#*:}
+      M=slab; [ "$B" = simprof_ag ] && M=allgather; [ "$B" = simprof_xa ] && M=xagg
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${B}_P$PP -o run --output-format csv -- \
+        python bench.py --simulate-world $PP --sim-rank 0 --dist-mode $M --steps 20 --warmup 3 > gpurun_out/${T}_${B}_P$PP.log 2>&1 || exit $?
+      python tools/step_timeline.py gpurun_out/${T}_${B}_P$PP/run_kernel_trace.csv 10 > gpurun_out/${T}_${B}_P${PP}_timeline.txt || exit $?
       echo "$S ok" ;;
     align)
       # python -m hicgat.align (HiC_GAT_generalize_directly.py's flow) on GM12878 chr19 1 mb -> 500 kb,
