@@ -26,13 +26,14 @@ itself still ends cleanly before the error propagates.  Outside a capture the fu
 stream operations (events are still tagged, so an event from an eager step cannot be waited on in
 a later capture).
 
-Rule 2 is the round-5 abort (a ``capture_end`` segfault and a core dump, both in the slab form with
-the simulated communicator; DESIGN.md section 6, "Streams and capture"): the slab step recorded
-events on the side lanes after their parameter-gradient launches, joined the lanes back
-(``ops.side_join``), and only then made the comm stream wait on those events before its gradient
-all-reduce.  The HIP runtime attaches a stream that waits on an event inside a capture to the
-capture of the event's stream; after the join that stream's capture state is gone, and the comm
-stream was attached to nothing.
+Rule 2 is the pattern the round-5 slab step had when its captures aborted (a ``capture_end``
+segfault and a core dump, both in the slab form with the simulated communicator; DESIGN.md section
+6, "Streams and capture"): it recorded events on the side lanes after their parameter-gradient
+launches, joined the lanes back (``ops.side_join``), and only then made the comm stream wait on
+those events before its gradient all-reduce.  The bare pattern alone did not fault in a standalone
+probe (tools/capture_probe.py); the streams of the same runs also aliased through torch's pool (see
+above).  Both are gone, and the ledger keeps the step inside the fork / join forms that are known
+to replay.
 """
 import ctypes
 import threading
