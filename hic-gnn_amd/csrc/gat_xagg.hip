@@ -629,13 +629,15 @@ __global__ __launch_bounds__(256) void xagg_colred_kernel(const float *__restric
 
 // ---- dW[w, :] += att_src[w] g_src[h, :] + att_dst[w] g_dst[h, :]; datt[w] += <W[w, :], g[h, :]> -----
 // one block per row w = 256 h + c of W (512 rows), 256 threads over its 512 columns
+// g in `segs` segments (seg_stride floats apart), added in segment order
 __global__ __launch_bounds__(256) void xagg_param_finish_kernel(const float *__restrict__ W,
                                                                 const float *__restrict__ att_s,
                                                                 const float *__restrict__ att_d,
                                                                 const float *__restrict__ g_src,
                                                                 const float *__restrict__ g_dst,
                                                                 float *__restrict__ dW, float *__restrict__ datt_s,
-                                                                float *__restrict__ datt_d) {
+                                                                float *__restrict__ datt_d, int segs,
+                                                                int64_t seg_stride) {
   __shared__ float red[2][4];
   const int w = blockIdx.x, hd = w >> 8, t = threadIdx.x;
   const float as = att_s[w], adv = att_d[w];
@@ -643,7 +645,11 @@ __global__ __launch_bounds__(256) void xagg_param_finish_kernel(const float *__r
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int k = q * 256 + t;
-    const float gs = g_src[hd * 512 + k], gd = g_dst[hd * 512 + k];
+    float gs = g_src[hd * 512 + k], gd = g_dst[hd * 512 + k];
+    for (int sg = 1; sg < segs; ++sg) {
+      gs += g_src[sg * seg_stride + hd * 512 + k];
+      gd += g_dst[sg * seg_stride + hd * 512 + k];
+    }
     const float wk = W[(size_t)w * 512 + k];
     dW[(size_t)w * 512 + k] += fmaf(as, gs, adv * gd);
     ps = fmaf(wk, gs, ps);
@@ -789,7 +795,20 @@ extern "C" int hicgat_xagg_param_finish(const float *W, const float *att_src, co
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (!W || !att_src || !att_dst || !g_src || !g_dst || !dW || !datt_src || !datt_dst) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_param_finish_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, W, att_src, att_dst,
-                     g_src, g_dst, dW, datt_src, datt_dst);
+                     g_src, g_dst, dW, datt_src, datt_dst, 1, (int64_t)0);
+  HICGAT_CHECK_LAUNCH();
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_param_finish_seg(const float *W, const float *att_src, const float *att_dst,
+                                            const float *g_src, const float *g_dst, int segs, int64_t seg_stride,
+                                            int F, int H, int C, float *dW, float *datt_src, float *datt_dst,
+                                            hicgat_stream_t stream) {
+  if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
+  if (!W || !att_src || !att_dst || !g_src || !g_dst || !dW || !datt_src || !datt_dst) return HICGAT_EINVAL;
+  if (segs < 1 || (segs > 1 && seg_stride < 1024)) return HICGAT_EINVAL;
+  hipLaunchKernelGGL(xagg_param_finish_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, W, att_src, att_dst,
+                     g_src, g_dst, dW, datt_src, datt_dst, segs, seg_stride);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }

@@ -355,8 +355,9 @@ struct CJob {
   const float *src;
   float *dst;
   const float *wt;    // optional row weights (stride ldw)
-  int64_t ld, rows, cols, ldw;
+  int64_t ld, rows, cols, ldw, ldd;
   int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (6: 4 groups ... 2: 64 groups)
+  int segs, nchunk;   // row segments (segment s of the rows into dst + s * ldd), column chunks per segment
 };
 struct CJobs {
   int start[kMaxCJobs];   // job k's first block (= j[k].blk0)
@@ -376,8 +377,10 @@ __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
   // one lane stays short either way
   const int L = 1 << J.lg, ng = 256 >> J.lg;
   const int lane = threadIdx.x & (L - 1), g = threadIdx.x >> J.lg;
-  const int64_t c = ((int64_t)(blockIdx.x - J.blk0) * L + lane) * 4;   // first of this lane's 4 columns
-  const int64_t r0 = J.rows * g / ng, r1 = J.rows * (g + 1) / ng;
+  const int lb = blockIdx.x - J.blk0, seg = lb / J.nchunk;
+  const int64_t c = ((int64_t)(lb - seg * J.nchunk) * L + lane) * 4;   // first of this lane's 4 columns
+  const int64_t s0 = J.rows * seg / J.segs, sn = J.rows * (seg + 1) / J.segs - s0;   // the block's row segment
+  const int64_t r0 = s0 + sn * g / ng, r1 = s0 + sn * (g + 1) / ng;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < J.cols) {
     const bool vec = J.vec;
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
     __syncthreads();
   }
   if (g != 0 || c >= J.cols) return;
-  float *d = J.dst + c;
+  float *d = J.dst + (int64_t)seg * J.ldd + c;
   const float o[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e)
@@ -596,26 +599,33 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
   float *slab = static_cast<float *>(workspace);
   size_t used = 0;
   auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc,
-                     const float *wt = nullptr, int64_t ldw = 0) {
+                     const float *wt = nullptr, int64_t ldw = 0, int segs = 1, int64_t ldd = 0) {
     if (cols <= 0) return HICGAT_OK;
     if (cj.n == kMaxCJobs) return HICGAT_EUNSUPPORTED;
+    if (segs < 1) segs = 1;
+    if (segs > 1 && (ldd < cols || rows < segs)) return HICGAT_EINVAL;
     CJob &J = cj.j[cj.n++];
     J.src = src;
     J.dst = dst;
     J.wt = wt;
     J.ld = ld;
     J.ldw = ldw;
+    J.ldd = ldd;
+    J.segs = segs;
     J.rows = rows;
     J.cols = cols;
     J.accumulate = acc;
-    J.vec = (cols % 4 == 0 && ld % 4 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
-    // lanes per row group (one lane per group for the tallest jobs, uncoalesced, measured slower:
-    // P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
-    J.lg = rows <= 64 ? 6 : rows <= 256 ? 4 : (wt && rows > WEIGHTED_LG1_ROWS) ? kWeightedLg : 2;
+    J.vec = (cols % 4 == 0 && ld % 4 == 0 && (segs == 1 || ldd % 4 == 0) &&
+             ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
+    // lanes per row group by the rows of one segment (one lane per group for the tallest jobs,
+    // uncoalesced, measured slower: P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
+    const int64_t srows = (rows + segs - 1) / segs;
+    J.lg = srows <= 64 ? 6 : srows <= 256 ? 4 : (wt && srows > WEIGHTED_LG1_ROWS) ? kWeightedLg : 2;
     J.blk0 = blk;
     cj.start[cj.n - 1] = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block
-    blk += (int)((cols + per - 1) / per);
+    J.nchunk = (int)((cols + per - 1) / per);
+    blk += J.nchunk * segs;
     return HICGAT_OK;
   };
   for (int i = 0; i < nw; ++i) {
@@ -662,7 +672,8 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
   for (int i = 0; i < nc; ++i) {
     if (c[i].rows < 0 || c[i].cols < 0 || (c[i].cols > 0 && !c[i].dst) || (c[i].rows > 0 && !c[i].src))
       return HICGAT_EINVAL;
-    const int rc = add_col(c[i].src, c[i].ld, c[i].rows, c[i].cols, c[i].dst, c[i].accumulate, c[i].wt, c[i].ldw);
+    const int rc = add_col(c[i].src, c[i].ld, c[i].rows, c[i].cols, c[i].dst, c[i].accumulate, c[i].wt, c[i].ldw,
+                           c[i].segs, c[i].ldd);
     if (rc != HICGAT_OK) return rc;
   }
   if (wg > 0) {

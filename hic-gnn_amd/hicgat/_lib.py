@@ -28,7 +28,7 @@ class WgradJob(ctypes.Structure):
 class ColsumJob(ctypes.Structure):
     """include/hicgat.h hicgat_colsum_job."""
     _fields_ = [("src", c_p), ("ld", c_i64), ("rows", c_i64), ("cols", c_i64), ("dst", c_p), ("accumulate", c_int),
-                ("wt", c_p), ("ldw", c_i64)]
+                ("wt", c_p), ("ldw", c_i64), ("segs", c_int), ("ldd", c_i64)]
 
 
 class GemmJob(ctypes.Structure):
@@ -103,6 +103,8 @@ SIGNATURES = {
     "hicgat_xagg_slab_workspace_bytes": (c_sz, []),
     "hicgat_xagg_slab_sum": (c_int, [c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_xagg_param_finish": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
+    "hicgat_xagg_param_finish_seg": (c_int, [c_p, c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_int, c_int, c_p, c_p,
+                                             c_p, c_p]),
     "hicgat_pairdist_mse_fused_support_range": (c_int, [c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64, c_int,
                                                         c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_pairdist_mse_fused_support_range_ex": (c_int, [c_p, c_p, c_int, c_f, c_p, c_p, c_p, c_p, c_i64, c_i64,

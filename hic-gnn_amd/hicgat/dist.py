@@ -87,6 +87,8 @@ XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "256"))
 # the edge pass; False: the same launches in the same order on the step's own stream (the serial
 # order tests/test_gpu_xagg.py compares the overlapped step against)
 XAGG_SIDE_BRANCH = True
+# row segments of the xagg step's g sums (the g all-reduce then moves S x 8 KB)
+XAGG_G_SEGS = int(os.environ.get("HICGAT_XAGG_G_SEGS", "8"))
 
 
 def _null():
@@ -448,9 +450,11 @@ class ShardedTrainer:
             self.gpart = torch.zeros((kern.edge_acc_blocks(Rl), 2 * F), **f32)   # g_src partial rows
             self.a_src = torch.zeros((N, self.H), **f32)
             self.a_dst = torch.zeros((N, self.H), **f32)
-            # [g_src | g_dst] (the edge pass's partial sums), one buffer: the step's second all-reduce
-            self.gsd = torch.zeros(2, 2 * F, **f32)
-            self.g_src, self.g_dst = self.gsd[0], self.gsd[1]
+            # [g_src | g_dst] (the edge pass's partial sums) in S row segments, one buffer: the step's
+            # second all-reduce; the finish adds the segments (XAGG_G_SEGS)
+            S = max(1, min(XAGG_G_SEGS, Rl)) if self.cuda else 1
+            self.gsd = torch.zeros(S, 2, 2 * F, **f32)
+            self.g_src, self.g_dst = self.gsd[:, 0], self.gsd[:, 1]
             rows = 0                                                       # no [N, D] node buffers
         self.h = torch.zeros((rows, D), **f32)
         self.out = torch.zeros((rows, D), **f32)
@@ -713,8 +717,16 @@ class ShardedTrainer:
             if self.cuda and XAGG_SIDE_BRANCH:
                 side = self.grad_stream
                 streams.fork(side, torch.cuda.current_stream())
-            g_jobs = [("c", self.gpart, self.g_src, False),
-                      ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst.view(H, F), None, False)]
+            # g_src = column sums of the edge pass's partial rows, g_dst^h = sum_i da_dst_i^h x_i over own
+            # rows: tall sums (rows / 2 and rows), taken in the S row segments of gsd -- S x the blocks of
+            # one sum per column chunk (profiles/r06b: 51 us at P = 2, 16 at P = 8 as one sum)
+            if self.cuda:
+                g_jobs = [("c", self.gpart, self.g_src, False)] + [
+                    ("c", self.x[r0:r1], self.g_dst[:, hd * F:(hd + 1) * F], False, rs_own[:, 3 * H + hd])
+                    for hd in range(H)]
+            else:
+                g_jobs = [("c", self.gpart, self.g_src[0], False),
+                          ("w", rs_own[:, 3 * H:4 * H], self.x[r0:r1], self.g_dst[0].view(H, F), None, False)]
             # (the side work captured after the edge pass instead -- the edge pass first in the graph's
             # order -- measured slower: 0.485 / 0.491 vs 0.468 / 0.470 ms, profiles/r05l_sim_ab.txt)
             # Buffers on the two branches until the join below.  The side branch reads dout_l, X4[:, 0],
@@ -739,7 +751,8 @@ class ShardedTrainer:
             if side is not None:
                 streams.join(torch.cuda.current_stream(), side)
             del keep
-            K.xagg_param_finish(W, al, ar, self.g_src, self.g_dst, self.W.grad, self.att_l.grad.view(-1),
+            K.xagg_param_finish(W, al, ar, self.g_src if self.cuda else self.g_src[0],
+                                self.g_dst if self.cuda else self.g_dst[0], self.W.grad, self.att_l.grad.view(-1),
                                 self.att_r.grad.view(-1))
 
     def _step_allgather(self):

@@ -279,7 +279,15 @@ class HipKernels:
                                                      ws.numel(), _lib.stream(ds.device)), "hicgat_xagg_slab_sum")
 
     def xagg_param_finish(self, W, att_l, att_r, g_src, g_dst, dW, datt_l, datt_r):
+        """``g_src`` / ``g_dst``: [2 * 512] or, segmented, [segs, 2 * 512] views (the segments are added)."""
         H, C = att_l.shape[-2], att_l.shape[-1]
+        if g_src.dim() == 2:
+            assert g_dst.shape == g_src.shape and g_src.stride(0) == g_dst.stride(0) and g_src.stride(1) == 1
+            _lib.check(self.lib.hicgat_xagg_param_finish_seg(P(W), P(att_l), P(att_r), P(g_src), P(g_dst),
+                                                             g_src.shape[0], g_src.stride(0), W.shape[1], H, C, P(dW),
+                                                             P(datt_l), P(datt_r), _lib.stream(W.device)),
+                       "hicgat_xagg_param_finish_seg")
+            return
         _lib.check(self.lib.hicgat_xagg_param_finish(P(W), P(att_l), P(att_r), P(g_src), P(g_dst), W.shape[1], H, C,
                                                      P(dW), P(datt_l), P(datt_r), _lib.stream(W.device)),
                    "hicgat_xagg_param_finish")
@@ -440,10 +448,16 @@ class HipKernels:
         for k, job in enumerate(cjobs):
             src, dst, acc = job[:3]
             wt = job[3] if len(job) > 3 else None
-            assert src.dim() == 2 and src.stride(1) == 1 and dst.is_contiguous() and dst.numel() == src.shape[1]
+            assert src.dim() == 2 and src.stride(1) == 1
+            if dst.dim() == 2:    # [segs, cols]: the rows summed in segs segments, one dst row each
+                assert dst.stride(1) == 1 and dst.shape[1] == src.shape[1] and 1 <= dst.shape[0] <= max(1, src.shape[0])
+                segs, ldd = dst.shape[0], dst.stride(0)
+            else:
+                assert dst.is_contiguous() and dst.numel() == src.shape[1]
+                segs, ldd = 1, 0
             assert wt is None or (wt.dim() == 1 and wt.shape[0] == src.shape[0])
             C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(), int(acc),
-                                  None if wt is None else wt.data_ptr(), 0 if wt is None else wt.stride(0))
+                                  None if wt is None else wt.data_ptr(), 0 if wt is None else wt.stride(0), segs, ldd)
         dev = (wjobs[0][0] if wjobs else cjobs[0][0]).device
         ws = _lib.workspace(self.lib.hicgat_param_grads_workspace_bytes(W, len(wjobs), target), dev)
         with _timed("param_grads_grouped"):

@@ -148,9 +148,11 @@ def grouped_flush(K=None, extra=(), target_wgs=None):
     if not jobs:
         return []
     K = K if K is not None else kernels.default()
-    # descriptors: ("w", dy, x, dW, db[, accumulate]) / ("c", src, dst[, accumulate]); accumulate defaults on
+    # descriptors: ("w", dy, x, dW, db[, accumulate]) / ("c", src, dst[, accumulate[, row weights]]);
+    # accumulate defaults on; a 2-D dst [segs, cols] takes the rows' sum in segments (kernels.param_grads_grouped)
     w = [(j[1], j[2], j[3], j[4], j[5] if len(j) > 5 else True) for j, _ in jobs if j[0] == "w"]
-    c = [(j[1], j[2], j[3] if len(j) > 3 else True) for j, _ in jobs if j[0] == "c"]
+    c = [(j[1], j[2], j[3] if len(j) > 3 else True) + ((j[4],) if len(j) > 4 else ()) for j, _ in jobs
+         if j[0] == "c"]
     K.param_grads_grouped(w, c, target_wgs)
     return [t for _, keep in jobs for t in keep]
 

@@ -202,6 +202,11 @@ int hicgat_xagg_slab_sum(const int32_t *rowptr_s, const int32_t *perm, int N, co
 int hicgat_xagg_param_finish(const float *W, const float *att_src, const float *att_dst, const float *g_src,
                              const float *g_dst, int F, int H, int C, float *dW, float *datt_src, float *datt_dst,
                              hicgat_stream_t stream);
+/* The same with g in `segs` segments (the segmented column sums of hicgat_param_grads_grouped):
+ * g_src = sum over s of g_src + s * seg_stride (floats), g_dst likewise, added in segment order. */
+int hicgat_xagg_param_finish_seg(const float *W, const float *att_src, const float *att_dst, const float *g_src,
+                                 const float *g_dst, int segs, int64_t seg_stride, int F, int H, int C, float *dW,
+                                 float *datt_src, float *datt_dst, hicgat_stream_t stream);
 
 /* ---- a4+a5 and the source pass with the dense tiles on the matrix cores (gat_tiles.hip) -------
  * The same results as hicgat_gat_agg_fwd_act / hicgat_gat_agg_bwd_src_ld (fp32; the tiles' sums are
@@ -406,6 +411,9 @@ typedef struct hicgat_colsum_job {
   int accumulate;
   const float *wt;    /* NULL, or row weights: dst[c] (+)= sum_r wt[r * ldw] src[r * ld + c] (a dW row of a */
   int64_t ldw;        /* weight gradient with a handful of output rows, e.g. dense3's 3 x 64) */
+  int segs;           /* <= 1: one sum into dst; else the rows in `segs` contiguous segments, segment s */
+  int64_t ldd;        /* (rows [rows s / segs, rows (s + 1) / segs)) into dst + s * ldd: a tall job's sum
+                       * spread over segs x more blocks, the segments added by the consumer */
 } hicgat_colsum_job;
 size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *wjobs, int nw, int target_wgs);
 int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
