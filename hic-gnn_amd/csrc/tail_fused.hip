@@ -402,8 +402,8 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
                                             int64_t ldy, const float2 *__restrict__ stats,
                                             const float *__restrict__ gamma, const float *__restrict__ beta,
                                             float *__restrict__ Gs, int lds, float *__restrict__ dY,
-                                            float *__restrict__ part, int slot, float *__restrict__ red, int rsd,
-                                            int m0, int M, int wv, int lane) {
+                                            float *__restrict__ part, int slot, float *__restrict__ red, int m0,
+                                            int M, int wv, int lane) {
   constexpr int V = W / 64, LDY = RES ? 2 * W : W;
   float g_[V], b_[V], pg[V], pb[V];
 #pragma unroll
@@ -443,19 +443,18 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
       if (live) dY[(size_t)row * LDY + q * 64 + lane] = v;
     }
   }
-  // the NW waves' partials added in wave order through LDS (red: 2 NW rows of W floats, row stride
-  // rsd), one [2W] row per workgroup (slot = blockIdx.x): at 16 waves a wave holds one row, and
-  // per-wave rows would double the grouped column sum's input
+  // the NW waves' partials added in wave order through LDS (red: [NW][2W] floats), one [2W] row per
+  // workgroup (slot = blockIdx.x): at 16 waves a wave holds one row, and per-wave rows would double the
+  // grouped column sum's input
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    red[(wv * 2 + 0) * rsd + q * 64 + lane] = pg[q];
-    red[(wv * 2 + 1) * rsd + q * 64 + lane] = pb[q];
+    red[(wv * 2 + 0) * W + q * 64 + lane] = pg[q];
+    red[(wv * 2 + 1) * W + q * 64 + lane] = pb[q];
   }
   __syncthreads();
   for (int c = wv * 64 + lane; c < 2 * W; c += NW * 64) {
-    const int k = c >= W ? 1 : 0, cc = c - k * W;
-    float v = red[k * rsd + cc];
-    for (int w = 1; w < NW; ++w) v += red[(w * 2 + k) * rsd + cc];
+    float v = red[c];
+    for (int w = 1; w < NW; ++w) v += red[w * 2 * W + c];
     part[(size_t)slot * 2 * W + c] = v;
   }
   __syncthreads();   // red is reused by the next call
@@ -482,12 +481,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // dz3, dz2, dz1 rows
   float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
-  // the LayerNorm parameter partials, 2 NW rows of W <= 256 floats: when the block has 2 NW rows
-  // (RB = 32), in the columns 256 .. 511 of As, which the dz rows (W <= 256 wide) leave free while
-  // ln_bwd_rows runs (132 KiB of LDS instead of 164); else in a region of their own after Bs
-  constexpr bool RS_IN_AS = 2 * NW <= RB;
-  float *Rs = RS_IN_AS ? lds_tail + 256 : lds_tail + 2 * RB * XS;
-  constexpr int RSD = RS_IN_AS ? XS : 256;
+  float *Rs = lds_tail + 2 * RB * XS;   // [NW][2W] LayerNorm parameter partials (W <= 256)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int slot = blockIdx.x;
   const int m0 = blockIdx.x * RB;
@@ -504,7 +498,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     As[r * XS + c] = s;
   }
   __syncthreads();
-  ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, Rs, RSD, m0, M, wv, lane);
+  ln_bwd_rows<RB, 64, false, NW>(As, XS, y3, 64, st3, g3, be3, Bs, XS, dy3, p3, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // dense2 backward: dz2 = dy3 W3 ([RB x 64] [64 x 128]), wave wv: columns 16 ND wv ..
   constexpr int WD = NW < 8 ? NW : 8, ND = 8 / WD, NT2 = 16 / NW, NT1 = 32 / NW;   // dense2: WD waves
@@ -519,7 +513,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     put_tiles<RB, ND>(acc, 16 * ND * wd, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
-  ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, Rs, RSD, m0, M, wv, lane);
+  ln_bwd_rows<RB, 128, true, NW>(As, XS, Y2, 256, st2, g2, be2, Bs, XS, dY2, p2, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // block 2 backward: dz1 = [dy2 | dres2] [W_1; W_1al] ([RB x 256] [256 x 256]), wave wv: columns 16 NT2 wv ..
   {
@@ -532,7 +526,7 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     put_tiles<RB, NT2>(acc, 16 * NT2 * ws, As, XS, nullptr, 0, m0, M, lane);
   }
   __syncthreads();
-  ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, Rs, RSD, m0, M, wv, lane);
+  ln_bwd_rows<RB, 256, true, NW>(As, XS, Y1, 512, st1, g1, be1, Bs, XS, dY1, p1, slot, Rs, m0, M, wv, lane);
   __syncthreads();
   // block 1 backward: dx = [dy1 | dres1] [W_a; W_al] ([RB x 512] [512 x 512]), wave wv: columns 16 NT1 wv ..
   {
@@ -721,23 +715,7 @@ struct TailHeads {   // the HEADS operands of the head-fused forms (all null: th
   float *Y0 = nullptr, *O = nullptr;
 };
 
-// Rows per workgroup by row count (one workgroup of 16 waves per CU either way): 32 rows halve the
-// weight rows each workgroup streams from L2 per node row (the 1.3 MB of W1c / W2c once per
-// workgroup: 1.6 GB per launch at 16 rows and N = 20000) and the rounds of the grid; a grid that
-// fills fewer than all CUs (a rank's shard, the head-fused forms) keeps 16.  HICGAT_TAIL_RB = 16 / 32
-// forces one form for the plain tail (A/B runs).
-constexpr int kTailRB32MinRows = 256 * 32;
-inline int tail_rb(int M, bool heads) {
-  static const int forced = [] {
-    const char *e = getenv("HICGAT_TAIL_RB");
-    return e ? atoi(e) : 0;
-  }();
-  if (heads) return 16;
-  if (forced == 16 || forced == 32) return forced;
-  return M >= kTailRB32MinRows ? 32 : 16;
-}
-
-template <bool HEADS, bool PK, int RB>
+template <bool HEADS, bool PK>
 int tail_fwd_go(const float *x, int64_t ldx, int M, const float *W1c, const float *b1c, const float *g1,
                 const float *be1, const float *W2c, const float *b2c, const float *g2, const float *be2, const float *W3,
                 const float *b3, const float *g3, const float *be3, const float *W4, const float *b4, float eps,
@@ -747,7 +725,7 @@ int tail_fwd_go(const float *x, int64_t ldx, int M, const float *W1c, const floa
   // one per CU, each weight fetch serving twice the rows) measured slower at N = 20000 (the one-kernel
   // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
   // with one workgroup per CU every phase's latency is exposed.
-  constexpr int NW = kTailWaves;
+  constexpr int RB = 16, NW = kTailWaves;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS, PK>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
@@ -779,18 +757,15 @@ int tail_fwd_launch(const float *x, int64_t ldx, int M, const float *W1c, const 
   if (((uintptr_t)x | (uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)W3 | (uintptr_t)hh.Wh | (uintptr_t)hh.Y0 |
        (uintptr_t)hh.O | (uintptr_t)pack) & 15)
     return HICGAT_EUNSUPPORTED;
-  constexpr int RB32 = HEADS ? 16 : 32;   // the head-fused forms stay at 16 rows (tail_rb)
-  const bool rb32 = tail_rb(M, HEADS) == 32;
   if (pack) {
     if (HEADS && !pack_has_heads(pack)) return HICGAT_EINVAL;   // packed without Wh
     const float *pk = static_cast<const float *>(pack);
-    auto go = rb32 ? tail_fwd_go<HEADS, true, RB32> : tail_fwd_go<HEADS, true, 16>;
-    return go(x, ldx, M, pk + kPackF1, b1c, g1, be1, pk + kPackF2, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
-              st1, z1, Y2, st2, z2, y3, st3, z3, coords, HEADS ? pk + kPackFH : nullptr, hh, stream);
+    return tail_fwd_go<HEADS, true>(x, ldx, M, pk + kPackF1, b1c, g1, be1, pk + kPackF2, b2c, g2, be2, W3, b3, g3,
+                                    be3, W4, b4, eps, Y1, st1, z1, Y2, st2, z2, y3, st3, z3, coords,
+                                    HEADS ? pk + kPackFH : nullptr, hh, stream);
   }
-  auto go = rb32 ? tail_fwd_go<HEADS, false, RB32> : tail_fwd_go<HEADS, false, 16>;
-  return go(x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1, st1, z1, Y2, st2, z2,
-            y3, st3, z3, coords, hh.Wh, hh, stream);
+  return tail_fwd_go<HEADS, false>(x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, eps, Y1,
+                                   st1, z1, Y2, st2, z2, y3, st3, z3, coords, hh.Wh, hh, stream);
 }
 }  // namespace
 
@@ -826,12 +801,6 @@ extern "C" int hicgat_tail_fwd_fused_heads(const float *xa, int64_t ld_xa, int64
 
 extern "C" int hicgat_tail_bwd_waves(void) { return kTailWaves; }
 
-extern "C" int hicgat_tail_bwd_partial_rows(int M, int heads) {
-  if (M <= 0) return 0;
-  const int rb = tail_rb(M, heads != 0);
-  return (M + rb - 1) / rb;
-}
-
 extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
   return M <= 0 ? 16 : (size_t)((M + 15) / 16) * 2 * W * sizeof(float);   // one [2W] row per workgroup
 }
@@ -843,15 +812,15 @@ struct TailHeadsBwd {   // the HEADS operands of the backward (all null: the pla
   float *dout = nullptr, *row_stats = nullptr, *dxa = nullptr;
 };
 
-template <bool HEADS, bool PK, int RB>
+template <bool HEADS, bool PK>
 int tail_bwd_go(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
                 const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c, const float *W1c,
                 const float *g1, const float *be1, const float *g2, const float *be2, const float *g3,
                 const float *be3, float *dx, float *dY1, float *dY2, float *dy3, void *ws1, void *ws2, void *ws3,
                 const float *Wh, const TailHeadsBwd &hh, hipStream_t stream) {
-  constexpr int NW = kTailWaves;
-  // [As | Bs] row images + (RB = 16) the [NW][2 x 256] LayerNorm partial scratch (RB = 32: inside As)
-  constexpr int kBwdLds = (2 * RB * XS + (2 * NW <= RB ? 0 : NW * 2 * 256)) * (int)sizeof(float);
+  constexpr int RB = 16, NW = kTailWaves;
+  // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
+  constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS, PK>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kBwdLds) == hipSuccess;
@@ -887,18 +856,15 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
   if (ws1_bytes < hicgat_tail_bwd_workspace_bytes(M, 256) || ws2_bytes < hicgat_tail_bwd_workspace_bytes(M, 128) ||
       ws3_bytes < hicgat_tail_bwd_workspace_bytes(M, 64))
     return HICGAT_EINVAL;
-  constexpr int RB32 = HEADS ? 16 : 32;
-  const bool rb32 = tail_rb(M, HEADS) == 32;
   if (pack) {
     if (HEADS && !pack_has_heads(pack)) return HICGAT_EINVAL;   // packed without Wh
     const float *pk = static_cast<const float *>(pack);
-    auto go = rb32 ? tail_bwd_go<HEADS, true, RB32> : tail_bwd_go<HEADS, true, 16>;
-    return go(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1, g1, be1, g2, be2, g3, be3, dx,
-              dY1, dY2, dy3, ws1, ws2, ws3, HEADS ? pk + kPackBH : nullptr, hh, stream);
+    return tail_bwd_go<HEADS, true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1, g1, be1,
+                                    g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1, ws2, ws3,
+                                    HEADS ? pk + kPackBH : nullptr, hh, stream);
   }
-  auto go = rb32 ? tail_bwd_go<HEADS, false, RB32> : tail_bwd_go<HEADS, false, 16>;
-  return go(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1,
-            ws2, ws3, hh.Wh, hh, stream);
+  return tail_bwd_go<HEADS, false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
+                                   dx, dY1, dY2, dy3, ws1, ws2, ws3, hh.Wh, hh, stream);
 }
 }  // namespace
 

@@ -134,7 +134,6 @@ SIGNATURES = {
     "hicgat_tail_fwd_fused": (c_int, [c_p, c_i64, c_int] + [c_p] * 14 + [c_f] + [c_p] * 10 + [c_p, c_p]),
     "hicgat_tail_bwd_waves": (c_int, []),
     "hicgat_tail_bwd_workspace_bytes": (c_sz, [c_int, c_int]),
-    "hicgat_tail_bwd_partial_rows": (c_int, [c_int, c_int]),
     "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p, c_p]),
     "hicgat_tail_fwd_fused_heads": (c_int, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_int] + [c_p] * 14 + [c_f]
                                     + [c_p] * 10 + [c_p, c_p]),

@@ -596,10 +596,9 @@ class HipKernels:
         """Waves per workgroup of the fused tail kernels (hicgat_tail_bwd_waves)."""
         return int(self.lib.hicgat_tail_bwd_waves())
 
-    def tail_partial_rows(self, M, heads=False):
-        """Rows of LayerNorm partials hicgat_tail_bwd_fused(_heads) leaves per workspace: one per
-        workgroup (hicgat_tail_bwd_partial_rows: 16 or 32 rows per workgroup by M)."""
-        return int(self.lib.hicgat_tail_bwd_partial_rows(int(M), int(bool(heads))))
+    def tail_partial_rows(self, M):
+        """Rows of LayerNorm partials hicgat_tail_bwd_fused leaves per workspace: one per workgroup."""
+        return -(-M // 16)
 
     def ln_workspace(self, W, device):
         return _lib.workspace(self.lib.hicgat_ln_relu_res_workspace_bytes(W), device)

@@ -729,7 +729,7 @@ class _FusedTailFn(torch.autograd.Function):
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
                 g2.contiguous(), be2.contiguous(), heads=ctx.heads, pack=ctx.pack)
-            rows = K.tail_partial_rows(dc.shape[0], heads=ctx.heads is not None)   # one per workgroup
+            rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per workgroup
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)
             dW2, db2 = _wb_grad_to(K, W2, b2, dy3, z2)

@@ -506,10 +506,6 @@ int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *
  * hicgat_tail_bwd_waves(): the waves per workgroup of both tail kernels. */
 int hicgat_tail_bwd_waves(void);
 size_t hicgat_tail_bwd_workspace_bytes(int M, int W);
-/* The rows of LayerNorm partials the backward of M rows leaves in each workspace (one per
- * workgroup: M / 16 or, for the plain tail on M >= 8192 rows, M / 32 rounded up; heads != 0: the
- * head-fused form) -- the rows hicgat_ln_relu_res_bwd_params / a column sum must add. */
-int hicgat_tail_bwd_partial_rows(int M, int heads);
 int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
                           const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
                           const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
