@@ -87,8 +87,12 @@ XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "256"))
 # the edge pass; False: the same launches in the same order on the step's own stream (the serial
 # order tests/test_gpu_xagg.py compares the overlapped step against)
 XAGG_SIDE_BRANCH = True
-# row segments of the xagg step's g sums (the g all-reduce then moves S x 8 KB)
+# row segments of the xagg step's g sums (the g all-reduce then moves S x 8 KB) for shards of at least
+# XAGG_G_SEG_MIN_ROWS rows: P = 4 0.733 -> 0.719 ms, P = 2 1.216 -> 1.211 (the g sums 51 -> 41 us);
+# at P = 8 (2 700 rows) the 16 -> 10 us of the sums went to the finish's segment adds (4.9 -> 8.0 us)
+# and the g all-reduce still waited for the flat-gradient one: one sum there (profiles/r06d, r06e)
 XAGG_G_SEGS = int(os.environ.get("HICGAT_XAGG_G_SEGS", "8"))
+XAGG_G_SEG_MIN_ROWS = 4096
 
 
 def _null():
@@ -452,7 +456,7 @@ class ShardedTrainer:
             self.a_dst = torch.zeros((N, self.H), **f32)
             # [g_src | g_dst] (the edge pass's partial sums) in S row segments, one buffer: the step's
             # second all-reduce; the finish adds the segments (XAGG_G_SEGS)
-            S = max(1, min(XAGG_G_SEGS, Rl)) if self.cuda else 1
+            S = max(1, min(XAGG_G_SEGS, Rl)) if (self.cuda and Rl >= XAGG_G_SEG_MIN_ROWS) else 1
             self.gsd = torch.zeros(S, 2, 2 * F, **f32)
             self.g_src, self.g_dst = self.gsd[:, 0], self.gsd[:, 1]
             rows = 0                                                       # no [N, D] node buffers
