@@ -466,7 +466,14 @@ __device__ __forceinline__ void ln_bwd_rows(const float *__restrict__ Dz, int ld
 // with delta^h = <dout^h, Y0^h - b^h> into row_stats[8r + 4 + h] (S3 moved to [6:8], as
 // xagg_rows_bwd does), then dxa^h = dout^h W_h ([RB x 256] [256 x 512], waves 0-3 head 0, 4-7 head 1)
 // into dxa [M][1024].
-template <int RB, int NW, bool HEADS = false, bool PK = false>
+// ROWS (the single-GPU h-first GATConv, gat_fwd.hip's training form): the GATConv's gather-free
+// rows backward (hicgat_gat_agg_bwd_rows, gat_bwd.hip) on the dx rows while they are in LDS -- dout
+// = dx [y > 0] (act) or dx into dout, delta^h = <dout^h, y^h - b^h> and da_dst^h = <dout^h, out2^h>
+// - delta^h S3^h into row_stats[8r + 4 .. 8r + 8), with the same arithmetic as agg_bwd_rows_kernel
+// (bitwise) -- instead of writing dx for a separate pass that reads it back.  Y0 = y (the GATConv's
+// relu output: the tail's input), bh = its bias, out2 = sum alpha lrelu' h; each wave's row of y /
+// out2 is loaded at the kernel's start and held to the end.
+template <int RB, int NW, bool HEADS = false, bool PK = false, bool ROWS = false>
 __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     const float *__restrict__ dc, int M, const float *__restrict__ Y1, const float2 *__restrict__ st1,
     const float *__restrict__ Y2, const float2 *__restrict__ st2, const float *__restrict__ y3,
@@ -477,7 +484,9 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
     float *__restrict__ dY2, float *__restrict__ dy3, float *__restrict__ p1, float *__restrict__ p2,
     float *__restrict__ p3, int act = 0, const float *__restrict__ Y0 = nullptr, const float *__restrict__ Wh = nullptr,
     const float *__restrict__ bh = nullptr, float *__restrict__ dout = nullptr, float *__restrict__ row_stats = nullptr,
-    float *__restrict__ dxa = nullptr) {
+    float *__restrict__ dxa = nullptr, const float *__restrict__ out2 = nullptr) {
+  static_assert(!(HEADS && ROWS), "one GATConv epilogue");
+  static_assert(!ROWS || RB == NW, "ROWS: one row per wave");
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // dz3, dz2, dz1 rows
   float *Bs = lds_tail + RB * XS;    // dy3, [dy2 | dres2], [dy1 | dres1] rows
@@ -487,6 +496,17 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
   const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16;
   const int rot = (blockIdx.x >> 3) & (NW - 1), ws = (wv + rot) & (NW - 1);   // as in tail_fwd_kernel
+  float4 ry0, ry1, rq0, rq1;   // ROWS: the wave's row of y and out2 (lane l: float4 l and 64 + l)
+  if constexpr (ROWS) {
+    const int row = m0 + wv;
+    if (row < M) {
+      const size_t o0 = (size_t)row * 128 + lane;
+      ry0 = reinterpret_cast<const float4 *>(Y0)[o0];
+      ry1 = reinterpret_cast<const float4 *>(Y0)[o0 + 64];
+      rq0 = reinterpret_cast<const float4 *>(out2)[o0];
+      rq1 = reinterpret_cast<const float4 *>(out2)[o0 + 64];
+    }
+  }
   // dense3 backward: dz3 = dc W4 ([RB x 3] [3 x 64]), fp32 fma chain over j
   for (int e = tid; e < RB * 64; e += 64 * NW) {
     const int r = e >> 6, c = e & 63;
@@ -536,7 +556,37 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
 #pragma unroll
       for (int t = 0; t < NT1; ++t) acc[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     mfma_rows_t<RB, NT1, 512, PK>(Bs, XS, W1c, 512, 16 * NT1 * ws, acc, lane);
-    put_tiles<RB, NT1>(acc, 16 * NT1 * ws, HEADS ? As : nullptr, XS, HEADS ? nullptr : dx, 512, m0, M, lane);
+    put_tiles<RB, NT1>(acc, 16 * NT1 * ws, (HEADS || ROWS) ? As : nullptr, XS, (HEADS || ROWS) ? nullptr : dx, 512,
+                       m0, M, lane);
+  }
+  if constexpr (ROWS) {
+    __syncthreads();
+    const int row = m0 + wv;
+    if (row < M) {   // wave-uniform; agg_bwd_rows_kernel's arithmetic on the LDS dx row
+      float4 d0 = *reinterpret_cast<const float4 *>(&As[wv * XS + 4 * lane]);
+      float4 d1 = *reinterpret_cast<const float4 *>(&As[wv * XS + 256 + 4 * lane]);
+      const float4 b0 = reinterpret_cast<const float4 *>(bh)[lane], b1 = reinterpret_cast<const float4 *>(bh)[64 + lane];
+      if (act) {
+        d0 = make_float4(ry0.x <= 0.f ? 0.f : d0.x, ry0.y <= 0.f ? 0.f : d0.y, ry0.z <= 0.f ? 0.f : d0.z,
+                         ry0.w <= 0.f ? 0.f : d0.w);
+        d1 = make_float4(ry1.x <= 0.f ? 0.f : d1.x, ry1.y <= 0.f ? 0.f : d1.y, ry1.z <= 0.f ? 0.f : d1.z,
+                         ry1.w <= 0.f ? 0.f : d1.w);
+      }
+      float4 *d4 = reinterpret_cast<float4 *>(dout) + (size_t)row * 128 + lane;
+      d4[0] = d0;
+      d4[64] = d1;
+      const float4 e0 = make_float4(ry0.x - b0.x, ry0.y - b0.y, ry0.z - b0.z, ry0.w - b0.w);
+      const float4 e1 = make_float4(ry1.x - b1.x, ry1.y - b1.y, ry1.z - b1.z, ry1.w - b1.w);
+      float v[4] = {f4_dot(d0, e0), f4_dot(d1, e1), f4_dot(d0, rq0), f4_dot(d1, rq1)};
+      transpose_reduce<4>(v, lane);
+      const float dl0 = readlane_f(v[0], 0), dl1 = readlane_f(v[0], 16);
+      const float q0 = readlane_f(v[0], 32), q1 = readlane_f(v[0], 48);
+      if (lane == 0) {
+        float4 *rs4 = reinterpret_cast<float4 *>(row_stats);
+        const float4 t = rs4[2 * (size_t)row + 1];   // (S3_0, S3_1, -, -) from the forward
+        rs4[2 * (size_t)row + 1] = make_float4(dl0, dl1, fmaf(-dl0, t.x, q0), fmaf(-dl1, t.y, q1));
+      }
+    }
   }
   if constexpr (HEADS) {
     static_assert(NW == 8 || NW == 16, "the dxa GEMMs take NW / 2 waves per head");
@@ -806,13 +856,13 @@ extern "C" size_t hicgat_tail_bwd_workspace_bytes(int M, int W) {
 }
 
 namespace {
-struct TailHeadsBwd {   // the HEADS operands of the backward (all null: the plain tail)
+struct TailHeadsBwd {   // the HEADS / ROWS operands of the backward (all null: the plain tail)
   int act = 0;
-  const float *Y0 = nullptr, *Wh = nullptr, *bh = nullptr;
+  const float *Y0 = nullptr, *Wh = nullptr, *bh = nullptr, *out2 = nullptr;
   float *dout = nullptr, *row_stats = nullptr, *dxa = nullptr;
 };
 
-template <bool HEADS, bool PK>
+template <bool HEADS, bool PK, bool ROWS = false>
 int tail_bwd_go(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
                 const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c, const float *W1c,
                 const float *g1, const float *be1, const float *g2, const float *be2, const float *g3,
@@ -821,21 +871,21 @@ int tail_bwd_go(const float *dcoords, int M, const float *Y1, const float *st1, 
   constexpr int RB = 16, NW = kTailWaves;
   // [As | Bs] row images + the [NW][2 x 256] LayerNorm partial scratch
   constexpr int kBwdLds = (2 * RB * XS + NW * 2 * 256) * (int)sizeof(float);
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS, PK>),
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_bwd_kernel<RB, NW, HEADS, PK, ROWS>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kBwdLds) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS, PK>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+  hipLaunchKernelGGL((tail_bwd_kernel<RB, NW, HEADS, PK, ROWS>), dim3((M + RB - 1) / RB), dim3(64 * NW),
                      (size_t)kBwdLds, stream, dcoords, M, Y1, reinterpret_cast<const float2 *>(st1),
                      Y2, reinterpret_cast<const float2 *>(st2), y3, reinterpret_cast<const float2 *>(st3), W4, W3, W2c,
                      W1c, g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, static_cast<float *>(ws1),
                      static_cast<float *>(ws2), static_cast<float *>(ws3), hh.act, hh.Y0, Wh, hh.bh, hh.dout,
-                     hh.row_stats, hh.dxa);
+                     hh.row_stats, hh.dxa, hh.out2);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
 }
 
-template <bool HEADS>
+template <bool HEADS, bool ROWS = false>
 int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2, const float *st2,
                     const float *y3, const float *st3, const float *W4, const float *W3, const float *W2c,
                     const float *W1c, const float *g1, const float *be1, const float *g2, const float *be2,
@@ -845,11 +895,13 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
   if (M < 0) return HICGAT_EINVAL;
   if (M == 0) return HICGAT_OK;
   const void *ps[] = {dcoords, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
-                      HEADS ? hh.dout : dx, dY1, dY2, dy3, ws1, ws2, ws3};
+                      (HEADS || ROWS) ? hh.dout : dx, dY1, dY2, dy3, ws1, ws2, ws3};
   for (const void *p : ps)
     if (!p) return HICGAT_EINVAL;
   if (HEADS && (!hh.Y0 || !hh.Wh || !hh.bh || !hh.row_stats || !hh.dxa)) return HICGAT_EINVAL;
-  if (HEADS && (((uintptr_t)hh.Y0 | (uintptr_t)hh.bh | (uintptr_t)hh.dout | (uintptr_t)hh.row_stats) & 15))
+  if (ROWS && (!hh.Y0 || !hh.bh || !hh.out2 || !hh.row_stats)) return HICGAT_EINVAL;
+  if ((HEADS || ROWS) &&
+      (((uintptr_t)hh.Y0 | (uintptr_t)hh.bh | (uintptr_t)hh.dout | (uintptr_t)hh.row_stats | (uintptr_t)hh.out2) & 15))
     return HICGAT_EUNSUPPORTED;
   if ((uintptr_t)pack & 15) return HICGAT_EUNSUPPORTED;
   // every workgroup owns NW partial rows of each LN workspace (one per wave)
@@ -859,12 +911,12 @@ int tail_bwd_launch(const float *dcoords, int M, const float *Y1, const float *s
   if (pack) {
     if (HEADS && !pack_has_heads(pack)) return HICGAT_EINVAL;   // packed without Wh
     const float *pk = static_cast<const float *>(pack);
-    return tail_bwd_go<HEADS, true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1, g1, be1,
-                                    g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1, ws2, ws3,
-                                    HEADS ? pk + kPackBH : nullptr, hh, stream);
+    return tail_bwd_go<HEADS, true, ROWS>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, pk + kPackB2, pk + kPackB1,
+                                          g1, be1, g2, be2, g3, be3, dx, dY1, dY2, dy3, ws1, ws2, ws3,
+                                          HEADS ? pk + kPackBH : nullptr, hh, stream);
   }
-  return tail_bwd_go<HEADS, false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
-                                   dx, dY1, dY2, dy3, ws1, ws2, ws3, hh.Wh, hh, stream);
+  return tail_bwd_go<HEADS, false, ROWS>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3,
+                                         be3, dx, dY1, dY2, dy3, ws1, ws2, ws3, hh.Wh, hh, stream);
 }
 }  // namespace
 
@@ -878,6 +930,28 @@ extern "C" int hicgat_tail_bwd_fused(const float *dcoords, int M, const float *Y
   return tail_bwd_launch<false>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3,
                                 dx, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, TailHeadsBwd{}, pack,
                                 (hipStream_t)stream);
+}
+
+extern "C" int hicgat_tail_bwd_fused_rows(const float *dcoords, int M, const float *Y1, const float *st1,
+                                          const float *Y2, const float *st2, const float *y3, const float *st3,
+                                          const float *W4, const float *W3, const float *W2c, const float *W1c,
+                                          const float *g1, const float *be1, const float *g2, const float *be2,
+                                          const float *g3, const float *be3, float *dY1, float *dY2, float *dy3,
+                                          void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
+                                          size_t ws3_bytes, int act, const float *y, const float *out2,
+                                          const float *bias, float *dout, float *row_stats, const void *pack,
+                                          hicgat_stream_t stream) {
+  if (kTailWaves != 16) return HICGAT_EUNSUPPORTED;   // one row per wave
+  TailHeadsBwd hh;
+  hh.act = act ? 1 : 0;
+  hh.Y0 = y;
+  hh.bh = bias;
+  hh.out2 = out2;
+  hh.dout = dout;
+  hh.row_stats = row_stats;
+  return tail_bwd_launch<false, true>(dcoords, M, Y1, st1, Y2, st2, y3, st3, W4, W3, W2c, W1c, g1, be1, g2, be2, g3,
+                                      be3, nullptr, dY1, dY2, dy3, ws1, ws1_bytes, ws2, ws2_bytes, ws3, ws3_bytes, hh,
+                                      pack, (hipStream_t)stream);
 }
 
 extern "C" int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const float *Y1, const float *st1,

@@ -137,6 +137,8 @@ SIGNATURES = {
     "hicgat_tail_bwd_fused": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 4 + [c_p, c_sz] * 3 + [c_p, c_p]),
     "hicgat_tail_fwd_fused_heads": (c_int, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_int] + [c_p] * 14 + [c_f]
                                     + [c_p] * 10 + [c_p, c_p]),
+    "hicgat_tail_bwd_fused_rows": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 3 + [c_p, c_sz] * 3
+                                   + [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_tail_bwd_fused_heads": (c_int, [c_p, c_int] + [c_p] * 16 + [c_p] * 3 + [c_p, c_sz] * 3
                                     + [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "hicgat_sage_weights": (c_int, [c_p, c_int, c_i64, c_p, c_p, c_p, c_p, c_p]),

@@ -562,22 +562,35 @@ class HipKernels:
                     *tail), "hicgat_tail_fwd_fused_heads")
         return coords, (Y1, st1, z1, Y2, st2, z2, y3, st3, z3)
 
-    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=None, pack=None):
+    def tail_bwd_fused(self, dcoords, saved, W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3, heads=None, pack=None,
+                       rows=None):
         """The tail's input-gradient chain in one launch (tail_fused.hip): returns (dx, dY1, dY2, dy3,
         (ws1, ws2, ws3)) -- the LayerNorm dgamma/dbeta partials stay in the workspaces
         (``ln_relu_res_bwd_params``).  ``heads``: the head-fused form (dx None; the xagg GATConv's
-        dout, delta and dxa written into the ``ops.TailHeads`` buffers instead)."""
+        dout, delta and dxa written into the ``ops.TailHeads`` buffers instead).  ``rows`` = (act, y,
+        out2, bias, row_stats, dout): the single-GPU GATConv's rows pass in the epilogue
+        (hicgat_tail_bwd_fused_rows; dx None, dout and row_stats[:, 4:8] written instead)."""
         Y1, st1, z1, Y2, st2, z2, y3, st3, z3 = saved
         M = dcoords.shape[0]
         dev = dcoords.device
         f = dict(dtype=torch.float32, device=dev)
-        dx, dY1, dY2, dy3 = (torch.empty((M, w), **f) for w in (512, 512, 256, 64))
+        dY1, dY2, dy3 = (torch.empty((M, w), **f) for w in (512, 256, 64))
+        dx = torch.empty((M, 512), **f) if heads is None and rows is None else None
         ws = [_lib.workspace(self.lib.hicgat_tail_bwd_workspace_bytes(M, w), dev) for w in (256, 128, 64)]
         ts = [W4, W3, W2c, W1c, g1, be1, g2, be2, g3, be3]
         assert all(t.is_contiguous() for t in ts) and dcoords.is_contiguous()
         wsa = [P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), P(ws[2]), ws[2].numel()]
         with _timed("tail_bwd_fused"):
-            if heads is None:
+            if rows is not None:
+                act, y, out2, bias, rs, dout = rows
+                for t, w in ((y, 512), (out2, 512), (dout, 512), (rs, 8)):
+                    assert t.shape == (M, w) and t.is_contiguous()
+                assert bias.is_contiguous() and bias.numel() == 512
+                _lib.check(self.lib.hicgat_tail_bwd_fused_rows(
+                    P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dY1), P(dY2),
+                    P(dy3), *wsa, int(act), P(y), P(out2), P(bias), P(dout), P(rs), P(pack), _lib.stream(dev)),
+                    "hicgat_tail_bwd_fused_rows")
+            elif heads is None:
                 _lib.check(self.lib.hicgat_tail_bwd_fused(
                     P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dx), P(dY1),
                     P(dY2), P(dy3), *wsa, P(pack), _lib.stream(dev)), "hicgat_tail_bwd_fused")
@@ -585,7 +598,6 @@ class HipKernels:
                 h = heads
                 assert h.dout.shape == (M, 512) and h.dout.is_contiguous() and h.dxa.shape == (M, 1024)
                 assert h.dxa.is_contiguous() and h.rs.shape == (M, 8) and h.rs.is_contiguous()
-                dx = None
                 _lib.check(self.lib.hicgat_tail_bwd_fused_heads(
                     P(dcoords), M, P(Y1), P(st1), P(Y2), P(st2), P(y3), P(st3), *[P(t) for t in ts], P(dY1), P(dY2),
                     P(dy3), *wsa, int(h.act), P(h.Y0), P(h.W), P(h.bias), P(h.dout), P(h.rs), P(h.dxa), P(pack),

@@ -251,6 +251,10 @@ def _dev_check(*ts):
 
 
 _ACTS = {None: 0, "relu": 1}
+# the single-GPU GATConv's gather-free rows pass (hicgat_gat_agg_bwd_rows) in the one-kernel tail
+# backward's epilogue when that tail consumes the layer's output (hicgat_tail_bwd_fused_rows); 0: the
+# separate pass
+FUSE_ROWS = os.environ.get("HICGAT_FUSE_ROWS", "1") != "0"
 
 
 class _GATConvFn(torch.autograd.Function):
@@ -281,8 +285,15 @@ class _GATConvFn(torch.autograd.Function):
         else:
             K.agg_fwd_act(rowptr, col, 0, N, h, a_src, a_dst, b, negative_slope, act, out, out2, row_stats)
         ctx.tiles = tiles
+        ctx.rows_state = None
         if train:
             ctx.save_for_backward(x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col, out, out2, b)
+            if FUSE_ROWS:
+                # the one-kernel tail that consumes ``out`` may run this layer's rows pass in its
+                # backward's epilogue (_FusedTailFn; hicgat_tail_bwd_fused_rows): it finds these
+                # operands on ``out`` and records the dout it wrote in the shared state
+                ctx.rows_state = {"dout": None}
+                out._hicgat_rows = (act, out2, row_stats, b, ctx.rows_state)
         ctx.has_bias = bias is not None
         ctx.ns = float(negative_slope)
         ctx.act = act
@@ -293,13 +304,22 @@ class _GATConvFn(torch.autograd.Function):
     def backward(ctx, dout):
         K = kernels.default()
         x, W, al, ar, h, a_src, a_dst, row_stats, rowptr, col, out, out2, b = ctx.saved_tensors
-        dout = dout.contiguous()
         N = x.shape[0]
         H = al.shape[-2]
-        if ctx.act:
-            g, dout = dout, torch.empty_like(dout)
+        fused = ctx.rows_state is not None and ctx.rows_state["dout"] is not None
+        if fused:
+            # the tail's backward ran this layer's rows pass: dout (relu'd) and row_stats[:, 4:8] are
+            # written, and the gradient that reached us must be exactly the dout it returned (a second
+            # consumer of ``out`` would have added into it: then the rows pass saw only a part)
+            if dout.data_ptr() != ctx.rows_state["dout"].data_ptr():
+                raise RuntimeError("the GATConv output fed more than the fused tail: its rows pass was fused "
+                                   "into the tail's backward (set HICGAT_FUSE_ROWS=0 for such a model)")
+            ctx.rows_state["dout"] = None
+        elif ctx.act:
+            g, dout = dout.contiguous(), torch.empty_like(dout)
             K.agg_bwd_rows(0, N, ctx.act, g, out, b, out2, dout, row_stats)
         else:
+            dout = dout.contiguous()
             K.agg_bwd_rows(0, N, 0, dout, out, b, out2, None, row_stats)
         fork = side_mark()   # the tail's queued dW / db launches run beside the source pass below
         dh = torch.empty_like(h)
@@ -704,6 +724,9 @@ class _FusedTailFn(torch.autograd.Function):
                                          heads=heads, pack=pack)
         ctx.heads = heads
         ctx.pack = pack
+        link = getattr(x, "_hicgat_rows", None) if heads is None else None
+        # the GATConv's rows pass in this backward's epilogue: its relu output is exactly our input rows
+        ctx.rows = link if (link is not None and FUSE_ROWS and K.tail_waves() == 16 and x.shape[1] == 512) else None
         if coords_out is not None:
             # the kernel wrote into the caller's buffer (e.g. the all-gather rows); the output is a
             # fresh tensor object over the same memory, so autograd sees a new output (no view or
@@ -725,10 +748,18 @@ class _FusedTailFn(torch.autograd.Function):
             # block 1)
             K = kernels.default()
             dc = dcoords.contiguous()
+            rows = None
+            if ctx.rows is not None and ctx.needs_input_grad[0]:
+                act, out2, rs, b, state = ctx.rows
+                dout = torch.empty((dc.shape[0], 512), dtype=torch.float32, device=dc.device)
+                rows = (act, x, out2, b, rs, dout)
             dx, dY1, dY2, dy3, (ws1, ws2, ws3) = K.tail_bwd_fused(
                 dc, ctx.saved_tensors[1:], W3.contiguous(), W2.contiguous(), _joined(W1, W1al).contiguous(),
                 _joined(Wa, Wal).contiguous(), ga.contiguous(), bea.contiguous(), g1.contiguous(), be1.contiguous(),
-                g2.contiguous(), be2.contiguous(), heads=ctx.heads, pack=ctx.pack)
+                g2.contiguous(), be2.contiguous(), heads=ctx.heads, pack=ctx.pack, rows=rows)
+            if rows is not None:
+                dx = dout               # the GATConv's backward finds it in the shared state and skips its rows pass
+                state["dout"] = dout
             rows = K.tail_partial_rows(dc.shape[0])   # the kernel's partial rows: one per workgroup
             dW3, db3 = _wb_grad_to(K, W3, b3, dc, z3)
             dg2, dbe2 = _ln_param_grads(K, g2, be2, ws3, rows)

@@ -536,6 +536,19 @@ int hicgat_tail_bwd_fused_heads(const float *dcoords, int M, const float *Y1, co
                                 float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
                                 size_t ws3_bytes, int act, const float *Y0, const float *Wh, const float *bh,
                                 float *dout, float *row_stats, float *dxa, const void *pack, hicgat_stream_t stream);
+/* The plain tail's backward with the single-GPU GATConv's gather-free rows pass in its epilogue
+ * (hicgat_gat_agg_bwd_rows on the dx rows while they are in LDS, same arithmetic, bitwise): no dx is
+ * written; dout [M][512] = dx [y > 0] (act != 0) or dx, and row_stats[8i + 4 .. 8i + 8) = (delta,
+ * da_dst) from the forward's S3 there, for y = the GATConv's relu output (the tail's input rows),
+ * out2 and bias of hicgat_gat_agg_fwd_act.  One row per wave: HICGAT_EUNSUPPORTED unless the kernels
+ * run 16 waves (hicgat_tail_bwd_waves). */
+int hicgat_tail_bwd_fused_rows(const float *dcoords, int M, const float *Y1, const float *st1, const float *Y2,
+                               const float *st2, const float *y3, const float *st3, const float *W4, const float *W3,
+                               const float *W2c, const float *W1c, const float *g1, const float *be1, const float *g2,
+                               const float *be2, const float *g3, const float *be3, float *dY1, float *dY2,
+                               float *dy3, void *ws1, size_t ws1_bytes, void *ws2, size_t ws2_bytes, void *ws3,
+                               size_t ws3_bytes, int act, const float *y, const float *out2, const float *bias,
+                               float *dout, float *row_stats, const void *pack, hicgat_stream_t stream);
 
 /* ---- f1: SAGEConv of the baseline model Net (layers.py:41-79, models.py:14-55) ----------------
  * hicgat_sage_weights: the float32 edge weight w of every entry of the (set_diag'd) device CSR --

@@ -1593,3 +1593,40 @@ def test_fused_tail_matches_per_layer_path(monkeypatch, m, sinks, bwd):
             continue      # exactly 0 up to rounding when the upstream gradient sums to ~0
         assert (b - a).abs().max().item() <= 1e-4 * a.abs().max().item(), nm
     assert _rel(c1.double().cpu(), ref.cpu()) < 1e-5      # the fp64 forward of models.py:638-659
+
+
+@pytest.mark.parametrize("n,graphed", [(3000, False), (3000, True), (20000, False)])
+def test_rows_pass_fused_into_tail_backward_is_bitwise(monkeypatch, n, graphed):
+    """The single-GPU GATConv's rows pass (dout = g relu'(y), delta, da_dst; hicgat_gat_agg_bwd_rows)
+    run in the one-kernel tail backward's epilogue (hicgat_tail_bwd_fused_rows, ops.FUSE_ROWS) against
+    the separate pass: two training steps (eager, or captured and replayed) give the same loss,
+    gradients and parameters bit for bit (same arithmetic on the same dx values)."""
+    import hicgat
+    from hicgat import ops, synth
+    i, j, c = synth.contact_pairs(n, density=0.05 if n < 20000 else 0.01, seed=3)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    x = torch.tensor(synth.features(n, seed=3), device=DEV)
+    res = {}
+    for fuse in (False, True):
+        monkeypatch.setattr(ops, "FUSE_ROWS", fuse)
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+        assert ops.fused_tail_ok(model, torch.empty(n, 512, device=DEV))
+        opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+        out = []
+        if graphed:
+            step = hicgat.graphs.captured_train_step(model, opt, x, adj, tr, warmup=1)
+            for _ in range(2):
+                loss = float(step()[0])
+                out.append((loss, opt.grad.clone(), opt.flat.clone()))
+        else:
+            for _ in range(2):
+                loss, _, _ = hicgat.train.train_step(model, opt, x, adj, tr)
+                out.append((float(loss), opt.grad.clone(), opt.flat.clone()))
+        torch.cuda.synchronize()
+        res[fuse] = out
+    for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
+        assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
