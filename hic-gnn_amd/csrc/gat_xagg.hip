@@ -28,6 +28,7 @@
 //                       and g_src^h = sum_j da_src_j^h x_j in the same pass (+ xagg_colred)
 //   xagg_param_finish   dW += att (x) g terms, datt_src / datt_dst = W_h g
 #include "common.hpp"
+#include "pack.hpp"
 
 constexpr int kXaggU = 4;    // neighbours gathered per inner step (4 x 2 float4 in flight per lane)
 constexpr int kXaggGL = 8;   // edge pass (slab form): lanes per edge (16 float4 of x_j per lane in flight)
@@ -40,7 +41,7 @@ namespace hicgat {
 __global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__ W, const float *__restrict__ att_s,
                                                        const float *__restrict__ att_d, float *__restrict__ v,
                                                        float *__restrict__ zero_buf, int64_t zero_n,
-                                                       int64_t *__restrict__ step_ctr) {
+                                                       int64_t *__restrict__ step_ctr, const PackJobs pj) {
   __shared__ float red[4][64];
   // the optimizer's device step count advances here, at the step's first launch (Adam reads it at
   // the step's end: hicgat_adam_step_table_ex with counted = 1, no increment launch of its own)
@@ -50,6 +51,12 @@ __global__ __launch_bounds__(256) void xagg_vec_kernel(const float *__restrict__
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) reinterpret_cast<float4 *>(zero_buf)[i] = z;
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < zero_n; i += stride) zero_buf[i] = 0.f;
+  }
+  // blocks 32.. (hicgat_xagg_logits_zero_pack): the one-kernel tail's packed weights of this step
+  // (pack.hpp; hicgat_tail_pack's launch folded into the step's first one)
+  if (blockIdx.x >= 32) {
+    pack_block(pj, blockIdx.x - 32);
+    return;
   }
   const int which = blockIdx.x >> 3;                 // 0, 1: att_src heads 0, 1; 2, 3: att_dst heads 0, 1
   const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
@@ -674,23 +681,39 @@ using namespace hicgat;
 
 extern "C" size_t hicgat_xagg_vec_bytes(void) { return 4 * 512 * sizeof(float); }
 
-extern "C" int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst,
-                                       int N, int F, int H, int C, float *vec, float *a_src, float *a_dst,
-                                       float *zero_buf, int64_t zero_n, int64_t *step_counter,
-                                       hicgat_stream_t stream) {
+extern "C" int hicgat_xagg_logits_zero_pack(const float *x, const float *W, const float *att_src,
+                                            const float *att_dst, int N, int F, int H, int C, float *vec,
+                                            float *a_src, float *a_dst, float *zero_buf, int64_t zero_n,
+                                            int64_t *step_counter, const float *W1c, const float *W2c, void *pack,
+                                            size_t pack_bytes, hicgat_stream_t stream) {
   if (N < 0 || zero_n < 0) return HICGAT_EINVAL;
   if (F != 512 || H != 2 || C != 256) return HICGAT_EUNSUPPORTED;
   if (!W || !att_src || !att_dst || !vec || (zero_n > 0 && !zero_buf)) return HICGAT_EINVAL;
   if (zero_buf && (reinterpret_cast<uintptr_t>(zero_buf) & 15)) return HICGAT_EINVAL;
+  PackJobs pj{};
+  int nb = 0;
+  if (pack) {   // the heads form's pack: Wh is lin_l's weight W itself
+    nb = pack_jobs(W1c, W2c, W, pack, pack_bytes, pj);
+    if (nb < 0) return nb;
+  }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(xagg_vec_kernel, dim3(32), dim3(256), 0, s, W, att_src, att_dst, vec, zero_n > 0 ? zero_buf : nullptr,
-                     zero_n, step_counter);
+  hipLaunchKernelGGL(xagg_vec_kernel, dim3(32 + nb), dim3(256), 0, s, W, att_src, att_dst, vec,
+                     zero_n > 0 ? zero_buf : nullptr, zero_n, step_counter, pj);
   HICGAT_CHECK_LAUNCH();
+  if (pack) pack_note(pack, true);
   if (N == 0) return HICGAT_OK;
   if (!x || !a_src || !a_dst) return HICGAT_EINVAL;
   hipLaunchKernelGGL(xagg_logits_kernel, dim3((N + 3) / 4), dim3(256), 0, s, x, vec, N, a_src, a_dst);
   HICGAT_CHECK_LAUNCH();
   return HICGAT_OK;
+}
+
+extern "C" int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst,
+                                       int N, int F, int H, int C, float *vec, float *a_src, float *a_dst,
+                                       float *zero_buf, int64_t zero_n, int64_t *step_counter,
+                                       hicgat_stream_t stream) {
+  return hicgat_xagg_logits_zero_pack(x, W, att_src, att_dst, N, F, H, C, vec, a_src, a_dst, zero_buf, zero_n,
+                                      step_counter, nullptr, nullptr, nullptr, 0, stream);
 }
 
 extern "C" int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, const float *att_dst, int N,

@@ -21,7 +21,9 @@
 // LayerNorm: one wave per row, the arithmetic of ln_relu_res_fwd_kernel (layernorm.hip) on the row
 // held in LDS (torch.nn.LayerNorm: biased variance, eps 1e-5 inside the square root).
 #include "common.hpp"
+#include "pack.hpp"
 
+#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -639,67 +641,22 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_bwd_kernel(
   }
 }
 
-// ---- packed weight copies (hicgat_tail_pack) ------------------------------------------------------
-// Float offsets in the pack buffer: the forward (mfma_rows) layouts of W1c [512][512], W2c [256][256]
-// and Wh [512][512], then their backward (mfma_rows_t) layouts.
-constexpr int64_t kPackF1 = 0, kPackF2 = kPackF1 + 512 * 512, kPackFH = kPackF2 + 256 * 256,
-                  kPackB1 = kPackFH + 512 * 512, kPackB2 = kPackB1 + 512 * 512, kPackBH = kPackB2 + 256 * 256,
-                  kPackTotal = kPackBH + 512 * 512;
-struct PackJob {
-  const float *src;   // [R][C] row-major
-  float *dst;
-  int R, C, bwd, blk0;
-};
-struct PackJobs {
-  PackJob j[6];
-  int n;
-};
-// One wave per unit: the forward layout's unit is a 16-row x 32-column block of W (the two 1 KB
-// chunks e = 0, 1 of super-group g), the backward layout's a 16 x 16 block (one 1 KB chunk).  The
-// wave reads the block as whole 128-B / 64-B row pieces (contiguous quads of lanes), turns it
-// through LDS and writes its chunks as 1 KB contiguous -- a lane-per-row read or write runs the
-// vector memory path at a quarter of the rate (tools/ld_pattern_bench.hip).
-// the wave's LDS writes visible to its other lanes' reads
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__global__ __launch_bounds__(256) void tail_pack_kernel(const PackJobs jobs) {
-  __shared__ float tile[4][16][36];
-  int q = 0;
-#pragma unroll
-  for (int k = 1; k < 6; ++k) q += (k < jobs.n && (int)blockIdx.x >= jobs.j[k].blk0) ? 1 : 0;
-  const PackJob &J = jobs.j[q];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int u = (blockIdx.x - J.blk0) * 4 + wv;                       // this wave's unit
-  float (*T)[36] = tile[wv];
-  float4 *out = reinterpret_cast<float4 *>(J.dst);
-  if (!J.bwd) {   // P[((b * G + g) * 2 + e) * 256 + 4L + c] = W[16b + (L & 15)][32g + 8(L >> 4) + 4e + c]
-    const int G = J.C / 32;
-    if (u >= (J.R / 16) * G) return;                                   // wave-uniform
-    const int b = u / G, g = u % G;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int t = lane + 64 * h, r = t >> 3, c4 = t & 7;
-      *reinterpret_cast<float4 *>(&T[r][4 * c4]) =
-          *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * b + r) * J.C + 32 * g + 4 * c4);
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-      out[((size_t)u * 2 + e) * 64 + lane] = *reinterpret_cast<const float4 *>(&T[lane & 15][8 * (lane >> 4) + 4 * e]);
-  } else {        // P[((g * (C / 16) + c) * 64 + L) * 4 + s] = W[16g + 4(L >> 4) + s][16c + (L & 15)]
-    const int CB = J.C / 16;
-    if (u >= (J.R / 16) * CB) return;
-    const int g = u / CB, cb = u % CB;
-    const int r = lane >> 2, c4 = lane & 3;
-    *reinterpret_cast<float4 *>(&T[r][4 * c4]) =
-        *reinterpret_cast<const float4 *>(J.src + (size_t)(16 * g + r) * J.C + 16 * cb + 4 * c4);
-    wave_lds_sync();
-    const int r0 = 4 * (lane >> 4), cc = lane & 15;
-    out[(size_t)u * 64 + lane] = make_float4(T[r0][cc], T[r0 + 1][cc], T[r0 + 2][cc], T[r0 + 3][cc]);
+__global__ __launch_bounds__(256) void tail_pack_kernel(const PackJobs jobs) { pack_block(jobs, (int)blockIdx.x); }
+
+// The step's first launch with the pack riding along: blocks [0, zb) are hicgat_step_begin's (zero the
+// flat gradient, advance the device step count), the rest pack the tail's weights -- one launch
+// fewer on the step's chain (the weights change only at the previous step's Adam).
+__global__ __launch_bounds__(256) void step_pack_kernel(const PackJobs jobs, float *__restrict__ grad, int64_t n,
+                                                        int64_t *__restrict__ step_ctr, int zb) {
+  if ((int)blockIdx.x >= zb) {   // block-uniform
+    pack_block(jobs, (int)blockIdx.x - zb);
+    return;
   }
+  if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] = step_ctr[0] + 1;
+  const int64_t n4 = n / 4, stride = (int64_t)zb * 256;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) reinterpret_cast<float4 *>(grad)[i] = z;
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) grad[i] = 0.f;
 }
 
 }  // namespace hicgat
@@ -714,6 +671,8 @@ extern "C" size_t hicgat_tail_pack_bytes(void) { return (size_t)kPackTotal * siz
 namespace {
 std::mutex g_pack_mu;
 std::unordered_map<const void *, bool> g_pack_heads;
+}  // namespace
+namespace hicgat {
 void pack_note(const void *pack, bool heads) {
   std::lock_guard<std::mutex> lk(g_pack_mu);
   g_pack_heads[pack] = heads;
@@ -723,15 +682,13 @@ bool pack_has_heads(const void *pack) {
   auto it = g_pack_heads.find(pack);
   return it != g_pack_heads.end() && it->second;
 }
-}  // namespace
 
-extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
-                                hicgat_stream_t stream) {
+// the pack's job table (block ranges per weight and layout); returns the block count, or < 0 on error
+int pack_jobs(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes, PackJobs &pj) {
   if (!W1c || !W2c || !pack) return HICGAT_EINVAL;
   if (pack_bytes < hicgat_tail_pack_bytes()) return HICGAT_EINVAL;
   if (((uintptr_t)W1c | (uintptr_t)W2c | (uintptr_t)Wh | (uintptr_t)pack) & 15) return HICGAT_EUNSUPPORTED;
   float *pk = static_cast<float *>(pack);
-  PackJobs pj;
   pj.n = 0;
   int blk = 0;
   auto add = [&](const float *src, int64_t off, int R, int C, int bwd) {
@@ -751,7 +708,32 @@ extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float 
   add(W1c, kPackB1, 512, 512, 1);
   add(W2c, kPackB2, 256, 256, 1);
   if (Wh) add(Wh, kPackBH, 512, 512, 1);
+  return blk;
+}
+}  // namespace hicgat
+
+extern "C" int hicgat_tail_pack(const float *W1c, const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
+                                hicgat_stream_t stream) {
+  PackJobs pj;
+  const int blk = pack_jobs(W1c, W2c, Wh, pack, pack_bytes, pj);
+  if (blk < 0) return blk;
   hipLaunchKernelGGL(tail_pack_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, pj);
+  HICGAT_CHECK_LAUNCH();
+  pack_note(pack, Wh != nullptr);
+  return HICGAT_OK;
+}
+
+extern "C" int hicgat_step_begin_pack(float *grad, int64_t n, int64_t *step_counter, const float *W1c,
+                                     const float *W2c, const float *Wh, void *pack, size_t pack_bytes,
+                                     hicgat_stream_t stream) {
+  if (n < 0 || (n > 0 && !grad)) return HICGAT_EINVAL;
+  if (grad && (reinterpret_cast<uintptr_t>(grad) & 15)) return HICGAT_EINVAL;
+  PackJobs pj;
+  const int blk = pack_jobs(W1c, W2c, Wh, pack, pack_bytes, pj);
+  if (blk < 0) return blk;
+  const int zb = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, 1024));   // as hicgat_step_begin
+  hipLaunchKernelGGL(step_pack_kernel, dim3(zb + blk), dim3(256), 0, (hipStream_t)stream, pj, grad, n, step_counter,
+                     zb);
   HICGAT_CHECK_LAUNCH();
   pack_note(pack, Wh != nullptr);
   return HICGAT_OK;

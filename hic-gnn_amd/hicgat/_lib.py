@@ -91,6 +91,8 @@ SIGNATURES = {
     "hicgat_xagg_logits": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p]),
     "hicgat_xagg_logits_zero": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_i64,
                                         c_p, c_p]),
+    "hicgat_xagg_logits_zero_pack": (c_int, [c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_p,
+                                             c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_xagg_fwd": (c_int, [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p, c_f, c_p, c_p,
                                 c_p]),
     "hicgat_xagg_bias_relu": (c_int, [c_p, c_p, c_p, c_int, c_int, c_p]),
@@ -153,6 +155,7 @@ SIGNATURES = {
     "hicgat_adam_step_table": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_p]),
     "hicgat_adam_step_table_ex": (c_int, [c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_p, c_i64, c_p, c_int, c_p]),
     "hicgat_step_begin": (c_int, [c_p, c_i64, c_p, c_p]),
+    "hicgat_step_begin_pack": (c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "hicgat_sim_collective": (c_int, [c_f, c_int, c_int, c_p]),
     "hicgat_stream_create": (c_int, [c_int, ctypes.POINTER(c_p)]),
     "hicgat_wall_stamp": (c_int, [c_p, c_int, c_p]),

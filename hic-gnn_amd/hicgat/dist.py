@@ -677,17 +677,21 @@ class ShardedTrainer:
         W, al, ar = self.W.detach(), self.att_l.detach(), self.att_r.detach()
         bias = self.bias.detach()
         # ---- forward ------------------------------------------------------------------------
+        use_heads = self.act and self.cuda and ops.tail_heads_ok(self.model, self.O)
+        # the head-fused tail's packed weights (W1c, W2c and lin_l's W) ride in the same first launch
+        pk = ops.step_pack(self.model, self.O) if use_heads else None
         K.xagg_logits(self.x, W, al, ar, self.a_src, self.a_dst, zero=self.opt.grad if self.cuda else None,
-                      step_ctr=self._ctr())
+                      step_ctr=self._ctr(), **({"pack": pk} if pk is not None else {}))
         K.xagg_fwd(self.rowptr, self.col, r0, r1, self.x, self.a_src, self.a_dst, self.ns, self.X4, self.rs)
         Y0 = self.Y0
         rs_own = self.rs[r0:r1]
         hc = [slice(hd * C, (hd + 1) * C) for hd in (0, 1)]
-        if self.act and self.cuda and ops.tail_heads_ok(self.model, self.O):
+        if use_heads:
             # the head GEMMs (+ bias, relu) at the head of the one-kernel tail forward, and the rows
             # backward + dxa GEMMs at the end of its backward: four launches fewer per step
             heads = ops.TailHeads(self.X4, W.contiguous(), bias, Y0, self.dout_l, rs_own, self.dxa, act=self.act)
-            o, coords_loc, coords = self._tail(self.O, heads=heads)
+            with ops.prepacked(self.model, pk):
+                o, coords_loc, coords = self._tail(self.O, heads=heads)
         else:
             heads = None
             # out (head hd columns) = xa^hd W_hd^T + b^hd (and relu(out) for the tail): both heads in one

@@ -210,18 +210,27 @@ class HipKernels:
         return datt_l, datt_r, dbias
 
     # -- aggregate-first GATConv (gat_xagg.hip): the multi-GPU "xagg" step (hicgat.dist) ---------------
-    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None, step_ctr=None):
+    def xagg_logits(self, x, W, att_l, att_r, a_src, a_dst, zero=None, step_ctr=None, pack=None):
         """a_src / a_dst [N, 2] = x . (W_h^T att^h) for every row of x; ``zero``: a contiguous buffer
         zeroed in the same launch (the step's flat gradient buffer); ``step_ctr``: the optimizer's
-        device step count, advanced in the same launch (its Adam then runs with ``counted=True``)."""
+        device step count, advanced in the same launch (its Adam then runs with ``counted=True``);
+        ``pack`` ((W1c, W2c, _, buffer), ``ops.step_pack``): the head-fused tail's packed weights of
+        W1c, W2c and W written into the buffer by the same launch."""
         N, F = x.shape
         H, C = att_l.shape[-2], att_l.shape[-1]
         vec = _lib.workspace(self.lib.hicgat_xagg_vec_bytes(), x.device)
         assert zero is None or zero.is_contiguous()
+        W1c = W2c = buf = None
+        nb = 0
+        if pack is not None:
+            W1c, W2c, _, buf = pack
+            assert W.is_contiguous() and W1c.is_contiguous() and W2c.is_contiguous()
+            nb = buf.numel() * buf.element_size()
         with _timed("xagg_logits"):
-            _lib.check(self.lib.hicgat_xagg_logits_zero(P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src),
-                                                        P(a_dst), P(zero), 0 if zero is None else zero.numel(),
-                                                        P(step_ctr), _lib.stream(x.device)), "hicgat_xagg_logits_zero")
+            _lib.check(self.lib.hicgat_xagg_logits_zero_pack(
+                P(x), P(W), P(att_l), P(att_r), N, F, H, C, P(vec), P(a_src), P(a_dst), P(zero),
+                0 if zero is None else zero.numel(), P(step_ctr), P(W1c), P(W2c), P(buf), nb,
+                _lib.stream(x.device)), "hicgat_xagg_logits_zero_pack")
 
     def xagg_fwd(self, rowptr, col, r0, r1, x, a_src, a_dst, ns, X4, row_stats):
         """Own rows [r0, r1): X4 [2, 2, r1 - r0, 512] = (xa, xa2) per head; row stats (global rows)."""
@@ -627,8 +636,19 @@ class HipKernels:
                                                           int(bool(counted)), _lib.stream(flat.device)),
                        "hicgat_adam_step_table_ex")
 
-    def step_begin(self, grad, step_ctr=None):
-        """zero_grad of the flat gradient buffer + (step_ctr) the device step count's advance, one launch."""
+    def step_begin(self, grad, step_ctr=None, pack=None):
+        """zero_grad of the flat gradient buffer + (step_ctr) the device step count's advance, one launch;
+        ``pack`` = (W1c, W2c, Wh or None, buffer): the tail's packed weight copies in the same launch
+        (hicgat_step_begin_pack)."""
+        if pack is not None:
+            W1c, W2c, Wh, buf = pack
+            for t in (W1c, W2c) + ((Wh,) if Wh is not None else ()):
+                assert t.is_contiguous() and t.dtype == torch.float32
+            n = int(self.lib.hicgat_tail_pack_bytes())
+            assert buf.numel() * buf.element_size() >= n
+            _lib.check(self.lib.hicgat_step_begin_pack(P(grad), grad.numel(), P(step_ctr), P(W1c), P(W2c), P(Wh), P(buf),
+                                                       n, _lib.stream(grad.device)), "hicgat_step_begin_pack")
+            return
         _lib.check(self.lib.hicgat_step_begin(P(grad), grad.numel(), P(step_ctr), _lib.stream(grad.device)),
                    "hicgat_step_begin")
 

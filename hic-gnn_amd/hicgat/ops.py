@@ -255,6 +255,8 @@ _ACTS = {None: 0, "relu": 1}
 # backward's epilogue when that tail consumes the layer's output (hicgat_tail_bwd_fused_rows); 0: the
 # separate pass
 FUSE_ROWS = os.environ.get("HICGAT_FUSE_ROWS", "1") != "0"
+# the tail's weight pack written by the step's first launch (step_pack); 0: its own launch in the forward
+STEP_PACK = os.environ.get("HICGAT_STEP_PACK", "1") != "0"
 
 
 class _GATConvFn(torch.autograd.Function):
@@ -710,14 +712,18 @@ class _FusedTailFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, Wa, ba, Wal, bal, ga, bea, W1, b1, W1al, b1al, g1, be1, W2, b2, g2, be2, W3, b3, eps,
-                coords_out=None, heads=None):
+                coords_out=None, heads=None, prepack=None):
         K = kernels.default()
         x = x.contiguous()
         W1c, b1c = _joined(Wa, Wal).contiguous(), _joined(ba, bal).contiguous()
         W2c, b2c = _joined(W1, W1al).contiguous(), _joined(b1, b1al).contiguous()
         # heads: x's rows are formed (written) by the kernel from the xagg GATConv's aggregates
-        # the weights as packed copies for both kernels (made once per forward; the backward reuses them)
-        pack = K.tail_pack(W1c, W2c, heads.W if heads is not None else None) if TAIL_PACK else None
+        # the weights as packed copies for both kernels (made once per forward -- or by the training
+        # step's first launch, ``prepack``: step_pack -- the backward reuses them)
+        if prepack is not None:
+            pack = prepack          # (heads: a pack with the heads' W, else the launch is refused)
+        else:
+            pack = K.tail_pack(W1c, W2c, heads.W if heads is not None else None) if TAIL_PACK else None
         coords, saved = K.tail_fwd_fused(x, W1c, b1c, ga.contiguous(), bea.contiguous(), W2c, b2c, g1.contiguous(),
                                          be1.contiguous(), W2.contiguous(), b2.contiguous(), g2.contiguous(),
                                          be2.contiguous(), W3.contiguous(), b3.contiguous(), eps, coords=coords_out,
@@ -769,7 +775,7 @@ class _FusedTailFn(torch.autograd.Function):
             dga, dbea = _ln_param_grads(K, ga, bea, ws1, rows)
             dWa, dba, dWal, dbal = _dual_param_grads(K, Wa, ba, Wal, bal, dY1, x)
             return (dx if ctx.needs_input_grad[0] else None, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al,
-                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None, None, None)
+                    dg1, dbe1, dW2, db2, dg2, dbe2, dW3, db3, None, None, None, None)
         T = (True,) * 8
 
         def c(**kw):
@@ -785,7 +791,7 @@ class _FusedTailFn(torch.autograd.Function):
                                      saved_tensors=(x, Y1, st1, ga, bea), params=(Wa, ba, Wal, bal, ga, bea))
         dx, dWa, dba, dWal, dbal, dga, dbea, _ = _DualLnReluResFn.backward(ctx1, dz1)
         return (dx, dWa, dba, dWal, dbal, dga, dbea, dW1, db1, dW1al, db1al, dg1, dbe1, dW2, db2, dg2, dbe2,
-                dW3, db3, None, None, None)
+                dW3, db3, None, None, None, None)
 
 
 def fused_tail_ok(model, x):
@@ -824,7 +830,44 @@ def fused_tail(model, x, coords_out=None, heads=None):
                               m.norm_a.weight, m.norm_a.bias, m.dense1.weight, m.dense1.bias, m.align_dense1.weight,
                               m.align_dense1.bias, m.norm1.weight, m.norm1.bias, m.dense2.weight, m.dense2.bias,
                               m.norm2.weight, m.norm2.bias, m.dense3.weight, m.dense3.bias, m.norm_a.eps, coords_out,
-                              heads)
+                              heads, getattr(m, "_hicgat_prepack", None))
+
+
+def step_pack(model, x):
+    """The tail's packed weights as part of a training step's first launch: (W1c, W2c, None, buffer)
+    for ``FlatAdam.zero_grad(pack=...)`` when the step's forward will run the one-kernel tail on x's
+    N rows with packed weights (the flagship, ``fused_tail_ok``'s row range, the residual pairs
+    adjacent in FlatAdam's buffer so [W; W_align] are views), else None.  The forward inside
+    ``prepacked(model, job)`` then reads the buffer instead of packing again: one launch fewer per
+    step (the weights change only at the previous step's Adam).  The sharded xagg step passes its
+    own rows and hands the job to ``kernels.xagg_logits(pack=...)``, which adds lin_l's W (the
+    head-fused tail's third weight)."""
+    m = model
+    if not (STEP_PACK and TAIL_PACK and FUSED_TAIL and x.is_cuda and hasattr(m, "align_densea") and hasattr(m, "norm_a")
+            and FUSED_TAIL_MIN_M <= x.shape[0] <= FUSED_TAIL_MAX_M
+            and m.norm_a.eps == m.norm1.eps == m.norm2.eps):
+        return None
+    if not (_adjacent(m.densea.weight, m.align_densea.weight) and _adjacent(m.dense1.weight, m.align_dense1.weight)):
+        return None
+    W1c, W2c = _joined(m.densea.weight, m.align_densea.weight), _joined(m.dense1.weight, m.align_dense1.weight)
+    buf = getattr(m, "_hicgat_pack_buf", None)
+    if buf is None or buf.device != x.device:
+        n = int(kernels.default().lib.hicgat_tail_pack_bytes())
+        buf = m._hicgat_pack_buf = torch.empty(n // 4, dtype=torch.float32, device=x.device)
+    return (W1c.detach(), W2c.detach(), None, buf)
+
+
+@contextlib.contextmanager
+def prepacked(model, job):
+    """The forward inside reads the pack ``job`` (``step_pack``) wrote, if any."""
+    if job is None:
+        yield
+        return
+    model._hicgat_prepack = job[3]
+    try:
+        yield
+    finally:
+        model._hicgat_prepack = None
 
 
 def gat_conv(x, W, att_l, att_r, bias, adj, negative_slope=0.2, act=None):

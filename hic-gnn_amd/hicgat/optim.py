@@ -52,15 +52,17 @@ class FlatAdam:
         self.step_ctr = torch.full((1,), self.step_count, dtype=torch.int64, device=self.flat.device)
         return self
 
-    def zero_grad(self, set_to_none=False):
+    def zero_grad(self, set_to_none=False, pack=None):
         """Zero the flat gradient buffer (``set_to_none`` is ignored: the ``.grad`` views stay).  With
         the device step count on (and a GPU buffer) the zeroing launch also advances the count, and
-        the next ``step()`` reads it without its own increment launch."""
-        if getattr(self, "step_ctr", None) is not None and self.grad.is_cuda:
+        the next ``step()`` reads it without its own increment launch.  ``pack`` (GPU): the one-kernel
+        tail's packed weights written by the same launch (``ops.step_pack``)."""
+        if self.grad.is_cuda and (pack is not None or getattr(self, "step_ctr", None) is not None):
             kern = self.kern if self.kern is not None else kernels.default()
+            ctr = getattr(self, "step_ctr", None)
             # a second zero_grad before the step only zeroes (the count advances once per step)
-            kern.step_begin(self.grad, None if getattr(self, "_counted", False) else self.step_ctr)
-            self._counted = True
+            kern.step_begin(self.grad, None if (ctr is None or getattr(self, "_counted", False)) else ctr, pack=pack)
+            self._counted = ctr is not None
         else:
             self.grad.zero_()
         self._reattach()

@@ -27,8 +27,13 @@ from .optim import FlatAdam
 def train_step(model, opt, x, edge_index, truth, kind="mse", stats=None):
     """One step without any host sync: returns (loss tensor, stats tensor, coords)."""
     model.train()
-    opt.zero_grad()
-    loss, stats, coords = model.loss(x, edge_index, truth, kind, stats=stats)
+    pk = ops.step_pack(model, x) if x.is_cuda else None   # the tail's packed weights ride in the first launch
+    if pk is not None:
+        opt.zero_grad(pack=pk)
+    else:
+        opt.zero_grad()
+    with ops.prepacked(model, pk):
+        loss, stats, coords = model.loss(x, edge_index, truth, kind, stats=stats)
     with ops.overlapped_param_grads(None if x.is_cuda else False):   # dW, db beside the backward
         ops.backward_from_loss(loss)
     opt.step()

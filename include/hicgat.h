@@ -176,6 +176,13 @@ int hicgat_xagg_logits(const float *x, const float *W, const float *att_src, con
 int hicgat_xagg_logits_zero(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
                             int F, int H, int C, float *vec, float *a_src, float *a_dst, float *zero_buf,
                             int64_t zero_n, int64_t *step_counter, hicgat_stream_t stream);
+/* hicgat_xagg_logits_zero that, with pack (NULL: none), also writes the head-fused tail's packed
+ * weights of W1c, W2c and Wh = W (hicgat_tail_pack's layout and pack_bytes rule) in the same launch:
+ * the sharded step's tail kernels then read them without a pack launch of their own. */
+int hicgat_xagg_logits_zero_pack(const float *x, const float *W, const float *att_src, const float *att_dst, int N,
+                                 int F, int H, int C, float *vec, float *a_src, float *a_dst, float *zero_buf,
+                                 int64_t zero_n, int64_t *step_counter, const float *W1c, const float *W2c, void *pack,
+                                 size_t pack_bytes, hicgat_stream_t stream);
 int hicgat_xagg_fwd(const int32_t *rowptr, const int32_t *col, int N, int F, int H, int C, int row_begin,
                     int row_end, const float *x, const float *a_src, const float *a_dst, float neg_slope, float *X4,
                     float *row_stats, hicgat_stream_t stream);
@@ -616,6 +623,11 @@ int hicgat_adam_step_table_ex(float *param, const float *grad, float *exp_avg, f
 /* A step's first launch: grad[0, n) = 0 (zero_grad, HiC-GNN_main.py:124) and, with step_counter
  * (NULL: none), *step_counter += 1 (the step's Adam then uses counted = 1).  grad 16-B aligned. */
 int hicgat_step_begin(float *grad, int64_t n, int64_t *step_counter, hicgat_stream_t stream);
+/* hicgat_step_begin and hicgat_tail_pack(W1c, W2c, Wh, pack) in ONE launch (the step's first: the
+ * weights change only at the previous step's Adam), so the one-kernel tail's packed copies cost no
+ * launch of their own on the step's chain.  Same arguments and checks as the two. */
+int hicgat_step_begin_pack(float *grad, int64_t n, int64_t *step_counter, const float *W1c, const float *W2c,
+                           const float *Wh, void *pack, size_t pack_bytes, hicgat_stream_t stream);
 
 /* ---- measurement infrastructure (no reference counterpart) ----------------------------------
  * An emulated collective for the simulated P-rank step (bench.py --simulate-world,

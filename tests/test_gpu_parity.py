@@ -1630,3 +1630,46 @@ def test_rows_pass_fused_into_tail_backward_is_bitwise(monkeypatch, n, graphed):
         res[fuse] = out
     for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
         assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("n", [3000, 20000])
+def test_step_pack_in_first_launch_is_bitwise(monkeypatch, n):
+    """The one-kernel tail's packed weights written by the training step's first launch
+    (hicgat_step_begin_pack via ops.step_pack / FlatAdam.zero_grad(pack=...)) against the forward's
+    own hicgat_tail_pack launch: two training steps give the same loss, gradients and parameters bit
+    for bit, and the step's buffer holds exactly the packed copy of the step's weights."""
+    import hicgat
+    from hicgat import kernels, ops, synth
+    i, j, c = synth.contact_pairs(n, density=0.05 if n < 20000 else 0.01, seed=5)
+    A = synth.dense_contacts(n, i, j, c, device=DEV)
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    tr = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    x = torch.tensor(synth.features(n, seed=5), device=DEV)
+    res = {}
+    real = ops.step_pack
+    for fold in (False, True):
+        monkeypatch.setattr(ops, "step_pack", real if fold else (lambda model, x: None))
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to(DEV)
+        opt = hicgat.FlatAdam(model.flat_parameters(), lr=1e-3)
+        out = []
+        for _ in range(2):
+            if fold:
+                m = model
+                W1c = torch.cat([m.densea.weight, m.align_densea.weight]).detach()
+                W2c = torch.cat([m.dense1.weight, m.align_dense1.weight]).detach()
+                want = kernels.default().tail_pack(W1c, W2c)
+            loss, _, _ = hicgat.train.train_step(model, opt, x, adj, tr)
+            if fold:
+                torch.cuda.synchronize()
+                # the F1, F2, B1 and B2 regions (the head regions FH, BH stay unwritten without Wh)
+                fh, b1, bh = 512 * 512 + 256 * 256, 2 * 512 * 512 + 256 * 256, 3 * 512 * 512 + 2 * 256 * 256
+                got = model._hicgat_pack_buf
+                for r0, r1 in ((0, fh), (b1, bh)):
+                    assert torch.equal(got[r0:r1], want[r0:r1]), (r0, r1)
+            out.append((float(loss), opt.grad.clone(), opt.flat.clone()))
+        torch.cuda.synchronize()
+        res[fold] = out
+    for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
+        assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)

@@ -257,3 +257,46 @@ def test_xagg_side_branch_equals_serial_order_with_a_real_reduce(n, world):
         hdist.XAGG_SIDE_BRANCH = saved
     for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
         assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("n,world", [(3000, 2), (20000, 8)])
+def test_xagg_step_pack_in_first_launch_is_bitwise(monkeypatch, n, world):
+    """The head-fused tail's packed weights (W1c, W2c and lin_l's W) written by the xagg step's first
+    launch (hicgat_xagg_logits_zero_pack) against the tail forward's own hicgat_tail_pack launch
+    (ops.STEP_PACK = False): the captured step replays to the same loss, gradients and parameters bit
+    for bit, and after each replay the buffer holds exactly the pack of that step's weights."""
+    for p in (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import hicgat
+    from hicgat import dist as hdist
+    from hicgat import kernels, ops, synth
+    density, seed = (0.01, 0) if n == 20000 else (0.05, 3)
+    i, j, c = synth.contact_pairs(n, density=density, seed=seed)
+    A = synth.dense_contacts(n, i, j, c, device="cuda")
+    adj = hicgat.Adj.from_dense_device(A, keep_host=False)
+    truth = hicgat.Truth.from_contacts(A, 0.5)
+    del A
+    x = torch.tensor(synth.features(n, seed=seed), device="cuda")
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(ops, "STEP_PACK", fold)
+        torch.manual_seed(0)
+        model = hicgat.GATNetSelectiveResidualsUpdated().to("cuda")
+        tr = hdist.ShardedTrainer(model, x, adj, truth, lr=1e-3, mode="xagg", comm=hdist.SimComm(world, 0))
+        step = tr.captured(warmup=1)
+        out = []
+        for _ in range(3):
+            m = model
+            W1c = torch.cat([m.densea.weight, m.align_densea.weight]).detach()
+            W2c = torch.cat([m.dense1.weight, m.align_dense1.weight]).detach()
+            want = kernels.default().tail_pack(W1c, W2c, m.conv.lin_l.weight.detach().contiguous())
+            loss = float(step()[0])
+            torch.cuda.synchronize()
+            if fold:
+                assert torch.equal(model._hicgat_pack_buf, want)
+            out.append((loss, tr.opt.grad.clone(), tr.opt.flat.clone()))
+        res[fold] = out
+        del step, tr, model
+    for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
+        assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
