@@ -305,6 +305,13 @@ static int dispatch(const float *A, int64_t lda, const float *B, int64_t ldb, fl
 // takes the scalar-staged path of the same tile in the same launch.
 constexpr int kMaxWJobs = 16, kMaxCJobs = 32, kGroupTile = 128;
 constexpr int64_t WEIGHTED_LG1_ROWS = 1024;   // weighted column-sum jobs taller than this: 2 lanes per row group
+// jobs of at most this many rows (the split-K slabs: 6-16 splits) take one lane per 4 columns with
+// every row in that lane (lg = 8: 1024 columns per block, no LDS combine) instead of 4 row groups of
+// 64 lanes (256 columns per block): a quarter of the blocks for the same bytes
+#ifndef HICGAT_COLSUM_SHORT
+#define HICGAT_COLSUM_SHORT 16
+#endif
+constexpr int64_t kColsumShortRows = HICGAT_COLSUM_SHORT;
 constexpr int kWeightedLg = 1;   // log2 lanes per row group of those jobs (2: 0.425-0.427 ms, 1: 0.422-0.423 at P = 8)
 // The job a block belongs to: the number of later job starts <= b, every start read at a constant
 // offset of the kernel argument block (one batch of scalar loads instead of one dependent load per
@@ -356,7 +363,7 @@ struct CJob {
   float *dst;
   const float *wt;    // optional row weights (stride ldw)
   int64_t ld, rows, cols, ldw, ldd;
-  int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (6: 4 groups ... 2: 64 groups)
+  int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (8: 1 group, 6: 4 ... 2: 64 groups)
   int segs, nchunk;   // row segments (segment s of the rows into dst + s * ldd), column chunks per segment
 };
 struct CJobs {
@@ -439,6 +446,20 @@ static int group_kchunk(const hicgat_wgrad_job *w, int nw, int target, int *spli
     tk += (int64_t)((w[i].M + kGroupTile - 1) / kGroupTile) * ((w[i].N + kGroupTile - 1) / kGroupTile) * w[i].K;
   int64_t kc = target > 0 ? (tk + target - 1) / target : tk;
   kc = std::max<int64_t>(128, (kc + GK - 1) / GK * GK);
+  // deeper chunks until the workgroups fit the target: rounding the split count up overshoots it
+  // (a P = 8 shard: 38 tiles x 7 splits = 266 one-per-CU workgroups on 256 CUs, a second round for
+  // 10 of them; 6 splits: 228)
+  int64_t kmax = 0;
+  for (int i = 0; i < nw; ++i) kmax = std::max<int64_t>(kmax, w[i].K);
+  auto wgs = [&](int64_t c) {
+    int64_t t = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int64_t tiles = (int64_t)((w[i].M + kGroupTile - 1) / kGroupTile) * ((w[i].N + kGroupTile - 1) / kGroupTile);
+      t += tiles * (w[i].lddw == w[i].N ? std::max<int64_t>(1, (w[i].K + c - 1) / c) : 1);
+    }
+    return t;
+  };
+  while (target > 0 && kc < kmax && wgs(kc) > target) kc += GK;
   for (int i = 0; i < nw; ++i) {
     // a job whose dW is not one contiguous [M, N] block is not split (its slab sum writes contiguous rows)
     const bool can = w[i].lddw == w[i].N;
@@ -620,7 +641,8 @@ extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, con
     // lanes per row group by the rows of one segment (one lane per group for the tallest jobs,
     // uncoalesced, measured slower: P = 8 rank step 0.447 vs 0.431 ms, profiles/r04m_sim_ab.txt)
     const int64_t srows = (rows + segs - 1) / segs;
-    J.lg = srows <= 64 ? 6 : srows <= 256 ? 4 : (wt && srows > WEIGHTED_LG1_ROWS) ? kWeightedLg : 2;
+    J.lg = srows <= kColsumShortRows ? 8 : srows <= 64 ? 6 : srows <= 256 ? 4
+         : (wt && srows > WEIGHTED_LG1_ROWS) ? kWeightedLg : 2;
     J.blk0 = blk;
     cj.start[cj.n - 1] = blk;
     const int64_t per = 4 * ((int64_t)1 << J.lg);   // columns per block

@@ -86,8 +86,9 @@ def main():
     for li, (w, c, tg) in enumerate(rec):   # every grouped launch pair of the step (side, then g's)
         pre = f"grads[{li}] target {tg}:"
         res[f"{pre} both launches"] = timeit(lambda: Kp.param_grads_grouped(w, c, tg))
-        res[f"{pre} weight-gradient jobs only (+ their slab sums)"] = timeit(lambda: Kp.param_grads_grouped(w, [], tg))
-        if c:
+        if w:
+            res[f"{pre} weight-gradient jobs only (+ their slab sums)"] = timeit(lambda: Kp.param_grads_grouped(w, [], tg))
+        if c and w:
             res[f"{pre} column-sum jobs only"] = timeit(lambda: Kp.param_grads_grouped([], c, tg))
         for k, job in enumerate(c):
             res[f"{pre} colsum job {k} {tuple(job[0].shape)}{' weighted' if len(job) > 3 else ''}"] = \
