@@ -193,7 +193,15 @@ constexpr int kTailWaves = 16;   // 16: 0.438 / 0.440 vs 0.448 ms per P = 8 rank
 // workgroups, 64 VGPRs at NW = 16) and sinks every weight load next to its MFMAs -- the prefetch ring
 // collapses to one group in flight
 #define HICGAT_TAIL_WPE __attribute__((amdgpu_waves_per_eu(kTailWaves / 4, kTailWaves / 4)))
-template <int RB, int NW, bool HEADS = false, bool PK = false>
+// PERSIST (the plain tail on grids of more than one round): one workgroup per CU walks the row tiles
+// blockIdx, blockIdx + gridDim, ...; the next tile's x rows are copied into a third LDS buffer by
+// LDS-DMA (global_load_lds) while this tile's LayerNorm / block 2 / block 3 run, so neither a tile's
+// x load nor a workgroup's launch sits between two tiles' GEMMs.  Same arithmetic per row: bitwise
+// the one-tile-per-workgroup grid.
+#ifndef HICGAT_TAIL_PERSIST
+#define HICGAT_TAIL_PERSIST 1
+#endif
+template <int RB, int NW, bool HEADS = false, bool PK = false, bool PERSIST = false>
 __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     const float *__restrict__ x, int64_t ldx, int M, const float *__restrict__ W1c, const float *__restrict__ b1c,
     const float *__restrict__ g1, const float *__restrict__ be1, const float *__restrict__ W2c,
@@ -203,25 +211,37 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     float *__restrict__ Y1, float2 *__restrict__ st1, float *__restrict__ z1, float *__restrict__ Y2,
     float2 *__restrict__ st2, float *__restrict__ z2, float *__restrict__ y3, float2 *__restrict__ st3,
     float *__restrict__ z3, float *__restrict__ coords, int64_t xa_hs = 0, const float *__restrict__ Wh = nullptr,
-    const float *__restrict__ bh = nullptr, float *__restrict__ Y0 = nullptr, float *__restrict__ O = nullptr) {
+    const float *__restrict__ bh = nullptr, float *__restrict__ Y0 = nullptr, float *__restrict__ O = nullptr,
+    int ntiles = 0) {
   extern __shared__ __attribute__((aligned(16))) float lds_tail[];
   float *As = lds_tail;              // x rows, then z1 / z2 / z3 rows
   float *Bs = lds_tail + RB * XS;    // Y1, then Y2 / y3 rows
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int m0 = blockIdx.x * RB;
   constexpr int H = RB / 16, NT1 = 32 / NW, NT2 = 16 / NW;   // 16-column tiles per wave: block 1 / block 2
-  // the waves' column tiles rotated by the workgroup (consecutive workgroups of an XCD -- blockIdx
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW: 4, 8 or 16 waves");
+  static_assert(!(PERSIST && HEADS), "the persistent form is the plain tail's");
+  int tile = blockIdx.x;
+  for (int it = 0;; ++it) {
+  if constexpr (PERSIST) {
+    if (tile >= ntiles) break;
+    As = lds_tail + ((it & 1) ? 2 * RB * XS : 0);   // x / z rows alternate between two buffers
+  }
+  const int m0 = tile * RB;
+  // the waves' column tiles rotated by the tile (consecutive workgroups of an XCD -- blockIdx
   // 8 apart -- start on different tiles): the CUs stream different weight rows at any moment instead
   // of all requesting the same L2 lines together.  Which wave computes a column does not change its
   // arithmetic (same k order): bitwise the unrotated kernel
-  const int rot = (blockIdx.x >> 3) & (NW - 1), ws = (wv + rot) & (NW - 1);
-  static_assert(NW == 4 || NW == 8 || NW == 16, "NW: 4, 8 or 16 waves");
-  // x rows (HEADS: xa^0 rows -> As, xa^1 rows -> Bs) -> LDS (rows past M: zeros)
-  for (int e = tid; e < (HEADS ? 2 : 1) * RB * 128; e += 64 * NW) {
-    const int hd = e / (RB * 128), r = (e >> 7) % RB, c4 = e & 127;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + hd * xa_hs + (size_t)(m0 + r) * ldx)[c4];
-    *reinterpret_cast<float4 *>(&(hd ? Bs : As)[r * XS + 4 * c4]) = v;
+  const int rot = (tile >> 3) & (NW - 1), ws = (wv + rot) & (NW - 1);
+  if (!PERSIST || it == 0) {
+    // x rows (HEADS: xa^0 rows -> As, xa^1 rows -> Bs) -> LDS (rows past M: zeros)
+    for (int e = tid; e < (HEADS ? 2 : 1) * RB * 128; e += 64 * NW) {
+      const int hd = e / (RB * 128), r = (e >> 7) % RB, c4 = e & 127;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m0 + r < M) v = reinterpret_cast<const float4 *>(x + hd * xa_hs + (size_t)(m0 + r) * ldx)[c4];
+      *reinterpret_cast<float4 *>(&(hd ? Bs : As)[r * XS + 4 * c4]) = v;
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's copies of the tile's x rows landed
   }
   __syncthreads();
   if constexpr (HEADS) {
@@ -265,6 +285,20 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
     mfma_rows<RB, NT1, 512, PK>(As, XS, W1c, 16 * NT1 * ws, acc, lane);
     store_tiles<RB, NT1>(acc, 16 * NT1 * ws, b1c, Bs, XS, Y1, 512, m0, M, lane);
   }
+  if constexpr (PERSIST) {
+    // the next tile's x rows into the other buffer (free: the previous tile ended at a barrier), one
+    // 1 KB half row per LDS-DMA instruction; rows past M repeat row M - 1 (finite; never stored)
+    const int mn = (tile + (int)gridDim.x) * RB;
+    if (mn < M) {
+      float *nb = lds_tail + ((it & 1) ? 0 : 2 * RB * XS);
+      for (int r = wv; r < RB; r += NW)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const float *src = x + (size_t)min(mn + r, M - 1) * ldx + 256 * hf + 4 * lane;
+          __builtin_amdgcn_global_load_lds(src, nb + r * XS + 256 * hf, 16, 0, 0);
+        }
+    }
+  }
   __syncthreads();
   ln_rows<RB, 256, true, NW>(Bs, XS, g1, be1, eps, As, XS, z1, st1, m0, M, wv, lane);
   __syncthreads();
@@ -303,6 +337,10 @@ __global__ __launch_bounds__(64 * NW) HICGAT_TAIL_WPE void tail_fwd_kernel(
       for (int k = 0; k < 64; ++k) s = fmaf(zr[k], w[k], s);
       coords[(size_t)(m0 + r) * 3 + j] = s + b4[j];
     }
+  }
+  if constexpr (!PERSIST) break;
+  tile += gridDim.x;
+  __syncthreads();   // every wave is done with this tile's LDS rows
   }
 }
 
@@ -758,11 +796,33 @@ int tail_fwd_go(const float *x, int64_t ldx, int M, const float *W1c, const floa
   // tail 1.977 vs 1.913 ms per step for the per-layer kernels, profiles/r03r_ab_fused_tail.txt):
   // with one workgroup per CU every phase's latency is exposed.
   constexpr int RB = 16, NW = kTailWaves;
+  const int ntiles = (M + RB - 1) / RB;
+  if constexpr (!HEADS && HICGAT_TAIL_PERSIST) {
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      return (hipGetDevice(&dev) == hipSuccess &&
+              hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : 0;
+    }();
+    if (ncu > 0 && ntiles > ncu) {   // more than one round of workgroups: one per CU walks the tiles
+      static const bool pattr =
+          hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, false, PK, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 3 * RB * XS * (int)sizeof(float)) ==
+          hipSuccess;
+      if (!pattr) return HICGAT_ELAUNCH;
+      hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, false, PK, true>), dim3(ncu), dim3(64 * NW),
+                         (size_t)3 * RB * XS * sizeof(float), stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2,
+                         W3, b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1, Y2,
+                         reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords,
+                         (int64_t)0, nullptr, nullptr, nullptr, nullptr, ntiles);
+      HICGAT_CHECK_LAUNCH();
+      return HICGAT_OK;
+    }
+  }
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&tail_fwd_kernel<RB, NW, HEADS, PK>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * RB * XS * (int)sizeof(float)) == hipSuccess;
   if (!attr) return HICGAT_ELAUNCH;
-  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, HEADS, PK>), dim3((M + RB - 1) / RB), dim3(64 * NW),
+  hipLaunchKernelGGL((tail_fwd_kernel<RB, NW, HEADS, PK>), dim3(ntiles), dim3(64 * NW),
                      (size_t)2 * RB * XS * sizeof(float), stream, x, ldx, M, W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3,
                      b3, g3, be3, W4, b4, eps, Y1, reinterpret_cast<float2 *>(st1), z1, Y2,
                      reinterpret_cast<float2 *>(st2), z2, y3, reinterpret_cast<float2 *>(st3), z3, coords, hh.xa_hs,

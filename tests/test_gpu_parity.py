@@ -1673,3 +1673,30 @@ def test_step_pack_in_first_launch_is_bitwise(monkeypatch, n):
         res[fold] = out
     for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
         assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("M", [4097, 9001, 20000])
+def test_persistent_tail_forward_is_bitwise_the_tile_grid(M):
+    """More row tiles than CUs: the one-kernel tail forward runs as one workgroup per CU walking the
+    tiles, the next tile's x rows copied into LDS by LDS-DMA during the current one (tail_fused.hip
+    PERSIST).  Against the same launch on row slices of at most 4 096 rows (256 tiles: one tile per
+    workgroup), every output -- coordinates and the nine saved tensors -- is bitwise the same, with
+    and without the packed weights; M = 4097 / 9001: a partial last tile."""
+    from hicgat import kernels
+    K = kernels.default()
+    torch.manual_seed(13)
+    f = dict(device=DEV)
+    W1c, W2c = torch.randn(512, 512, **f) * 0.05, torch.randn(256, 256, **f) * 0.05
+    small = [torch.randn(n, **f) * 0.1 for n in (512, 256, 256, 256, 128, 128, 64, 64, 64)]
+    b1c, g1, be1, b2c, g2, be2, b3, g3, be3 = small
+    g1, g2, g3 = 1 + g1, 1 + g2, 1 + g3
+    W3, W4, b4 = torch.randn(64, 128, **f) * 0.1, torch.randn(3, 64, **f) * 0.1, torch.randn(3, **f) * 0.1
+    x = torch.relu(torch.randn(M, 512, **f))
+    args = (W1c, b1c, g1, be1, W2c, b2c, g2, be2, W3, b3, g3, be3, W4, b4, 1e-5)
+    for pk in (None, K.tail_pack(W1c, W2c)):
+        coords, saved = K.tail_fwd_fused(x, *args, pack=pk)
+        parts = [K.tail_fwd_fused(x[r0:r0 + 4096], *args, pack=pk) for r0 in range(0, M, 4096)]
+        torch.cuda.synchronize()
+        assert torch.equal(coords, torch.cat([c for c, _ in parts]))
+        for k, t in enumerate(saved):
+            assert torch.equal(t, torch.cat([s[k] for _, s in parts])), k
