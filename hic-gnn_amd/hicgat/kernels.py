@@ -430,17 +430,19 @@ class HipKernels:
     ROWS_WGS = int(os.environ.get("HICGAT_ROWS_WGS", "512"))
     SMALL_M = 16
 
-    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None):
         """Every queued parameter gradient of a step in two launches (include/hicgat.h
         hicgat_param_grads_grouped): ``wjobs`` = [(dy [K, M], x [K, N], dW [M, N], db [M] or None,
         accumulate)], ``cjobs`` = [(src [rows, cols], dst [cols], accumulate[, wt [rows] view])].
         A weight gradient of fewer than ``SMALL_M`` output rows (dense3: 3, g_dst: 2) becomes M
         weighted column sums (and a plain one for db) instead of a 128 x 128 MFMA tile that would
-        be 97 % padding."""
+        be 97 % padding (``small_m``: that bound, default ``SMALL_M``; 0: every job a tile -- the
+        tall weighted sums of a 20 000-row step are long single-block chains)."""
         target = self.GROUP_WGS if target_wgs is None else target_wgs
+        small_m = self.SMALL_M if small_m is None else small_m
         big, cjobs = [], list(cjobs)
         for dy, x, dw, db, acc in wjobs:
-            if dy.shape[1] < self.SMALL_M:
+            if dy.shape[1] < small_m:
                 cjobs += [(x, dw[m], acc, dy[:, m]) for m in range(dy.shape[1])]
                 if db is not None:
                     cjobs.append((dy, db, acc))

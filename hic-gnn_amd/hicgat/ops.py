@@ -47,9 +47,10 @@ OVERLAP_DEFAULT = True
 
 # single-GPU step: parameter-gradient jobs of at least this many multiply-adds (the first tail block's
 # 512 x 512 dW, 5.2e9 at N = 20000) are held and issued with lin_l's dW as ONE grouped launch after
-# the source gather (0: off -- they go to the side stream like the rest): 1.876 / 1.879 vs 1.889 /
-# 1.888 ms per step (profiles/r04i_ab_big_group.txt)
-BIG_GROUP = float(os.environ.get("HICGAT_BIG_GROUP", "5e9"))
+# the source gather (0: off -- they go to the side stream like the rest).  Round 4: 1.876 / 1.879 vs
+# 1.889 / 1.888 ms per step with one side launch per item (profiles/r04i_ab_big_group.txt); with the
+# side work as one grouped launch (SIDE_GROUPED) the big dW rides there: 0 since round 6
+BIG_GROUP = float(os.environ.get("HICGAT_BIG_GROUP", "0"))
 
 
 def side_begin():
@@ -67,6 +68,17 @@ def side_mark():
 
 _FLUSH_LANES = (0, 4, 5, 6)
 SMALL_WORK = 4e6   # side_flush(lanes > 1): items below this many multiply-adds go first in their lane
+# single-GPU step (one lane): the queued side work -- every dW / db / LayerNorm sum of the MLP tail,
+# the first block's 512 x 512 dW included (BIG_GROUP 0) -- as ONE grouped weight-gradient + ONE
+# grouped column-sum launch (hicgat_param_grads_grouped) beside the source gather, when every item has
+# a job descriptor, instead of ~13 launches that each waited for room beside the gather; 0: one
+# launch per item.  SIDE_GROUP_WGS: the grouped launch's workgroup target (the K split): fewer
+# workgroups take fewer CUs from the gather; SIDE_SMALL_M 0: dense3's 3-row dW as an MFMA tile, not
+# three 20 000-row weighted column sums (single-block chains, 157 µs of the side lane).  1.730-1.732
+# vs 1.769-1.771 ms per step (profiles/r06rst_ab_side_grouped.txt, r06u_ab_side_grouped.txt)
+SIDE_GROUPED = os.environ.get("HICGAT_SIDE_GROUPED", "1") != "0"
+SIDE_GROUP_WGS = int(os.environ.get("HICGAT_SIDE_GROUP_WGS", "192"))
+SIDE_SMALL_M = int(os.environ.get("HICGAT_SIDE_SMALL_M", "0"))
 
 
 def side_flush(after=None, lanes=1):
@@ -85,6 +97,12 @@ def side_flush(after=None, lanes=1):
     if not queue:
         return
     n = max(1, min(lanes, len(_FLUSH_LANES)))
+    if n == 1 and SIDE_GROUPED and all(q[3] is not None for q in queue):
+        with _side(*[t for _, keep, _, _ in queue for t in keep], after=after, lane=_FLUSH_LANES[0]):
+            streams.stamp("side_begin")
+            _grouped_launch(kernels.default(), [q[3] for q in queue], SIDE_GROUP_WGS, small_m=SIDE_SMALL_M)
+            streams.stamp("side_end")
+        return
     load, parts = [0] * n, [[] for _ in range(n)]
     if n == 1:
         parts[0] = queue                     # backward order
@@ -99,9 +117,9 @@ def side_flush(after=None, lanes=1):
             # first in their lane, then the GEMMs
             items = [q for q in items if q[2] < SMALL_WORK] + [q for q in items if q[2] >= SMALL_WORK]
         if items:
-            with _side(*[t for _, keep, _ in items for t in keep], after=after, lane=lane):
+            with _side(*[t for _, keep, _, _ in items for t in keep], after=after, lane=lane):
                 streams.stamp("side_begin")
-                for fn, _, _ in items:
+                for fn, _, _, _ in items:
                     fn()
                 streams.stamp("side_end")
 
@@ -147,14 +165,18 @@ def grouped_flush(K=None, extra=(), target_wgs=None):
     jobs = jobs + [(j, ()) for j in extra]
     if not jobs:
         return []
-    K = K if K is not None else kernels.default()
-    # descriptors: ("w", dy, x, dW, db[, accumulate]) / ("c", src, dst[, accumulate[, row weights]]);
-    # accumulate defaults on; a 2-D dst [segs, cols] takes the rows' sum in segments (kernels.param_grads_grouped)
-    w = [(j[1], j[2], j[3], j[4], j[5] if len(j) > 5 else True) for j, _ in jobs if j[0] == "w"]
-    c = [(j[1], j[2], j[3] if len(j) > 3 else True) + ((j[4],) if len(j) > 4 else ()) for j, _ in jobs
-         if j[0] == "c"]
-    K.param_grads_grouped(w, c, target_wgs)
+    _grouped_launch(K if K is not None else kernels.default(), [j for j, _ in jobs], target_wgs)
     return [t for _, keep in jobs for t in keep]
+
+
+def _grouped_launch(K, descs, target_wgs=None, small_m=None):
+    """descriptors: ("w", dy, x, dW, db[, accumulate]) / ("c", src, dst[, accumulate[, row weights]]);
+    accumulate defaults on; a 2-D dst [segs, cols] takes the rows' sum in segments
+    (kernels.param_grads_grouped)"""
+    w = [(j[1], j[2], j[3], j[4], j[5] if len(j) > 5 else True) for j in descs if j[0] == "w"]
+    c = [(j[1], j[2], j[3] if len(j) > 3 else True) + ((j[4],) if len(j) > 4 else ()) for j in descs
+         if j[0] == "c"]
+    K.param_grads_grouped(w, c, target_wgs, small_m)
 
 
 def side_join():
@@ -217,7 +239,7 @@ def _param_launch(fn, *keep, small=False, work=0, job=None):
         fn()
     else:
         with _SIDE_LOCK:
-            _SIDE["queue"].append((fn, keep, work))
+            _SIDE["queue"].append((fn, keep, work, job))
 
 
 def _side(*keep, after=None, lane=0):

@@ -286,7 +286,7 @@ class CpuKernels:
             s3 = row_stats[r0:r1, 3 * H:4 * H].double()
             row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
 
-    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None):
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None):
         for dy, x, dw, db, acc in wjobs:
             r = dy.double().t() @ x.double()
             dw.copy_((r + dw.double()).float() if acc else r.float())

@@ -12,7 +12,7 @@
 #   smoke        __graft_entry__.smoke()
 #   bench        default bench.py (N = 1, synth-20000, with the CPU baseline)
 #   bench2000    bench.py --workload synth-2000 --no-cpu-baseline
-#   ab:<env>     bench.py 200 steps under the environment assignment <env> (A/B lines "ab: ...")
+#   ab:<env>     bench.py 200 steps under the environment assignment(s) <env> (comma-separated; A/B lines "ab: ...")
 #   ab2000:<env> the same on synth-2000 (400 steps)
 #   prof         rocprofv3 --kernel-trace --stats of bench.py (20 steps, graph replay)
 #   pmc_traffic  two PMC passes (FETCH_SIZE, WRITE_SIZE) of an eager bench -> <tag>_pmc_traffic.json
@@ -76,16 +76,21 @@ for S in "$@"; do
         2> gpurun_out/${T}_bench_synth2000.err || exit $?
       grep -o '"ms_per_step": [0-9.]*' gpurun_out/${T}_bench_synth2000.json ;;
     ab:*)
-      env ${S#ab:} timeout -k 10 180 python bench.py --steps 200 --warmup 10 --no-cpu-baseline > gpurun_out/${T}_ab.json \
+      # ab:<env>[,<env>...]: one or more assignments, comma-separated
+      E=${S#ab:}
+      env ${E//,/ } timeout -k 10 180 python bench.py --steps 200 --warmup 10 --no-cpu-baseline > gpurun_out/${T}_ab.json \
         2> gpurun_out/${T}_ab.err || exit $?
       echo "ab: ${S#ab:} $(python -c "import json;d=json.loads(open('gpurun_out/${T}_ab.json').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],4), round(d['median_ms_per_step'],4))")" ;;
     ab2000:*)
       env ${S#ab2000:} timeout -k 10 180 python bench.py --workload synth-2000 --steps 400 --warmup 10 --no-cpu-baseline \
         > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err || exit $?
       echo "ab2000: ${S#ab2000:} $(python -c "import json;d=json.loads(open('gpurun_out/${T}_ab.json').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],4), round(d['median_ms_per_step'],4))")" ;;
-    prof)
+    prof|prof:*)
+      # prof:<env>[,<env>...]: under environment assignments (exported before rocprofv3: no launcher hop)
+      if [ "$S" != prof ]; then E=${S#prof:}; for a in ${E//,/ }; do export "$a"; done; fi
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run --output-format csv -- \
         python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_rocprof.log 2>&1 || exit $?
+      python tools/step_timeline.py gpurun_out/${T}_prof/run_kernel_trace.csv 10 > gpurun_out/${T}_step_timeline.txt || exit $?
       echo "prof ok" ;;
     pmc_traffic)
       timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/${T}_pmc_fetch -o run --output-format csv -- \
