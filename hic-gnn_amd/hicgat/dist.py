@@ -83,6 +83,9 @@ def resolve_mode(mode, P):
 # 0.489 ms; the tail's gradients and bucket alone on the side stream (the heads' dW and the GATConv
 # bucket after the edge pass): 0.495 / 0.497 (removed)
 XAGG_SIDE_WGS = int(os.environ.get("HICGAT_XAGG_SIDE_WGS", "256"))
+# that launch's bound below which a dW becomes weighted column sums (kernels.param_grads_grouped
+# small_m; 0: dense3's 3-row dW as an MFMA tile)
+XAGG_SMALL_M = int(os.environ.get("HICGAT_XAGG_SMALL_M", "16"))
 # the xagg step's side branch (grouped dW + the flat-gradient all-reduce) on the "grad" stream beside
 # the edge pass; False: the same launches in the same order on the step's own stream (the serial
 # order tests/test_gpu_xagg.py compares the overlapped step against)
@@ -746,7 +749,7 @@ class ShardedTrainer:
             # numbers with a communicator whose all-reduce really changes the buffer).
             with torch.cuda.stream(side) if side is not None else _null():
                 streams.stamp("grad_begin")
-                keep = ops.grouped_flush(K, heads, target_wgs=XAGG_SIDE_WGS)
+                keep = ops.grouped_flush(K, heads, target_wgs=XAGG_SIDE_WGS, small_m=XAGG_SMALL_M)
                 # every gradient but the attention vectors' (0 until the finish) and W's att (x) g term
                 self.comm.all_reduce(self.opt.grad, name="grad_all_reduce")
                 streams.stamp("grad_end")

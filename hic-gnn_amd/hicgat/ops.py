@@ -156,7 +156,7 @@ def grouped_param_grads():
             _SIDE["grouped"] -= 1
 
 
-def grouped_flush(K=None, extra=(), target_wgs=None):
+def grouped_flush(K=None, extra=(), target_wgs=None, small_m=None):
     """Issue the collected jobs (plus ``extra`` descriptors) on the current stream: one grouped
     weight-gradient launch and one grouped column-sum launch.  Returns the tensors they read (the
     caller keeps them alive until the launches are ordered before any reuse)."""
@@ -165,7 +165,7 @@ def grouped_flush(K=None, extra=(), target_wgs=None):
     jobs = jobs + [(j, ()) for j in extra]
     if not jobs:
         return []
-    _grouped_launch(K if K is not None else kernels.default(), [j for j, _ in jobs], target_wgs)
+    _grouped_launch(K if K is not None else kernels.default(), [j for j, _ in jobs], target_wgs, small_m)
     return [t for _, keep in jobs for t in keep]
 
 
