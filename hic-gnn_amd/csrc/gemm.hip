@@ -332,18 +332,15 @@ struct WJob {
   int64_t ldy, ldx, lddw;
   int M, N, K, kchunk, tm, tn, wg0, accumulate, vec;
 };
-template <int KMAX>
-struct WJobsT {
-  int start[KMAX];   // job k's first workgroup (= j[k].wg0), contiguous for find_job
-  WJob j[KMAX];
+struct WJobs {
+  int start[kMaxWJobs];   // job k's first workgroup (= j[k].wg0), contiguous for find_job
+  WJob j[kMaxWJobs];
   int n;
 };
-using WJobs = WJobsT<kMaxWJobs>;
-template <class JT>
-__device__ __forceinline__ void wgrad_block(const JT &jobs, int b) {
-  const int q = find_job(jobs.start, jobs.n, b);
+__global__ __launch_bounds__(256, kOcc128) void wgrad_grouped_kernel(const WJobs jobs) {
+  const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const WJob &J = jobs.j[q];
-  const int local = b - J.wg0, per = J.tm * J.tn;
+  const int local = blockIdx.x - J.wg0, per = J.tm * J.tn;
   const int bz = local / per, rem = local - bz * per, bx = rem % J.tm, by = rem / J.tm;
   const int64_t stride = (int64_t)J.M * J.N + J.M;
   float *cs = J.db ? (J.slab ? J.slab + (int64_t)J.M * J.N : J.db) : nullptr;
@@ -355,9 +352,6 @@ __device__ __forceinline__ void wgrad_block(const JT &jobs, int b) {
     gemm_tile<kGroupTile, kGroupTile, true, true, false, false, true>(J.dy, J.ldy, J.x, J.ldx, J.dw, J.lddw, J.M, J.N,
                                                                       J.K, J.kchunk, nullptr, J.slab, stride,
                                                                       J.accumulate, cs, bx, by, bz);
-}
-__global__ __launch_bounds__(256, kOcc128) void wgrad_grouped_kernel(const WJobs jobs) {
-  wgrad_block(jobs, (int)blockIdx.x);
 }
 
 // Launch 2: column sums dst[c] (+)= sum_{r < rows} src[r * ld + c] of every job -- the slab sums of
@@ -372,28 +366,25 @@ struct CJob {
   int blk0, accumulate, vec, lg;   // lg: log2 of the lanes per row group (8: 1 group, 6: 4 ... 2: 64 groups)
   int segs, nchunk;   // row segments (segment s of the rows into dst + s * ldd), column chunks per segment
 };
-template <int KMAX>
-struct CJobsT {
-  int start[KMAX];   // job k's first block (= j[k].blk0)
-  CJob j[KMAX];
+struct CJobs {
+  int start[kMaxCJobs];   // job k's first block (= j[k].blk0)
+  CJob j[kMaxCJobs];
   int n;
 };
-using CJobs = CJobsT<kMaxCJobs>;
 __device__ __forceinline__ float4 ld4(const float *p, bool vec, int64_t c, int64_t cols) {
   if (vec) return *reinterpret_cast<const float4 *>(p);
   return make_float4(p[0], c + 1 < cols ? p[1] : 0.f, c + 2 < cols ? p[2] : 0.f, c + 3 < cols ? p[3] : 0.f);
 }
-template <class JT>
-__device__ __forceinline__ void colsum_block(const JT &jobs, int b) {
+__global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
   __shared__ float4 red[256];
-  const int q = find_job(jobs.start, jobs.n, b);
+  const int q = find_job(jobs.start, jobs.n, (int)blockIdx.x);
   const CJob &J = jobs.j[q];
   // a job of many rows (LayerNorm partial rows, g_src's partial rows) takes 16 or 64 row groups of
   // 16 / 4 lanes per block, a short one (split-K slabs) 4 groups of 64 lanes: the in-order chain of
   // one lane stays short either way
   const int L = 1 << J.lg, ng = 256 >> J.lg;
   const int lane = threadIdx.x & (L - 1), g = threadIdx.x >> J.lg;
-  const int lb = b - J.blk0, seg = lb / J.nchunk;
+  const int lb = blockIdx.x - J.blk0, seg = lb / J.nchunk;
   const int64_t c = ((int64_t)(lb - seg * J.nchunk) * L + lane) * 4;   // first of this lane's 4 columns
   const int64_t s0 = J.rows * seg / J.segs, sn = J.rows * (seg + 1) / J.segs - s0;   // the block's row segment
   const int64_t r0 = s0 + sn * g / ng, r1 = s0 + sn * (g + 1) / ng;
@@ -444,22 +435,6 @@ __device__ __forceinline__ void colsum_block(const JT &jobs, int b) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
     if (c + e < J.cols) d[e] = o[e] + (J.accumulate ? d[e] : 0.f);
-}
-__global__ __launch_bounds__(256) void colsum_grouped_kernel(const CJobs jobs) {
-  colsum_block(jobs, (int)blockIdx.x);
-}
-
-// hicgat_param_grads_grouped_co's first launch: the weight-gradient tiles (blocks [0, nwg)) and, in the
-// same grid, column-sum jobs that need none of their results (blocks nwg ..): the memory-bound sums
-// run on the CUs beside the MFMA tiles instead of before or after them.  Small job tables (the
-// kernel argument block holds both).
-constexpr int kCoWJobs = 4, kCoCJobs = 8;
-__global__ __launch_bounds__(256, kOcc128) void wgrad_colsum_kernel(const WJobsT<kCoWJobs> wj, int nwg,
-                                                                   const CJobsT<kCoCJobs> cj) {
-  if ((int)blockIdx.x < nwg)
-    wgrad_block(wj, (int)blockIdx.x);
-  else
-    colsum_block(cj, (int)blockIdx.x - nwg);
 }
 
 // The common K-chunk depth: about target_wgs workgroups over the union of the jobs' tiles, a multiple
@@ -629,25 +604,23 @@ extern "C" size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *w, 
   return tot;
 }
 
-namespace {
-// both entries: launch 1 = the weight-gradient tiles (+ the concurrent column-sum jobs co, in the same
-// grid), launch 2 = the split slabs' sums + the column-sum jobs c
-int grouped_impl(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, int nc, const hicgat_colsum_job *co,
-                 int nco, int target_wgs, void *workspace, size_t workspace_bytes, hipStream_t s) {
-  if (nw < 0 || nc < 0 || nco < 0 || (nw && !w) || (nc && !c) || (nco && !co)) return HICGAT_EINVAL;
-  if (nw > kMaxWJobs || (nco && (nw > kCoWJobs || nco > kCoCJobs))) return HICGAT_EUNSUPPORTED;
+extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, int nc,
+                                          int target_wgs, void *workspace, size_t workspace_bytes,
+                                          hicgat_stream_t stream) {
+  if (nw < 0 || nc < 0 || (nw && !w) || (nc && !c)) return HICGAT_EINVAL;
+  if (nw > kMaxWJobs) return HICGAT_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
   int splits[kMaxWJobs];
   const int kc = nw ? group_kchunk(w, nw, target_wgs, splits) : 0;
   WJobs wj;
-  CJobs cj, cc;   // cc: the concurrent jobs (block numbers from 0 within their part of launch 1)
+  CJobs cj;
   wj.n = 0;
   cj.n = 0;
-  cc.n = 0;
-  int wg = 0, blk = 0, cblk = 0;
+  int wg = 0, blk = 0;
   float *slab = static_cast<float *>(workspace);
   size_t used = 0;
-  auto add_to = [&](CJobs &cj, int &blk, const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc,
-                    const float *wt, int64_t ldw, int segs, int64_t ldd) {
+  auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc,
+                     const float *wt = nullptr, int64_t ldw = 0, int segs = 1, int64_t ldd = 0) {
     if (cols <= 0) return HICGAT_OK;
     if (cj.n == kMaxCJobs) return HICGAT_EUNSUPPORTED;
     if (segs < 1) segs = 1;
@@ -676,10 +649,6 @@ int grouped_impl(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, 
     J.nchunk = (int)((cols + per - 1) / per);
     blk += J.nchunk * segs;
     return HICGAT_OK;
-  };
-  auto add_col = [&](const float *src, int64_t ld, int64_t rows, int64_t cols, float *dst, int acc,
-                     const float *wt = nullptr, int64_t ldw = 0, int segs = 1, int64_t ldd = 0) {
-    return add_to(cj, blk, src, ld, rows, cols, dst, acc, wt, ldw, segs, ldd);
   };
   for (int i = 0; i < nw; ++i) {
     const hicgat_wgrad_job &a = w[i];
@@ -729,30 +698,7 @@ int grouped_impl(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, 
                            c[i].segs, c[i].ldd);
     if (rc != HICGAT_OK) return rc;
   }
-  for (int i = 0; i < nco; ++i) {
-    if (co[i].rows < 0 || co[i].cols < 0 || (co[i].cols > 0 && !co[i].dst) || (co[i].rows > 0 && !co[i].src))
-      return HICGAT_EINVAL;
-    const int rc = add_to(cc, cblk, co[i].src, co[i].ld, co[i].rows, co[i].cols, co[i].dst, co[i].accumulate, co[i].wt,
-                          co[i].ldw, co[i].segs, co[i].ldd);
-    if (rc != HICGAT_OK) return rc;
-  }
-  if (cblk > 0) {
-    if (cc.n > kCoCJobs || wj.n > kCoWJobs) return HICGAT_EUNSUPPORTED;
-    WJobsT<kCoWJobs> w4{};
-    CJobsT<kCoCJobs> c8{};
-    w4.n = wj.n;
-    for (int i = 0; i < wj.n; ++i) {
-      w4.start[i] = wj.start[i];
-      w4.j[i] = wj.j[i];
-    }
-    c8.n = cc.n;
-    for (int i = 0; i < cc.n; ++i) {
-      c8.start[i] = cc.start[i];
-      c8.j[i] = cc.j[i];
-    }
-    hipLaunchKernelGGL(wgrad_colsum_kernel, dim3(wg + cblk), dim3(256), 0, s, w4, wg, c8);
-    HICGAT_CHECK_LAUNCH();
-  } else if (wg > 0) {
+  if (wg > 0) {
     hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(wg), dim3(256), 0, s, wj);
     HICGAT_CHECK_LAUNCH();
   }
@@ -761,19 +707,6 @@ int grouped_impl(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, 
     HICGAT_CHECK_LAUNCH();
   }
   return HICGAT_OK;
-}
-}  // namespace
-
-extern "C" int hicgat_param_grads_grouped(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, int nc,
-                                          int target_wgs, void *workspace, size_t workspace_bytes,
-                                          hicgat_stream_t stream) {
-  return grouped_impl(w, nw, c, nc, nullptr, 0, target_wgs, workspace, workspace_bytes, (hipStream_t)stream);
-}
-
-extern "C" int hicgat_param_grads_grouped_co(const hicgat_wgrad_job *w, int nw, const hicgat_colsum_job *c, int nc,
-                                             const hicgat_colsum_job *co, int nco, int target_wgs, void *workspace,
-                                             size_t workspace_bytes, hicgat_stream_t stream) {
-  return grouped_impl(w, nw, c, nc, co, nco, target_wgs, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" size_t hicgat_gemm_workspace_bytes(int M, int N, int splits) {

@@ -124,8 +124,6 @@ SIGNATURES = {
     "hicgat_gemm_rows_grouped": (c_int, [c_gjobs, c_int, c_int, c_int, c_p, c_sz, c_p]),
     "hicgat_param_grads_workspace_bytes": (c_sz, [c_wjobs, c_int, c_int]),
     "hicgat_param_grads_grouped": (c_int, [c_wjobs, c_int, c_cjobs, c_int, c_int, c_p, c_sz, c_p]),
-    "hicgat_param_grads_grouped_co": (c_int, [c_wjobs, c_int, c_cjobs, c_int, c_cjobs, c_int, c_int, c_p, c_sz,
-                                              c_p]),
     "hicgat_colsum": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_int, c_p, c_sz, c_p]),
     "hicgat_colsum_workspace_bytes": (c_sz, [c_int, c_int]),
     "hicgat_ln_relu_res_fwd": (c_int, [c_p, c_i64, c_int, c_int, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_p]),

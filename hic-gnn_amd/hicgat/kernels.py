@@ -430,17 +430,14 @@ class HipKernels:
     ROWS_WGS = int(os.environ.get("HICGAT_ROWS_WGS", "512"))
     SMALL_M = 16
 
-    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None, co=None):
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None):
         """Every queued parameter gradient of a step in two launches (include/hicgat.h
         hicgat_param_grads_grouped): ``wjobs`` = [(dy [K, M], x [K, N], dW [M, N], db [M] or None,
         accumulate)], ``cjobs`` = [(src [rows, cols], dst [cols], accumulate[, wt [rows] view])].
         A weight gradient of fewer than ``SMALL_M`` output rows (dense3: 3, g_dst: 2) becomes M
         weighted column sums (and a plain one for db) instead of a 128 x 128 MFMA tile that would
         be 97 % padding (``small_m``: that bound, default ``SMALL_M``; 0: every job a tile -- the
-        tall weighted sums of a 20 000-row step are long single-block chains).  ``co``: column-sum
-        jobs (same form) run INSIDE the weight-gradient launch, beside its tiles
-        (hicgat_param_grads_grouped_co: at most 4 weight-gradient and 8 such jobs, which must not read
-        what the tiles write; ``cjobs`` then run after both and may read what ``co`` wrote)."""
+        tall weighted sums of a 20 000-row step are long single-block chains)."""
         target = self.GROUP_WGS if target_wgs is None else target_wgs
         small_m = self.SMALL_M if small_m is None else small_m
         big, cjobs = [], list(cjobs)
@@ -458,37 +455,25 @@ class HipKernels:
             assert db is None or db.is_contiguous()
             W[k] = _lib.WgradJob(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), dw.stride(0),
                                  None if db is None else db.data_ptr(), dy.shape[1], x.shape[1], dy.shape[0], int(acc))
-        def table(jobs):
-            C = (_lib.ColsumJob * max(1, len(jobs)))()
-            for k, job in enumerate(jobs):
-                src, dst, acc = job[:3]
-                wt = job[3] if len(job) > 3 else None
-                assert src.dim() == 2 and src.stride(1) == 1
-                if dst.dim() == 2:    # [segs, cols]: the rows summed in segs segments, one dst row each
-                    assert (dst.stride(1) == 1 and dst.shape[1] == src.shape[1]
-                            and 1 <= dst.shape[0] <= max(1, src.shape[0]))
-                    segs, ldd = dst.shape[0], dst.stride(0)
-                else:
-                    assert dst.is_contiguous() and dst.numel() == src.shape[1]
-                    segs, ldd = 1, 0
-                assert wt is None or (wt.dim() == 1 and wt.shape[0] == src.shape[0])
-                C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(),
-                                      int(acc), None if wt is None else wt.data_ptr(),
-                                      0 if wt is None else wt.stride(0), segs, ldd)
-            return C
-
-        C = table(cjobs)
-        dev = (wjobs[0][0] if wjobs else (cjobs or co)[0][0]).device
+        C = (_lib.ColsumJob * max(1, len(cjobs)))()
+        for k, job in enumerate(cjobs):
+            src, dst, acc = job[:3]
+            wt = job[3] if len(job) > 3 else None
+            assert src.dim() == 2 and src.stride(1) == 1
+            if dst.dim() == 2:    # [segs, cols]: the rows summed in segs segments, one dst row each
+                assert dst.stride(1) == 1 and dst.shape[1] == src.shape[1] and 1 <= dst.shape[0] <= max(1, src.shape[0])
+                segs, ldd = dst.shape[0], dst.stride(0)
+            else:
+                assert dst.is_contiguous() and dst.numel() == src.shape[1]
+                segs, ldd = 1, 0
+            assert wt is None or (wt.dim() == 1 and wt.shape[0] == src.shape[0])
+            C[k] = _lib.ColsumJob(src.data_ptr(), src.stride(0), src.shape[0], src.shape[1], dst.data_ptr(), int(acc),
+                                  None if wt is None else wt.data_ptr(), 0 if wt is None else wt.stride(0), segs, ldd)
+        dev = (wjobs[0][0] if wjobs else cjobs[0][0]).device
         ws = _lib.workspace(self.lib.hicgat_param_grads_workspace_bytes(W, len(wjobs), target), dev)
         with _timed("param_grads_grouped"):
-            if co:
-                _lib.check(self.lib.hicgat_param_grads_grouped_co(W, len(wjobs), C, len(cjobs), table(co), len(co),
-                                                                  int(target), P(ws), ws.numel(), _lib.stream(dev)),
-                           "hicgat_param_grads_grouped_co")
-            else:
-                _lib.check(self.lib.hicgat_param_grads_grouped(W, len(wjobs), C, len(cjobs), int(target), P(ws),
-                                                               ws.numel(), _lib.stream(dev)),
-                           "hicgat_param_grads_grouped")
+            _lib.check(self.lib.hicgat_param_grads_grouped(W, len(wjobs), C, len(cjobs), int(target), P(ws), ws.numel(),
+                                                           _lib.stream(dev)), "hicgat_param_grads_grouped")
 
     def gemm_rows_grouped(self, jobs, b_kmajor, splits=None, name="gemm_grouped"):
         """include/hicgat.h hicgat_gemm_rows_grouped: ``jobs`` = [(A [M, K], B, C [M, N], bias or None,

@@ -79,9 +79,6 @@ SMALL_WORK = 4e6   # side_flush(lanes > 1): items below this many multiply-adds 
 SIDE_GROUPED = os.environ.get("HICGAT_SIDE_GROUPED", "1") != "0"
 SIDE_GROUP_WGS = int(os.environ.get("HICGAT_SIDE_GROUP_WGS", "192"))
 SIDE_SMALL_M = int(os.environ.get("HICGAT_SIDE_SMALL_M", "0"))
-# the single-GPU GATConv's param_grad sums inside lin_l's dW launch (hicgat_param_grads_grouped_co)
-PG_CONCURRENT = os.environ.get("HICGAT_PG_CONCURRENT", "0") != "0"
-PG_SEGS = int(os.environ.get("HICGAT_PG_SEGS", "32"))
 
 
 def side_flush(after=None, lanes=1):
@@ -364,26 +361,7 @@ class _GATConvFn(torch.autograd.Function):
         # after the gathers: the GAT column sums, then lin_l's dW on this stream (with the held
         # first-block dW: BIG_GROUP).  The column sums on a side stream beside the grouped dW launch:
         # 1.964 / 1.970 vs 1.877 / 1.872 ms per step (profiles/r04l_ab_single_gpu.txt)
-        gW = _sink(pW) if ctx.needs_input_grad[1] else None
-        co = (PG_CONCURRENT and use_sinks and gW is not None and not _SIDE["jobs"] and H == 2
-              and h.shape[1] == 2 * al.shape[-1])
-        if co:
-            # lin_l's dW and the GAT column sums (param_grad's three parts as weighted / plain column
-            # sums of h and dout) in ONE launch: the memory-bound sums beside the MFMA tiles
-            # each a tall sum in PG_SEGS row segments into a [segs, cols] buffer (short chains beside the
-            # tiles), the segments added by the slab-sum launch that follows
-            C = al.shape[-1]
-            sl, sr = sinks[0].view(-1), sinks[1].view(-1)
-            S = max(1, min(PG_SEGS, N // 256))
-            seg = torch.empty((5, S, 2 * C), dtype=torch.float32, device=h.device)
-            co = [(h[:, hd * C:(hd + 1) * C], seg[0, :, hd * C:(hd + 1) * C], False, da_src[:, hd]) for hd in range(H)]
-            co += [(h[:, hd * C:(hd + 1) * C], seg[1, :, hd * C:(hd + 1) * C], False, row_stats[:, 3 * H + hd])
-                   for hd in range(H)]
-            co += [(dout, seg[2], False)]
-            cj = [(seg[0], sl, True), (seg[1], sr, True), (seg[2], sinks[2], True)]
-            K.param_grads_grouped([(dh, x, gW, None, True)], cj, target_wgs=_DW_BLOCKS, co=co)
-            datt_l = datt_r = dbias = None
-        elif use_sinks:
+        if use_sinks:
             K.param_grad(h, dout, da_src, row_stats, H, out=(sinks[0].view(-1), sinks[1].view(-1), sinks[2]),
                          accumulate=True)
             datt_l = datt_r = dbias = None
@@ -392,7 +370,8 @@ class _GATConvFn(torch.autograd.Function):
             datt_l, datt_r = datt_l.view(al.shape), datt_r.view(ar.shape)
             dbias = dbias if ctx.has_bias else None
         dW = None
-        if ctx.needs_input_grad[1] and not co:
+        if ctx.needs_input_grad[1]:
+            gW = _sink(pW)
             if gW is not None and _SIDE["jobs"]:
                 # the held big dW jobs and lin_l's as one grouped launch (BIG_GROUP)
                 _SIDE["hold"].extend(grouped_flush(K, [("w", dh, x, gW, None)]))

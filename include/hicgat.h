@@ -425,15 +425,6 @@ typedef struct hicgat_colsum_job {
 size_t hicgat_param_grads_workspace_bytes(const hicgat_wgrad_job *wjobs, int nw, int target_wgs);
 int hicgat_param_grads_grouped(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
                                int target_wgs, void *workspace, size_t workspace_bytes, hicgat_stream_t stream);
-/* The same with the column-sum jobs `co` (at most 8; at most 4 weight-gradient jobs) issued INSIDE
- * the weight-gradient launch, in blocks after the GEMM tiles, so the memory-bound sums run beside the
- * MFMA tiles (they must not read what those write); the second launch carries the split slabs' sums
- * and the jobs `c` (which may read what `co` wrote: e.g. `co` sums tall columns in row segments into
- * a [segs, cols] buffer, `c` adds the segments).  Replaces the GATConv's hicgat_gat_param_grad before
- * lin_l's dW on one GPU. */
-int hicgat_param_grads_grouped_co(const hicgat_wgrad_job *wjobs, int nw, const hicgat_colsum_job *cjobs, int nc,
-                                  const hicgat_colsum_job *co, int nco, int target_wgs, void *workspace,
-                                  size_t workspace_bytes, hicgat_stream_t stream);
 /* Grouped node-row GEMMs of one layout: C_j = A_j op(B_j) (+ bias_j), A_j [M, K] row-major (ld lda),
  * op(B) = B^T (B [N, K], b_kmajor = 0: a Linear / head forward) or B (B [K, N], b_kmajor = 1: an
  * input gradient), c_relu (NULL or ld ldr): relu of the result too.  ONE launch of 64 x 128 fp32-MFMA

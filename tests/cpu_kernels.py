@@ -286,22 +286,15 @@ class CpuKernels:
             s3 = row_stats[r0:r1, 3 * H:4 * H].double()
             row_stats[r0:r1, 3 * H:4 * H] = (q - row_stats[r0:r1, 2 * H:3 * H].double() * s3).float()
 
-    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None, co=None):
+    def param_grads_grouped(self, wjobs, cjobs, target_wgs=None, small_m=None):
         for dy, x, dw, db, acc in wjobs:
             r = dy.double().t() @ x.double()
             dw.copy_((r + dw.double()).float() if acc else r.float())
             if db is not None:
                 b = dy.double().sum(0)
                 db.copy_((b + db.double()).float() if acc else b.float())
-        for job in list(co or []) + list(cjobs):   # co first: cjobs may read what it wrote
-            src, dst, acc = job[:3]
-            v = src.double() * (job[3].double()[:, None] if len(job) > 3 else 1.0)   # row weights
-            if dst.dim() == 2:   # [segs, cols]: row segment s into dst[s]
-                S, R = dst.shape[0], src.shape[0]
-                r = torch.stack([v[R * k // S:R * (k + 1) // S].sum(0) for k in range(S)])
-            else:
-                r = v.sum(0)
-            dst.copy_((r + dst.double()).float() if acc else r.float())
+        for src, dst, acc in cjobs:
+            self.colsum(src, dst, accumulate=acc)
 
     def xagg_slab_sum(self, rowptr_s, perm, ds, x, da_src, g_src):
         N = da_src.shape[0]

@@ -300,43 +300,3 @@ def test_xagg_step_pack_in_first_launch_is_bitwise(monkeypatch, n, world):
         del step, tr, model
     for (l0, g0, p0), (l1, g1, p1) in zip(res[False], res[True]):
         assert l0 == l1 and torch.equal(g0, g1) and torch.equal(p0, p1)
-
-
-def test_param_grads_grouped_concurrent_column_sums_match_float64():
-    """hicgat_param_grads_grouped_co (the single-GPU GATConv's lin_l dW with its param_grad sums in
-    the same launch): a 512 x 512 weight gradient over 20 000 rows (16 K splits) and, in blocks beside
-    its tiles, the four weighted column sums datt_src^h / datt_dst^h (weights: strided columns of
-    [N, 2] / [N, 8] arrays) and the plain column sum dbias in 32 row segments, the segments then added
-    (accumulating) by the second launch -- against float64, and the same bits on a second call."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import hicgat
-    K = hicgat.kernels.default()
-    g = torch.Generator().manual_seed(21)
-    R = 20000
-
-    def rnd(*shape):
-        return torch.randn(shape, generator=g).cuda()
-
-    dh, x, h, dout, da, rs = rnd(R, 512), rnd(R, 512), rnd(R, 512), rnd(R, 512), rnd(R, 2), rnd(R, 8)
-    W0, s0, t0, b0 = rnd(512, 512), rnd(512), rnd(512), rnd(512)
-    ref = {"W": W0.double() + dh.double().t() @ x.double(), "b": b0.double() + dout.double().sum(0)}
-    ref["s"] = s0.double() + torch.cat([(da[:, hd:hd + 1].double() * h[:, hd * 256:(hd + 1) * 256].double()).sum(0)
-                                        for hd in range(2)])
-    ref["t"] = t0.double() + torch.cat([(rs[:, 6 + hd:7 + hd].double() * h[:, hd * 256:(hd + 1) * 256].double()).sum(0)
-                                        for hd in range(2)])
-    res = []
-    for _ in range(2):
-        W, s, t, b = W0.clone(), s0.clone(), t0.clone(), b0.clone()
-        seg = torch.empty((3, 32, 512), device="cuda")
-        co = [(h[:, hd * 256:(hd + 1) * 256], seg[0, :, hd * 256:(hd + 1) * 256], False, da[:, hd]) for hd in range(2)]
-        co += [(h[:, hd * 256:(hd + 1) * 256], seg[1, :, hd * 256:(hd + 1) * 256], False, rs[:, 6 + hd])
-               for hd in range(2)]
-        co += [(dout, seg[2], False)]
-        cj = [(seg[0], s, True), (seg[1], t, True), (seg[2], b, True)]
-        K.param_grads_grouped([(dh, x, W, None, True)], cj, target_wgs=256, co=co)
-        torch.cuda.synchronize()
-        res.append({"W": W, "s": s, "t": t, "b": b})
-    errs = {k: _rel(res[0][k], ref[k]) for k in ref}
-    assert all(v < 1e-5 for v in errs.values()), errs
-    assert all(torch.equal(res[0][k], res[1][k]) for k in ref)
