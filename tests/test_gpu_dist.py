@@ -235,6 +235,69 @@ def test_sharded_single_rank_rccl_equals_autograd_step(tmp_path, mode, n, big):
     _assert_step_matches(ref, res, loss_tol=1e-6 if slab else 1e-5, grad_tol=1e-5 if slab else 1e-4, label=f"{mode} n={n}")
 
 
+_ORACLE20K = {}
+
+
+def _oracle_step1_synth20000():
+    """The CPU oracle's training step 1 on synth-20000 (oracle/gat.py, seed-0 weights, exact-formula
+    distances as the device computes them; the same construction as
+    tests/test_gpu_fullsize.py::test_synth20000_training_step_matches_oracle): loss, coordinates and
+    every parameter's gradient, computed once per module."""
+    if not _ORACLE20K:
+        from hicgat import synth
+        from oracle import gat as og
+        from oracle import graph as ogr
+        n = 20000
+        i, j, c = synth.contact_pairs(n, density=0.01, seed=0)
+        rows, cols = np.concatenate([i, j]), np.concatenate([j, i])
+        order = np.lexsort((cols, rows))
+        rows, cols = rows[order], cols[order]
+        rp = np.zeros(n + 1, dtype=np.int64)
+        np.add.at(rp, rows + 1, 1)
+        radj = (torch.tensor(np.cumsum(rp)), torch.tensor(cols.astype(np.int64)))
+        y = torch.zeros((n, n), dtype=torch.float64)
+        y[torch.tensor(i), torch.tensor(j)] = torch.tensor(c)
+        y[torch.tensor(j), torch.tensor(i)] = torch.tensor(c)
+        t_ref = ogr.cont2dist(y, 0.5).float()
+        del y
+        torch.manual_seed(0)
+        ref = og.GATNetSelectiveResidualsUpdated()
+        og.CDIST_MODE = "donot_use_mm_for_euclid_dist"
+        try:
+            c_ref = ref.get_model(torch.tensor(synth.features(n, seed=0)), radj)
+            l_ref = torch.nn.functional.mse_loss(torch.cdist(c_ref, c_ref, compute_mode=og.CDIST_MODE).float(), t_ref)
+            l_ref.backward()
+        finally:
+            og.CDIST_MODE = "use_mm_for_euclid_dist_if_necessary"
+        _ORACLE20K.update(loss=float(l_ref.item()), coords=c_ref.detach().clone(),
+                          grads={k: p.grad.detach().clone() for k, p in ref.named_parameters()})
+    return _ORACLE20K
+
+
+def _assert_step1_matches_oracle(ref, res, label=""):
+    """A sharded run's step 1 (rank 0: the all-gathered coordinates, the all-reduced flat gradient)
+    against the CPU oracle directly: loss and coordinates to the north star's 1e-5 relative, every
+    gradient to 2e-4 of its tensor's max outside the kink-decided entries of ``ref`` (bounded by
+    their flipped term, tests/kinks.py) -- the bar of the single-GPU oracle test."""
+    from kinks import compare_flat
+    o = _oracle_step1_synth20000()
+    rel_l = abs(res["loss"][0] - o["loss"]) / abs(o["loss"])
+    c, c_ref = res["coords1"].double(), o["coords"].double()
+    rel_c = float((c - c_ref).abs().max() / c_ref.abs().max())
+    model, opt = ref["model"], ref["opt"]
+    names = {id(p): k for k, p in model.named_parameters()}
+    g_ref = torch.zeros_like(ref["grad1"])
+    for p, off in zip(opt.params, opt.offsets):
+        g_ref[off:off + p.numel()] = o["grads"][names[id(p)]].reshape(-1).to(g_ref.device)
+    per = compare_flat(model, zip(opt.params, opt.offsets), g_ref, res["grad1"].to(g_ref.device), ref["masks"],
+                       bounds=ref["bounds"])
+    print(label, f"vs oracle: loss {res['loss'][0]:.9g} vs {o['loss']:.9g} (rel {rel_l:.2e}); coords rel {rel_c:.2e};",
+          {k: f"{d / m:.1e} ({n_})" for k, (d, m, n_) in per.items()})
+    assert rel_l < 1e-5 and rel_c < 1e-5, (rel_l, rel_c)
+    for k, (d, m, _) in per.items():
+        assert d <= 2e-4 * m, (label, k, d, m)
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("world,mode", [(2, "slab"), (2, "auto"), (8, "auto")])
 def test_configs3_synth20000_sharded_matches_single_gpu(tmp_path, world, mode):
@@ -244,11 +307,14 @@ def test_configs3_synth20000_sharded_matches_single_gpu(tmp_path, world, mode):
     pass) and the slab form at P = 2, gloo ranks sharing the one GPU, two training steps against
     the single-GPU step from the same seed (HiC-GNN_main.py:123-132): loss 1e-5 relative at both
     steps, every step-1 gradient to 1e-4 of its max with the kink-decided entries masked, the
-    step-1 Adam update."""
+    step-1 Adam update.  And step 1 against the CPU oracle itself (not only through the single-GPU
+    step): loss and coordinates 1e-5, gradients 2e-4 of their max."""
     res = _run(world, "gloo", 20000, tmp_path, mode)
     assert res["mode"] == ("slab" if mode == "slab" else "xagg") and len(res["rows"]) == world
     ref = _single_gpu_steps(20000)
-    _assert_step_matches(ref, res, label=f"P={world} {res['mode']} rows {res['rows']}")
+    label = f"P={world} {res['mode']} rows {res['rows']}"
+    _assert_step_matches(ref, res, label=label)
+    _assert_step1_matches_oracle(ref, res, label=label)
 
 
 @pytest.mark.parametrize("world,mode,n", [(2, "slab", 777), (2, "xagg", 777), (2, "allgather", 777), (3, "slab", 777),
